@@ -1,0 +1,109 @@
+"""ctypes binding of libdlamd.so (the C ABI declared in include/dlamd.h).
+
+This is the only door from Python into the HIP kernels.  It fails loudly: if the shared library
+is missing or was built without gfx950 code, importing a consumer raises instead of silently
+running anything on the CPU.  Tensor arguments are torch CUDA(HIP) tensors; only raw device
+pointers, sizes and the current HIP stream cross the boundary.
+"""
+import ctypes
+import os
+
+import torch  # loads torch's HIP runtime first, so libdlamd.so binds to the same one
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libdlamd.so")
+
+DL_OK, DL_ERR_INVALID, DL_ERR_WORKSPACE, DL_ERR_HIP, DL_ERR_UNSUPPORTED = 0, 1, 2, 3, 4
+
+_vp = ctypes.c_void_p
+_i32, _i64, _f32, _f64, _sz = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_double, \
+    ctypes.c_size_t
+
+
+class DlCsr(ctypes.Structure):
+    _fields_ = [("row_ptr", _vp), ("col", _vp), ("w", _vp), ("n_rows", _i32), ("nnz", _i32),
+                ("uniform_row_nnz", _i32)]
+
+
+class DlMixArgs(ctypes.Structure):
+    _fields_ = [("x", _vp), ("ldx", _i64), ("y", _vp), ("ldy", _i64), ("n_params", _i64),
+                ("W", DlCsr), ("g", _vp), ("ldg", _i64), ("lr", _f32), ("halo", _vp),
+                ("ldh", _i64), ("n_halo", _i32), ("dev_sq", _vp), ("dev_max", _vp),
+                ("mean", _vp)]
+
+
+class DlMixPlan(ctypes.Structure):
+    _fields_ = [("path", _i32), ("tile_cols", _i32), ("grid", _i32), ("lds_bytes", _i32),
+                ("n_tiles", _i32), ("regular", _i32)]
+
+
+class DlPerronArgs(ctypes.Structure):
+    _fields_ = [("dtype", _i32), ("y", _vp), ("ldy", _i64), ("n_rows", _i32), ("n_params", _i64),
+                ("row_ptr", _vp), ("col", _vp), ("weight", _vp), ("mean_weight", _f64),
+                ("eps", _f64), ("conv_eps", _f64), ("max_iter", _i32), ("iters_out", _vp)]
+
+
+# exported symbol -> (restype, argtypes); tests check every one is exported
+SIGNATURES = {
+    "dl_abi_version": (_i32, []),
+    "dl_last_error": (ctypes.c_char_p, []),
+    "dl_mix_workspace_bytes": (_sz, [_i32, _i32, _i64]),
+    "dl_mix_plan_query": (_i32, [ctypes.POINTER(DlMixArgs), ctypes.POINTER(DlMixPlan)]),
+    "dl_mix_round": (_i32, [ctypes.POINTER(DlMixArgs), _vp, _sz, _vp]),
+    "dl_deviation_workspace_bytes": (_sz, [_i32, _i64]),
+    "dl_deviation": (_i32, [_vp, _i64, _i32, _i64, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "dl_column_sum": (_i32, [_vp, _i64, _i32, _i64, _vp, _vp]),
+    "dl_max_column_std": (_i32, [_vp, _i64, _i32, _i64, _vp, _vp]),
+    "dl_step_rows": (_i32, [_vp, _i64, _vp, _i64, _f32, _vp, _i32, _i64, _vp, _i64, _vp]),
+    "dl_perron_workspace_bytes": (_sz, [_i32, _i32, _i64]),
+    "dl_perron_round": (_i32, [ctypes.POINTER(DlPerronArgs), _vp, _sz, _vp]),
+}
+
+ABI_VERSION = 1
+_lib = None
+
+
+class DlError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libdlamd.so (once).  Raises ImportError when the HIP library has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build the HIP extension first "
+            "(python -c 'import __graft_entry__ as g; g.build()'); there is no CPU fallback")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.dl_abi_version() != ABI_VERSION:
+        raise ImportError(f"libdlamd ABI {lib.dl_abi_version()} != expected {ABI_VERSION}")
+    _lib = lib
+    return lib
+
+
+def check(rc, what):
+    if rc == DL_OK:
+        return
+    msg = load().dl_last_error().decode(errors="replace")
+    if rc == DL_ERR_INVALID:
+        raise ValueError(f"{what}: {msg}")
+    raise DlError(f"{what} failed (status {rc}): {msg}")
+
+
+def ptr(t):
+    """Device pointer of a CUDA tensor (None -> NULL)."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise ValueError("libdlamd operates on device tensors; got a CPU tensor")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream_handle(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)

@@ -1,0 +1,293 @@
+// Auxiliary kernels around the mixing hot path (gfx950):
+//   column sums / means           (np.mean numerator, mixer.py:61; multi-GPU global mean)
+//   per-agent deviation rows      (mixer.py:65 against a given mean)
+//   max column std                (mixer.py:82-84 intent)
+//   boundary-row local step pack  (multi-GPU halo send buffers)
+//   Perron / asyncio Jacobi round (consensus_asyncio.py:231-310), fp32 and fp64
+#include "dl_internal.h"
+
+namespace dl {
+namespace {
+
+// sum over rows in row order (bit-identical to numpy's add.reduce over axis 0), optional /div.
+__global__ void __launch_bounds__(256) column_sum_kernel(const float *__restrict__ x, int64_t ldx,
+                                                         int n_rows, int64_t n_params,
+                                                         float *__restrict__ out, float div) {
+    const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (p >= n_params) return;
+    float s = x[p];
+    for (int r = 1; r < n_rows; ++r) s = s + x[(int64_t)r * ldx + p];
+    out[p] = div > 0.f ? s / div : s;
+}
+
+// partial[b][a] = sum over columns of block b of (x[a,p] - mean[p])^2
+__global__ void __launch_bounds__(256) dev_rows_kernel(const float *__restrict__ x, int64_t ldx,
+                                                       int n_rows, int64_t n_params,
+                                                       const float *__restrict__ mean,
+                                                       float *__restrict__ partial, int nparts) {
+    __shared__ float red[4];
+    const int ag = blockIdx.y;
+    const int64_t span = (n_params + nparts - 1) / nparts;
+    const int64_t p0 = (int64_t)blockIdx.x * span;
+    const int64_t p1 = p0 + span < n_params ? p0 + span : n_params;
+    const float *row = x + (int64_t)ag * ldx;
+    float acc = 0.f;
+    for (int64_t p = p0 + threadIdx.x; p < p1; p += 256) {
+        const float d = row[p] - mean[p];
+        acc += d * d;
+    }
+    for (int m = 32; m >= 1; m >>= 1) acc += __shfl_xor(acc, m);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0)
+        partial[(int64_t)blockIdx.x * n_rows + ag] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// numpy std(axis=0): mean = sum/N; var = sum((x-mean)^2)/N; std = sqrt(var); then max over p.
+__global__ void __launch_bounds__(256) max_column_std_kernel(const float *__restrict__ x,
+                                                             int64_t ldx, int n_rows,
+                                                             int64_t n_params,
+                                                             unsigned int *__restrict__ out_bits) {
+    __shared__ float red[4];
+    const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    float sd = 0.f;
+    if (p < n_params) {
+        float s = x[p];
+        for (int r = 1; r < n_rows; ++r) s = s + x[(int64_t)r * ldx + p];
+        const float n = (float)n_rows;
+        const float m = s / n;
+        float d0 = x[p] - m;
+        float v = d0 * d0;
+        for (int r = 1; r < n_rows; ++r) {
+            const float d = x[(int64_t)r * ldx + p] - m;
+            v = v + d * d;
+        }
+        sd = sqrtf(v / n);
+    }
+    for (int m = 32; m >= 1; m >>= 1) sd = fmaxf(sd, __shfl_xor(sd, m));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sd;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const float b = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+        atomicMax(out_bits, __float_as_uint(b));  // non-negative floats order like their bits
+    }
+}
+
+__global__ void __launch_bounds__(256) step_rows_kernel(const float *__restrict__ x, int64_t ldx,
+                                                        const float *__restrict__ g, int64_t ldg,
+                                                        float lr, const int32_t *__restrict__ rows,
+                                                        int n_sel, int64_t n_params,
+                                                        float *__restrict__ out, int64_t ldo) {
+    const int i = blockIdx.y;
+    const int r = rows[i];
+    for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < n_params;
+         p += (int64_t)gridDim.x * 256) {
+        float v = x[(int64_t)r * ldx + p];
+        if (g) v = v - lr * g[(int64_t)r * ldg + p];
+        out[(int64_t)i * ldo + p] = v;
+    }
+}
+
+// ---------------------------------------------------------------- Perron / asyncio round
+// One Jacobi iteration on element i of an [R, TP] tile held in LDS (cur), neighbour sums in
+// socket order (np.sum(list, axis=0): first term, then left fold), then scale.
+template <typename DT>
+__device__ __forceinline__ DT perron_update(const DT *cur, int r, int p, int TP,
+                                            const int32_t *__restrict__ rp,
+                                            const int32_t *__restrict__ col, double eps,
+                                            DT conv, bool &fail) {
+    const int e0 = rp[r], e1 = rp[r + 1];
+    const int cnt = e1 - e0;
+    DT s = (DT)0;
+    if (cnt > 0) {
+        s = cur[col[e0] * TP + p];
+        for (int e = e0 + 1; e < e1; ++e) s = s + cur[col[e] * TP + p];
+    }
+    const DT dcoef = (DT)(1.0 - eps * (double)cnt);
+    const DT t1 = cur[r * TP + p] * dcoef;
+    const DT t2 = (DT)eps * s;
+    const DT yn = t1 + t2;
+    for (int e = e0; e < e1; ++e) {
+        const DT v = cur[col[e] * TP + p];
+        if (!((yn - v) <= conv)) fail = true;
+    }
+    return yn;
+}
+
+template <typename DT>
+__device__ __forceinline__ DT prescale(DT v, const double *weight, double mean_w, int r) {
+    if (weight == nullptr) return v;
+    const DT t = v * (DT)weight[r];
+    return t / (DT)mean_w;
+}
+
+// All columns in one tile: the whole round (until every agent has converged) in one launch.
+template <typename DT>
+__global__ void __launch_bounds__(1024) perron_single_kernel(PerronArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int R = a.n_rows;
+    const int TP = (int)a.n_params;
+    const int E = R * TP;
+    DT *buf0 = reinterpret_cast<DT *>(smem);
+    DT *buf1 = buf0 + E;
+    int *flags = reinterpret_cast<int *>(buf1 + E);
+    DT *y = reinterpret_cast<DT *>(a.y);
+    for (int i = threadIdx.x; i < E; i += 1024) {
+        const int r = i / TP, p = i - r * TP;
+        buf0[i] = prescale<DT>(y[(int64_t)r * a.ldy + p], a.weight, a.mean_weight, r);
+    }
+    if (threadIdx.x < 2) flags[threadIdx.x] = 0;
+    __syncthreads();
+    const DT conv = (DT)a.conv_eps;
+    DT *cur = buf0, *nxt = buf1;
+    int it = 0;
+    while (it < a.max_iter) {
+        ++it;
+        bool fail = false;
+        for (int i = threadIdx.x; i < E; i += 1024) {
+            const int r = i / TP, p = i - r * TP;
+            nxt[i] = perron_update<DT>(cur, r, p, TP, a.rowptr, a.col, a.eps, conv, fail);
+        }
+        if (__any(fail) && (threadIdx.x & 63) == 0) atomicOr(&flags[it & 1], 1);
+        __syncthreads();
+        DT *t = cur;
+        cur = nxt;
+        nxt = t;
+        const bool done = flags[it & 1] == 0;
+        if (threadIdx.x == 0) flags[(it + 1) & 1] = 0;  // next iteration's flag; read after barrier
+        __syncthreads();
+        if (done) break;
+    }
+    for (int i = threadIdx.x; i < E; i += 1024) {
+        const int r = i / TP, p = i - r * TP;
+        y[(int64_t)r * a.ldy + p] = cur[i];
+    }
+    if (threadIdx.x == 0) a.iters_out[0] = it;
+}
+
+// Column tile of TP columns: one iteration, global in -> global out, global not-converged flag.
+template <typename DT>
+__global__ void __launch_bounds__(1024) perron_step_kernel(PerronArgs a, int TP, const DT *yin,
+                                                           int64_t ldin, DT *yout, int64_t ldout,
+                                                           int do_prescale) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int R = a.n_rows;
+    const int64_t p0 = (int64_t)blockIdx.x * TP;
+    const int64_t P = a.n_params;
+    DT *cur = reinterpret_cast<DT *>(smem);
+    const int E = R * TP;
+    for (int i = threadIdx.x; i < E; i += 1024) {
+        const int r = i / TP, p = i - r * TP;
+        DT v = (DT)0;
+        if (p0 + p < P) {
+            v = yin[(int64_t)r * ldin + p0 + p];
+            if (do_prescale) v = prescale<DT>(v, a.weight, a.mean_weight, r);
+        }
+        cur[i] = v;
+    }
+    __syncthreads();
+    const DT conv = (DT)a.conv_eps;
+    bool fail = false;
+    for (int i = threadIdx.x; i < E; i += 1024) {
+        const int r = i / TP, p = i - r * TP;
+        if (p0 + p >= P) continue;
+        bool f = false;
+        const DT yn = perron_update<DT>(cur, r, p, TP, a.rowptr, a.col, a.eps, conv, f);
+        fail |= f;
+        yout[(int64_t)r * ldout + p0 + p] = yn;
+    }
+    if (__any(fail) && (threadIdx.x & 63) == 0) atomicOr(a.notconv, 1);
+}
+
+}  // namespace
+
+int dev_rows_parts(int64_t n_params) {
+    int64_t parts = (n_params + 8191) / 8192;
+    if (parts < 1) parts = 1;
+    if (parts > 256) parts = 256;
+    return (int)parts;
+}
+
+hipError_t launch_column_sum(const float *x, int64_t ldx, int n_rows, int64_t n_params,
+                             float *colsum, float div, hipStream_t s) {
+    hipLaunchKernelGGL(column_sum_kernel, dim3((unsigned)((n_params + 255) / 256)), dim3(256), 0,
+                       s, x, ldx, n_rows, n_params, colsum, div);
+    return hipGetLastError();
+}
+
+hipError_t launch_dev_rows(const float *x, int64_t ldx, int n_rows, int64_t n_params,
+                           const float *mean, float *partial, int nparts, hipStream_t s) {
+    hipLaunchKernelGGL(dev_rows_kernel, dim3(nparts, n_rows), dim3(256), 0, s, x, ldx, n_rows,
+                       n_params, mean, partial, nparts);
+    return hipGetLastError();
+}
+
+hipError_t launch_max_column_std(const float *x, int64_t ldx, int n_rows, int64_t n_params,
+                                 float *out, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(out, 0, sizeof(float), s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(max_column_std_kernel, dim3((unsigned)((n_params + 255) / 256)), dim3(256),
+                       0, s, x, ldx, n_rows, n_params, reinterpret_cast<unsigned int *>(out));
+    return hipGetLastError();
+}
+
+hipError_t launch_step_rows(const float *x, int64_t ldx, const float *g, int64_t ldg, float lr,
+                            const int32_t *rows, int n_sel, int64_t n_params, float *out,
+                            int64_t ldo, hipStream_t s) {
+    int64_t bx = (n_params + 255) / 256;
+    if (bx > 1024) bx = 1024;
+    hipLaunchKernelGGL(step_rows_kernel, dim3((unsigned)bx, n_sel), dim3(256), 0, s, x, ldx, g,
+                       ldg, lr, rows, n_sel, n_params, out, ldo);
+    return hipGetLastError();
+}
+
+int perron_tile_cols(int dtype, int n_rows, int64_t n_params) {
+    const int64_t sz = dtype == 1 ? 8 : 4;
+    if (2 * (int64_t)n_rows * n_params * sz + 16 <= kLdsBytes) return (int)n_params;  // single
+    int64_t tp = (kLdsBytes - 16) / ((int64_t)n_rows * sz);
+    if (tp > 1024) tp = 1024;
+    return (int)(tp < 1 ? 0 : tp);
+}
+
+hipError_t launch_perron_single(const PerronArgs &a, int dtype, int tile_cols, hipStream_t s) {
+    const int64_t sz = dtype == 1 ? 8 : 4;
+    const int lds = (int)(2 * (int64_t)a.n_rows * tile_cols * sz + 16);
+    const void *k = dtype == 1 ? reinterpret_cast<const void *>(perron_single_kernel<double>)
+                               : reinterpret_cast<const void *>(perron_single_kernel<float>);
+    hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (e != hipSuccess) return e;
+    if (dtype == 1)
+        hipLaunchKernelGGL(perron_single_kernel<double>, dim3(1), dim3(1024), lds, s, a);
+    else
+        hipLaunchKernelGGL(perron_single_kernel<float>, dim3(1), dim3(1024), lds, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_perron_step(const PerronArgs &a, int dtype, int tile_cols, const void *yin,
+                              void *yout, bool do_prescale, hipStream_t s) {
+    const int64_t sz = dtype == 1 ? 8 : 4;
+    const int lds = (int)((int64_t)a.n_rows * tile_cols * sz);
+    const unsigned grid = (unsigned)((a.n_params + tile_cols - 1) / tile_cols);
+    const int64_t ldin = yin == a.y ? a.ldy : a.n_params;
+    const int64_t ldout = yout == a.y ? a.ldy : a.n_params;
+    if (dtype == 1) {
+        auto k = perron_step_kernel<double>;
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k, dim3(grid), dim3(1024), lds, s, a, tile_cols,
+                           static_cast<const double *>(yin), ldin, static_cast<double *>(yout),
+                           ldout, (int)do_prescale);
+    } else {
+        auto k = perron_step_kernel<float>;
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k, dim3(grid), dim3(1024), lds, s, a, tile_cols,
+                           static_cast<const float *>(yin), ldin, static_cast<float *>(yout),
+                           ldout, (int)do_prescale);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace dl

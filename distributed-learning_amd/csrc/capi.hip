@@ -1,0 +1,495 @@
+// C ABI of libdlamd.so (include/dlamd.h): argument validation, kernel-configuration planning,
+// workspace carving and error reporting.  No exceptions cross this boundary; every entry point
+// returns a dl_status and leaves a thread-local message for dl_last_error().
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+
+#include "../../include/dlamd.h"
+#include "dl_internal.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char *where) {
+    return fail(DL_ERR_HIP, "%s: %s (%d)", where, hipGetErrorString(e), (int)e);
+}
+
+// Compute units of the current device (cached per device ordinal).
+int device_cus() {
+    static std::mutex mu;
+    static int cache[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    std::lock_guard<std::mutex> lock(mu);
+    if (cache[dev] == 0) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            n <= 0)
+            n = 256;
+        cache[dev] = n;
+    }
+    return cache[dev];
+}
+
+constexpr size_t kAlign = 256;
+size_t align_up(size_t v) { return (v + kAlign - 1) & ~(kAlign - 1); }
+bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+// Upper bound of per-workgroup partial rows any path writes.
+int max_parts() {
+    int p = 2 * device_cus();
+    return p < 256 ? 256 : p;
+}
+
+bool overlaps(const void *a, size_t an, const void *b, size_t bn) {
+    const char *x = static_cast<const char *>(a), *y = static_cast<const char *>(b);
+    return x < y + bn && y < x + an;
+}
+
+struct Plan {
+    dl_mix_plan pub;
+    int chunks;
+    bool dev;
+};
+
+int next_pow2_chunks(int64_t n_params) {
+    int64_t need = (n_params + 3) / 4;
+    int c = 1;
+    while (c < dl::kMaxChunks && c < need) c <<= 1;
+    return c;
+}
+
+// Pick the kernel configuration for a mix round.
+int plan_mix(const dl_mix_args *a, Plan *pl) {
+    std::memset(pl, 0, sizeof *pl);
+    const int32_t R = a->W.n_rows + a->n_halo;
+    const int32_t nnz = a->W.nnz;
+    const bool want_dev = a->dev_sq || a->dev_max || a->mean;
+    pl->dev = want_dev;
+    const int reg = a->W.uniform_row_nnz > 0 ? 1 : 0;
+    const uint32_t csr = dl::csr_lds_bytes(a->W.n_rows, nnz, reg);
+    const int cmax = next_pow2_chunks(a->n_params);
+    // DLAMD_FORCE_GATHER=1 (tests only) forces the general gather kernel
+    const char *force = getenv("DLAMD_FORCE_GATHER");
+    const bool force_gather = force && force[0] == '1';
+    if (csr > 0 && R <= 65535 && !force_gather) {
+        for (int c = cmax; c >= 1; c >>= 1) {
+            if ((int64_t)R * c > (int64_t)dl::kRowsPerThread * dl::kTileThreads) continue;
+            int64_t tile = (int64_t)R * c * 16;
+            const int64_t scratch = want_dev ? (int64_t)(dl::kTileThreads / 64) * c * 16 : 0;
+            if (tile < scratch) tile = scratch;
+            const int64_t lds = tile + csr;
+            if (lds > dl::kLdsBytes) continue;
+            const int64_t T = 4 * c;
+            const int64_t n_tiles = (a->n_params + T - 1) / T;
+            if (n_tiles > 0x7fffffff) continue;
+            int bpc = (int)(dl::kLdsBytes / lds);
+            if (bpc > 2) bpc = 2;  // 1024-thread workgroups: at most 2 per CU (32 waves)
+            int64_t grid = (int64_t)device_cus() * bpc;
+            if (grid > n_tiles) grid = n_tiles;
+            pl->pub.path = 1;
+            pl->pub.tile_cols = (int32_t)T;
+            pl->pub.grid = (int32_t)grid;
+            pl->pub.lds_bytes = (int32_t)lds;
+            pl->pub.n_tiles = (int32_t)n_tiles;
+            pl->pub.regular = reg;
+            pl->chunks = c;
+            return DL_OK;
+        }
+    }
+    if (a->W.n_rows > 4 * 65535)
+        return fail(DL_ERR_UNSUPPORTED, "dl_mix_round: %d rows exceed the gather path limit",
+                    a->W.n_rows);
+    pl->pub.path = 2;
+    pl->pub.grid = (int32_t)(((a->n_params + 255) / 256) * ((a->W.n_rows + 3) / 4));
+    pl->pub.regular = reg;
+    return DL_OK;
+}
+
+int check_mix_args(const dl_mix_args *a) {
+    if (!a) return fail(DL_ERR_INVALID, "dl_mix_round: args is NULL");
+    const dl_csr &W = a->W;
+    if (W.n_rows <= 0) return fail(DL_ERR_INVALID, "dl_mix_round: n_rows must be > 0 (got %d)", W.n_rows);
+    if (a->n_params <= 0) return fail(DL_ERR_INVALID, "dl_mix_round: n_params must be > 0");
+    if (a->n_halo < 0) return fail(DL_ERR_INVALID, "dl_mix_round: n_halo < 0");
+    if (W.nnz < 0) return fail(DL_ERR_INVALID, "dl_mix_round: nnz < 0");
+    if (!a->x || !a->y || !W.row_ptr || (W.nnz > 0 && (!W.col || !W.w)))
+        return fail(DL_ERR_INVALID, "dl_mix_round: null x/y/row_ptr/col/w");
+    if (a->ldx < a->n_params || a->ldy < a->n_params)
+        return fail(DL_ERR_INVALID, "dl_mix_round: ldx/ldy smaller than n_params");
+    if (a->g && a->ldg < a->n_params) return fail(DL_ERR_INVALID, "dl_mix_round: ldg < n_params");
+    if (a->n_halo > 0 && (!a->halo || a->ldh < a->n_params))
+        return fail(DL_ERR_INVALID, "dl_mix_round: n_halo > 0 needs halo with ldh >= n_params");
+    if (W.uniform_row_nnz < 0 ||
+        (W.uniform_row_nnz > 0 && (int64_t)W.uniform_row_nnz * W.n_rows != W.nnz))
+        return fail(DL_ERR_INVALID, "dl_mix_round: uniform_row_nnz * n_rows != nnz");
+    if ((a->dev_sq || a->dev_max || a->mean) && a->n_halo > 0)
+        return fail(DL_ERR_INVALID,
+                    "dl_mix_round: fused deviation needs every agent local (n_halo == 0); use "
+                    "dl_column_sum + dl_deviation with a global mean");
+    const size_t xb = ((size_t)(W.n_rows - 1) * a->ldx + a->n_params) * 4;
+    const size_t yb = ((size_t)(W.n_rows - 1) * a->ldy + a->n_params) * 4;
+    if (overlaps(a->x, xb, a->y, yb)) return fail(DL_ERR_INVALID, "dl_mix_round: y overlaps x");
+    if (a->g) {
+        const size_t gb = ((size_t)(W.n_rows - 1) * a->ldg + a->n_params) * 4;
+        if (overlaps(a->g, gb, a->y, yb)) return fail(DL_ERR_INVALID, "dl_mix_round: y overlaps g");
+    }
+    return DL_OK;
+}
+
+dl::TileArgs tile_args(const dl_mix_args *a) {
+    dl::TileArgs t{};
+    t.x = a->x;
+    t.ldx = a->ldx;
+    t.halo = a->halo;
+    t.ldh = a->ldh;
+    t.g = a->g;
+    t.ldg = a->ldg;
+    t.y = a->y;
+    t.ldy = a->ldy;
+    t.rowptr = a->W.row_ptr;
+    t.col = a->W.col;
+    t.w = a->W.w;
+    t.n_rows = a->W.n_rows;
+    t.n_src = a->W.n_rows + a->n_halo;
+    t.nnz = a->W.nnz;
+    t.regular = a->W.uniform_row_nnz;
+    t.n_params = a->n_params;
+    t.lr = a->lr;
+    bool vec = aligned16(a->x) && aligned16(a->y) && a->ldx % 4 == 0 && a->ldy % 4 == 0;
+    if (a->g) vec = vec && aligned16(a->g) && a->ldg % 4 == 0;
+    if (a->halo) vec = vec && aligned16(a->halo) && a->ldh % 4 == 0;
+    if (a->mean) vec = vec && aligned16(a->mean);
+    // the float4 kernel addresses rows with 32-bit byte offsets from the tile base
+    const int64_t lim = (int64_t)1 << 32;
+    const int64_t R = a->W.n_rows;
+    if ((R * a->ldx + 128) * 4 >= lim || (R * a->ldy + 128) * 4 >= lim ||
+        (a->g && (R * a->ldg + 128) * 4 >= lim))
+        vec = false;
+    t.vec = vec ? 1 : 0;
+    t.mean = a->mean;
+    return t;
+}
+
+// Deviation of x (n_rows x n_params) via the two-pass path: mean (given or column mean), then
+// per-row partial sums, then the fixed-order reduce.
+int deviation_two_pass(const float *x, int64_t ldx, int32_t n_rows, int64_t n_params,
+                       const float *mean_in, float *dev_sq, float *dev_max, float *mean_out,
+                       char *ws, size_t ws_bytes, hipStream_t s) {
+    const int parts = dl::dev_rows_parts(n_params);
+    const size_t part_b = align_up((size_t)parts * n_rows * 4);
+    const size_t mean_b = align_up((size_t)n_params * 4);
+    if (ws_bytes < part_b + mean_b) return fail(DL_ERR_WORKSPACE, "deviation: workspace too small");
+    float *partial = reinterpret_cast<float *>(ws);
+    const float *mean = mean_in;
+    if (!mean) {
+        float *m = mean_out ? mean_out : reinterpret_cast<float *>(ws + part_b);
+        hipError_t e = dl::launch_column_sum(x, ldx, n_rows, n_params, m, (float)n_rows, s);
+        if (e != hipSuccess) return hip_fail(e, "column_sum");
+        mean = m;
+    } else if (mean_out && mean_out != mean_in) {
+        hipError_t e = hipMemcpyAsync(mean_out, mean_in, (size_t)n_params * 4,
+                                      hipMemcpyDeviceToDevice, s);
+        if (e != hipSuccess) return hip_fail(e, "mean copy");
+    }
+    hipError_t e = dl::launch_dev_rows(x, ldx, n_rows, n_params, mean, partial, parts, s);
+    if (e != hipSuccess) return hip_fail(e, "dev_rows");
+    e = dl::launch_dev_reduce(partial, parts, n_rows, dev_sq, dev_max, s);
+    if (e != hipSuccess) return hip_fail(e, "dev_reduce");
+    return DL_OK;
+}
+
+int zero_deviation(int32_t n_rows, float *dev_sq, float *dev_max, hipStream_t s) {
+    if (dev_sq) {
+        hipError_t e = hipMemsetAsync(dev_sq, 0, (size_t)n_rows * 4, s);
+        if (e != hipSuccess) return hip_fail(e, "memset dev_sq");
+    }
+    if (dev_max) {
+        hipError_t e = hipMemsetAsync(dev_max, 0, 4, s);
+        if (e != hipSuccess) return hip_fail(e, "memset dev_max");
+    }
+    return DL_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dl_abi_version(void) { return DLAMD_ABI_VERSION; }
+
+const char *dl_last_error(void) { return g_err.c_str(); }
+
+size_t dl_mix_workspace_bytes(int32_t n_rows, int32_t n_halo, int64_t n_params) {
+    (void)n_halo;
+    if (n_rows < 0 || n_params < 0) return 0;
+    return align_up((size_t)max_parts() * (size_t)n_rows * 4) + align_up((size_t)n_params * 4) +
+           kAlign;
+}
+
+int dl_mix_plan_query(const dl_mix_args *args, dl_mix_plan *plan) {
+    g_err.clear();
+    int rc = check_mix_args(args);
+    if (rc) return rc;
+    if (!plan) return fail(DL_ERR_INVALID, "dl_mix_plan_query: plan is NULL");
+    Plan pl;
+    rc = plan_mix(args, &pl);
+    if (rc) return rc;
+    *plan = pl.pub;
+    return DL_OK;
+}
+
+int dl_mix_round(const dl_mix_args *args, void *workspace, size_t ws_bytes, dl_stream_t stream) {
+    g_err.clear();
+    int rc = check_mix_args(args);
+    if (rc) return rc;
+    Plan pl;
+    rc = plan_mix(args, &pl);
+    if (rc) return rc;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int32_t Nr = args->W.n_rows;
+    char *ws = static_cast<char *>(workspace);
+    if (pl.dev && (!ws || (reinterpret_cast<uintptr_t>(ws) & 15u)))
+        return fail(DL_ERR_WORKSPACE, "dl_mix_round: deviation outputs need a 16-byte aligned "
+                                      "workspace of dl_mix_workspace_bytes()");
+    dl::TileArgs t = tile_args(args);
+    const bool sgd = args->g != nullptr;
+    if (pl.pub.path == 1) {
+        // full tiles on the branch-free float4 kernel, the ragged tail tile (and unaligned
+        // operands) on the guarded one; each launch writes its own deviation partial rows
+        const int64_t T = pl.pub.tile_cols;
+        const int64_t n_full = t.vec ? args->n_params / T : 0;
+        const int64_t n_tail = pl.pub.n_tiles - n_full;  // 0 or 1 when vec, else all tiles
+        int grid_full = (int)(n_full < pl.pub.grid ? n_full : pl.pub.grid);
+        int grid_tail = (int)(n_tail < pl.pub.grid ? n_tail : pl.pub.grid);
+        const size_t need = align_up((size_t)(grid_full + grid_tail) * Nr * 4);
+        if (pl.dev && ws_bytes < need)
+            return fail(DL_ERR_WORKSPACE, "dl_mix_round: workspace %zu < %zu bytes", ws_bytes, need);
+        t.csr_off = (uint32_t)(pl.pub.lds_bytes - (int)dl::csr_lds_bytes(Nr, t.nnz, t.regular > 0));
+        float *partial = pl.dev ? reinterpret_cast<float *>(ws) : nullptr;
+        if (grid_full > 0) {
+            t.n_tiles = (int32_t)n_full;
+            t.col_base = 0;
+            t.dev_partial = partial;
+            hipError_t e = dl::launch_mix_tile(t, pl.chunks, sgd, pl.dev, true, grid_full,
+                                               pl.pub.lds_bytes, true, s);
+            if (e != hipSuccess) return hip_fail(e, "mix_tile_kernel launch");
+        }
+        if (grid_tail > 0) {
+            t.n_tiles = (int32_t)n_tail;
+            t.col_base = n_full * T;
+            t.dev_partial = pl.dev ? partial + (size_t)grid_full * Nr : nullptr;
+            hipError_t e = dl::launch_mix_tile(t, pl.chunks, sgd, pl.dev, true, grid_tail,
+                                               pl.pub.lds_bytes, false, s);
+            if (e != hipSuccess) return hip_fail(e, "mix_tile_kernel (tail) launch");
+        }
+        if (pl.dev) {
+            if (Nr <= 1) return zero_deviation(Nr, args->dev_sq, args->dev_max, s);
+            hipError_t e = dl::launch_dev_reduce(partial, grid_full + grid_tail, Nr, args->dev_sq,
+                                                 args->dev_max, s);
+            if (e != hipSuccess) return hip_fail(e, "dev_reduce launch");
+        }
+        return DL_OK;
+    }
+    hipError_t e = dl::launch_mix_gather(t, sgd, s);
+    if (e != hipSuccess) return hip_fail(e, "mix_gather_kernel launch");
+    if (pl.dev) {
+        if (Nr <= 1) return zero_deviation(Nr, args->dev_sq, args->dev_max, s);
+        return deviation_two_pass(args->y, args->ldy, Nr, args->n_params, nullptr, args->dev_sq,
+                                  args->dev_max, args->mean, ws, ws_bytes, s);
+    }
+    return DL_OK;
+}
+
+size_t dl_deviation_workspace_bytes(int32_t n_rows, int64_t n_params) {
+    return dl_mix_workspace_bytes(n_rows, 0, n_params);
+}
+
+int dl_deviation(const float *x, int64_t ldx, int32_t n_rows, int64_t n_params,
+                 const float *mean_in, float *dev_sq, float *dev_max, float *mean_out,
+                 void *workspace, size_t ws_bytes, dl_stream_t stream) {
+    g_err.clear();
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (!x || n_rows <= 0 || n_params <= 0 || ldx < n_params)
+        return fail(DL_ERR_INVALID, "dl_deviation: bad x/n_rows/n_params/ldx");
+    char *ws = static_cast<char *>(workspace);
+    if (!ws || (reinterpret_cast<uintptr_t>(ws) & 15u))
+        return fail(DL_ERR_WORKSPACE, "dl_deviation: needs a 16-byte aligned workspace");
+    if (n_rows <= 1) {
+        if (mean_out) {
+            hipError_t e = mean_in ? hipMemcpyAsync(mean_out, mean_in, (size_t)n_params * 4,
+                                                    hipMemcpyDeviceToDevice, s)
+                                   : hipMemcpy2DAsync(mean_out, (size_t)n_params * 4, x,
+                                                      (size_t)ldx * 4, (size_t)n_params * 4, 1,
+                                                      hipMemcpyDeviceToDevice, s);
+            if (e != hipSuccess) return hip_fail(e, "dl_deviation mean copy");
+        }
+        return zero_deviation(n_rows, dev_sq, dev_max, s);
+    }
+    if (!mean_in) {
+        // one pass: every agent of a column tile in one workgroup (registers + LDS scratch)
+        const int cmax = next_pow2_chunks(n_params);
+        for (int c = cmax; c >= 1; c >>= 1) {
+            if ((int64_t)n_rows * c > (int64_t)dl::kRowsPerThread * dl::kTileThreads) continue;
+            const int lds = (dl::kTileThreads / 64) * c * 16;
+            const int64_t T = 4 * c;
+            const bool vec = aligned16(x) && ldx % 4 == 0 && (!mean_out || aligned16(mean_out)) &&
+                             ((int64_t)n_rows * ldx + 128) * 4 < ((int64_t)1 << 32);
+            const int64_t n_tiles = (n_params + T - 1) / T;
+            const int64_t n_full = vec ? n_params / T : 0;
+            const int64_t n_tail = n_tiles - n_full;
+            const int64_t gmax = (int64_t)device_cus() * 2;
+            const int grid_full = (int)(n_full < gmax ? n_full : gmax);
+            const int grid_tail = (int)(n_tail < gmax ? n_tail : gmax);
+            if (ws_bytes < align_up((size_t)(grid_full + grid_tail) * n_rows * 4))
+                return fail(DL_ERR_WORKSPACE, "dl_deviation: workspace too small");
+            dl::TileArgs t{};
+            t.x = x;
+            t.ldx = ldx;
+            t.n_rows = n_rows;
+            t.n_src = n_rows;
+            t.n_params = n_params;
+            t.vec = vec ? 1 : 0;
+            t.mean = mean_out;
+            float *partial = reinterpret_cast<float *>(ws);
+            if (grid_full > 0) {
+                t.n_tiles = (int32_t)n_full;
+                t.col_base = 0;
+                t.dev_partial = partial;
+                hipError_t e = dl::launch_mix_tile(t, c, false, true, false, grid_full, lds, true, s);
+                if (e != hipSuccess) return hip_fail(e, "dev tile launch");
+            }
+            if (grid_tail > 0) {
+                t.n_tiles = (int32_t)n_tail;
+                t.col_base = n_full * T;
+                t.dev_partial = partial + (size_t)grid_full * n_rows;
+                hipError_t e = dl::launch_mix_tile(t, c, false, true, false, grid_tail, lds, false, s);
+                if (e != hipSuccess) return hip_fail(e, "dev tile (tail) launch");
+            }
+            hipError_t e = dl::launch_dev_reduce(partial, grid_full + grid_tail, n_rows, dev_sq,
+                                                 dev_max, s);
+            if (e != hipSuccess) return hip_fail(e, "dev_reduce launch");
+            return DL_OK;
+        }
+    }
+    return deviation_two_pass(x, ldx, n_rows, n_params, mean_in, dev_sq, dev_max, mean_out, ws,
+                              ws_bytes, s);
+}
+
+int dl_column_sum(const float *x, int64_t ldx, int32_t n_rows, int64_t n_params, float *colsum,
+                  dl_stream_t stream) {
+    g_err.clear();
+    if (!x || !colsum || n_rows <= 0 || n_params <= 0 || ldx < n_params)
+        return fail(DL_ERR_INVALID, "dl_column_sum: bad arguments");
+    hipError_t e = dl::launch_column_sum(x, ldx, n_rows, n_params, colsum, 0.f,
+                                         static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? DL_OK : hip_fail(e, "column_sum launch");
+}
+
+int dl_max_column_std(const float *x, int64_t ldx, int32_t n_rows, int64_t n_params, float *out,
+                      dl_stream_t stream) {
+    g_err.clear();
+    if (!x || !out || n_rows <= 0 || n_params <= 0 || ldx < n_params)
+        return fail(DL_ERR_INVALID, "dl_max_column_std: bad arguments");
+    hipError_t e = dl::launch_max_column_std(x, ldx, n_rows, n_params, out,
+                                             static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? DL_OK : hip_fail(e, "max_column_std launch");
+}
+
+int dl_step_rows(const float *x, int64_t ldx, const float *g, int64_t ldg, float lr,
+                 const int32_t *rows, int32_t n_sel, int64_t n_params, float *out, int64_t ldo,
+                 dl_stream_t stream) {
+    g_err.clear();
+    if (n_sel == 0) return DL_OK;
+    if (!x || !rows || !out || n_sel < 0 || n_sel > 65535 || n_params <= 0 || ldx < n_params ||
+        ldo < n_params || (g && ldg < n_params))
+        return fail(DL_ERR_INVALID, "dl_step_rows: bad arguments");
+    hipError_t e = dl::launch_step_rows(x, ldx, g, ldg, lr, rows, n_sel, n_params, out, ldo,
+                                        static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? DL_OK : hip_fail(e, "step_rows launch");
+}
+
+size_t dl_perron_workspace_bytes(int32_t dtype, int32_t n_rows, int64_t n_params) {
+    const size_t sz = dtype == 1 ? 8 : 4;
+    return align_up((size_t)n_rows * (size_t)n_params * sz) + kAlign;
+}
+
+int dl_perron_round(const dl_perron_args *a, void *workspace, size_t ws_bytes,
+                    dl_stream_t stream) {
+    g_err.clear();
+    if (!a) return fail(DL_ERR_INVALID, "dl_perron_round: args is NULL");
+    if (a->dtype != 0 && a->dtype != 1) return fail(DL_ERR_INVALID, "dl_perron_round: dtype");
+    if (!a->y || !a->row_ptr || !a->iters_out || a->n_rows <= 0 || a->n_params <= 0 ||
+        a->ldy < a->n_params || a->max_iter < 1)
+        return fail(DL_ERR_INVALID, "dl_perron_round: bad arguments");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int tp = dl::perron_tile_cols(a->dtype, a->n_rows, a->n_params);
+    if (tp <= 0)
+        return fail(DL_ERR_UNSUPPORTED, "dl_perron_round: %d rows do not fit one LDS column",
+                    a->n_rows);
+    dl::PerronArgs p{};
+    p.y = a->y;
+    p.ldy = a->ldy;
+    p.n_rows = a->n_rows;
+    p.n_params = a->n_params;
+    p.rowptr = a->row_ptr;
+    p.col = a->col;
+    p.weight = a->weight;
+    p.mean_weight = a->mean_weight;
+    p.eps = a->eps;
+    p.conv_eps = a->conv_eps;
+    p.max_iter = a->max_iter;
+    p.iters_out = a->iters_out;
+    if (tp == a->n_params) {
+        hipError_t e = dl::launch_perron_single(p, a->dtype, tp, s);
+        return e == hipSuccess ? DL_OK : hip_fail(e, "perron_single launch");
+    }
+    // multi-tile: one launch per iteration, host checks the not-converged flag (synchronises)
+    const size_t sz = a->dtype == 1 ? 8 : 4;
+    const size_t buf_b = align_up((size_t)a->n_rows * a->n_params * sz);
+    if (!workspace || ws_bytes < buf_b + kAlign)
+        return fail(DL_ERR_WORKSPACE, "dl_perron_round: workspace too small");
+    char *ws = static_cast<char *>(workspace);
+    p.ybuf = ws;
+    p.notconv = reinterpret_cast<int32_t *>(ws + buf_b);
+    void *bufs[2] = {a->y, p.ybuf};
+    int it = 0, cur = 0;
+    int32_t host_flag = 1;
+    while (it < a->max_iter) {
+        ++it;
+        hipError_t e = hipMemsetAsync(p.notconv, 0, 4, s);
+        if (e != hipSuccess) return hip_fail(e, "perron flag memset");
+        e = dl::launch_perron_step(p, a->dtype, tp, bufs[cur], bufs[cur ^ 1], it == 1, s);
+        if (e != hipSuccess) return hip_fail(e, "perron_step launch");
+        cur ^= 1;
+        e = hipMemcpyAsync(&host_flag, p.notconv, 4, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return hip_fail(e, "perron flag readback");
+        if (host_flag == 0) break;
+    }
+    if (cur == 1) {
+        hipError_t e = hipMemcpy2DAsync(a->y, (size_t)a->ldy * sz, p.ybuf, (size_t)a->n_params * sz,
+                                        (size_t)a->n_params * sz, a->n_rows,
+                                        hipMemcpyDeviceToDevice, s);
+        if (e != hipSuccess) return hip_fail(e, "perron copy-back");
+    }
+    hipError_t e = hipMemcpyAsync(a->iters_out, &it, 4, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    return e == hipSuccess ? DL_OK : hip_fail(e, "perron iters write");
+}
+
+}  // extern "C"

@@ -1,0 +1,79 @@
+// Internal launcher interface between the C ABI (capi.hip) and the kernel files.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dl {
+
+constexpr int kTileThreads = 1024;      // 16 waves: one workgroup per CU owns a column tile
+constexpr int kRowsPerThread = 8;       // prefetch depth: rows x chunks <= 8 * 1024 float4
+constexpr int kLdsBytes = 163840;       // 160 KiB LDS per CU on gfx950
+constexpr int kMaxChunks = 32;          // T <= 128 columns per tile
+
+struct TileArgs {
+    const float *x;
+    int64_t ldx;
+    const float *halo;
+    int64_t ldh;
+    const float *g;
+    int64_t ldg;
+    float *y;
+    int64_t ldy;
+    const int32_t *rowptr;
+    const int32_t *col;
+    const float *w;
+    int32_t n_rows;   // output rows (local agents)
+    int32_t n_src;    // rows staged in LDS = n_rows + n_halo
+    int32_t nnz;
+    int32_t regular;  // >0: every row has exactly `regular` entries (row_ptr not staged)
+    int64_t n_params;
+    int32_t n_tiles;
+    int64_t col_base; // first column of tile 0
+    float lr;
+    int32_t vec;      // 1: x/g/y/halo 16-byte aligned and ld % 4 == 0
+    uint32_t csr_off; // byte offset of the staged CSR in LDS
+    float *dev_partial;  // [gridDim.x][n_rows] per-workgroup partial ||y_a - mean||^2
+    float *mean;         // [n_params] nullable
+};
+
+// LDS bytes the staged CSR needs (0 if it cannot be staged: > 65535 rows/entries).
+uint32_t csr_lds_bytes(int32_t n_rows, int32_t nnz, int32_t regular);
+
+hipError_t launch_mix_tile(const TileArgs &a, int chunks, bool sgd, bool dev, bool mix, int grid,
+                           int lds_bytes, bool fast, hipStream_t s);
+hipError_t launch_mix_gather(const TileArgs &a, bool sgd, hipStream_t s);
+hipError_t launch_dev_reduce(const float *partial, int nparts, int n_rows, float *dev_sq,
+                             float *dev_max, hipStream_t s);
+hipError_t launch_column_sum(const float *x, int64_t ldx, int n_rows, int64_t n_params,
+                             float *colsum, float scale, hipStream_t s);
+hipError_t launch_dev_rows(const float *x, int64_t ldx, int n_rows, int64_t n_params,
+                           const float *mean, float *partial, int nparts, hipStream_t s);
+int dev_rows_parts(int64_t n_params);
+hipError_t launch_max_column_std(const float *x, int64_t ldx, int n_rows, int64_t n_params,
+                                 float *out, hipStream_t s);
+hipError_t launch_step_rows(const float *x, int64_t ldx, const float *g, int64_t ldg, float lr,
+                            const int32_t *rows, int n_sel, int64_t n_params, float *out,
+                            int64_t ldo, hipStream_t s);
+
+struct PerronArgs {
+    void *y;
+    int64_t ldy;
+    void *ybuf;       // workspace ping-pong buffer [n_rows, n_params] (multi-tile only)
+    int32_t n_rows;
+    int64_t n_params;
+    const int32_t *rowptr;
+    const int32_t *col;
+    const double *weight;
+    double mean_weight;
+    double eps;
+    double conv_eps;
+    int32_t max_iter;
+    int32_t *iters_out;
+    int32_t *notconv;  // workspace flag (multi-tile)
+};
+int perron_tile_cols(int dtype, int n_rows, int64_t n_params);
+hipError_t launch_perron_single(const PerronArgs &a, int dtype, int tile_cols, hipStream_t s);
+hipError_t launch_perron_step(const PerronArgs &a, int dtype, int tile_cols, const void *yin,
+                              void *yout, bool prescale, hipStream_t s);
+
+}  // namespace dl

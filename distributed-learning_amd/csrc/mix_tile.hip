@@ -1,0 +1,393 @@
+// Fused gossip-mixing kernels for gfx950 (MI355X).
+//
+// Hot path: one consensus round X' = W (X - lr G) over a sparse agent graph, plus the
+// disagreement ||x'_a - mean(x')|| -- the work of Mixer._mix_params_once and
+// Mixer._get_deviation_dict (utils/consensus_simple/mixer.py:43-66) after a local step.
+//
+// Design: the mix is column-independent, so a workgroup owns a column tile of
+// T = 4*C floats for ALL agents.  The tile (n_src x T fp32) is staged once in LDS; every
+// neighbour read is an LDS read, so each element of X and G crosses HBM exactly once and each
+// element of X' is written once (12 B per element-round with the local step, 8 B without),
+// independent of the graph.  Workgroups are persistent (grid = CUs) and prefetch the next
+// tile's X/G rows into registers while mixing the current one from LDS, so HBM streaming
+// overlaps the LDS phase.  The CSR is staged in LDS once per workgroup (16-bit column ids), so
+// the mix phase issues no vector-memory loads that would queue behind the prefetch (vmcnt is
+// in-order on CDNA).  Products and sums are separate fp32 ops in CSR order (-ffp-contract=off),
+// which reproduces the reference's left fold bit for bit.
+#include "dl_internal.h"
+
+namespace dl {
+namespace {
+
+__device__ __forceinline__ float4 zero4() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+
+// Load 4 consecutive floats starting at column c0 of `row`; columns >= P read as 0.
+__device__ __forceinline__ float4 ld4(const float *__restrict__ row, int64_t c0, int64_t P,
+                                      bool vec) {
+    if (vec && c0 + 3 < P) return *reinterpret_cast<const float4 *>(row + c0);
+    float4 v = zero4();
+    if (c0 < P) v.x = row[c0];
+    if (c0 + 1 < P) v.y = row[c0 + 1];
+    if (c0 + 2 < P) v.z = row[c0 + 2];
+    if (c0 + 3 < P) v.w = row[c0 + 3];
+    return v;
+}
+
+__device__ __forceinline__ void st4(float *__restrict__ row, int64_t c0, int64_t P, bool vec,
+                                    float4 v) {
+    if (vec && c0 + 3 < P) {
+        *reinterpret_cast<float4 *>(row + c0) = v;
+        return;
+    }
+    if (c0 < P) row[c0] = v.x;
+    if (c0 + 1 < P) row[c0 + 1] = v.y;
+    if (c0 + 2 < P) row[c0 + 2] = v.z;
+    if (c0 + 3 < P) row[c0 + 3] = v.w;
+}
+
+// x - lr*g with two roundings (numpy: x - np.float32(lr) * g).
+__device__ __forceinline__ float4 local_step(float4 x, float4 g, float lr) {
+    float4 t;
+    t.x = x.x - lr * g.x;
+    t.y = x.y - lr * g.y;
+    t.z = x.z - lr * g.z;
+    t.w = x.w - lr * g.w;
+    return t;
+}
+
+__device__ __forceinline__ void axpy4(float4 &acc, float w, float4 v) {
+    acc.x = acc.x + w * v.x;
+    acc.y = acc.y + w * v.y;
+    acc.z = acc.z + w * v.z;
+    acc.w = acc.w + w * v.w;
+}
+
+__device__ __forceinline__ void add4(float4 &a, float4 b) {
+    a.x = a.x + b.x;
+    a.y = a.y + b.y;
+    a.z = a.z + b.z;
+    a.w = a.w + b.w;
+}
+
+__device__ __forceinline__ float4 shfl_xor4(float4 v, int m) {
+    v.x += __shfl_xor(v.x, m);
+    v.y += __shfl_xor(v.y, m);
+    v.z += __shfl_xor(v.z, m);
+    v.w += __shfl_xor(v.w, m);
+    return v;
+}
+
+// Offsets of one operand matrix inside a column tile, in BYTES: per lane (row s, chunk c) and
+// per prefetch pass (SLOTS rows further down).  32-bit: the host only picks this kernel when
+// every operand spans < 4 GiB, so loads use the uniform-base + 32-bit VGPR-offset form.
+__device__ __forceinline__ const float4 *at(const float *base, uint32_t off) {
+    return reinterpret_cast<const float4 *>(reinterpret_cast<const char *>(base) + off);
+}
+__device__ __forceinline__ float4 *at(float *base, uint32_t off) {
+    return reinterpret_cast<float4 *>(reinterpret_cast<char *>(base) + off);
+}
+
+// C    : float4 chunks per row in a tile (T = 4*C columns)
+// KV   : row passes per thread (rows s + k*SLOTS, k < KV); R <= KV * SLOTS
+// SGD  : fused local step x - lr*g on local rows before mixing
+// DEV  : fused column mean + per-agent ||y_a - mean||^2 (needs all agents in the tile)
+// MIX  : false = deviation of x only (no LDS staging, no output rows)
+// HALO : source rows [n_rows, n_src) come from the halo buffer
+// FAST : every tile is full and every operand 16-byte aligned (float4 path with 32-bit
+//        offsets from a uniform tile base); false = guarded scalar path (tail, unaligned)
+// Tiles cover columns [col_base + t*T, ...) for t < n_tiles.  Lanes whose row does not exist
+// (the last, ragged pass) re-read row 0 -- an L1 hit -- and never write LDS or y, so every
+// pass is straight-line code and the loads of the next tile stay in flight during the mix.
+template <int C, int KV, bool SGD, bool DEV, bool MIX, bool HALO, bool FAST>
+__global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float4 *tile = reinterpret_cast<float4 *>(smem);
+    constexpr int NT = kTileThreads;
+    constexpr int SLOTS = NT / C;  // rows covered per pass
+    constexpr int T = 4 * C;
+    const int tid = threadIdx.x;
+    const int c = tid & (C - 1);
+    const int s = tid / C;
+    const int R = a.n_src;
+    const int Nr = a.n_rows;
+    const int64_t P = a.n_params;
+    const int nnz = a.nnz;
+
+    float *lw = reinterpret_cast<float *>(smem + a.csr_off);
+    uint16_t *lcol = reinterpret_cast<uint16_t *>(smem + a.csr_off + 4u * (uint32_t)nnz);
+    uint16_t *lrp = lcol + nnz;
+    if (MIX) {
+        for (int i = tid; i < nnz; i += NT) {
+            lw[i] = a.w[i];
+            lcol[i] = (uint16_t)a.col[i];
+        }
+        if (!a.regular)
+            for (int i = tid; i <= Nr; i += NT) lrp[i] = (uint16_t)a.rowptr[i];
+    }
+    const int reg = a.regular;
+
+    // FAST-path byte offsets: lane row s / chunk c; pass k adds k * step
+    const uint32_t ox = (uint32_t)(((int64_t)s * a.ldx + 4 * c) * 4);
+    const uint32_t sx = (uint32_t)((int64_t)SLOTS * a.ldx * 4);
+    const uint32_t og = SGD ? (uint32_t)(((int64_t)s * a.ldg + 4 * c) * 4) : 0u;
+    const uint32_t sg = SGD ? (uint32_t)((int64_t)SLOTS * a.ldg * 4) : 0u;
+    const uint32_t oy = (uint32_t)(((int64_t)s * a.ldy + 4 * c) * 4);
+    const uint32_t sy = (uint32_t)((int64_t)SLOTS * a.ldy * 4);
+
+    float4 px[KV], pg[KV];
+    float dacc[KV];
+#pragma unroll
+    for (int k = 0; k < KV; ++k) dacc[k] = 0.f;
+
+    auto prefetch = [&](int tile_id) {
+        const int64_t col0 = a.col_base + (int64_t)tile_id * T;
+        if (FAST && !HALO) {
+            const float *xt = a.x + col0;
+            const float *gt = SGD ? a.g + col0 : nullptr;
+#pragma unroll
+            for (int k = 0; k < KV; ++k) {
+                const bool ok = s + k * SLOTS < R;
+                px[k] = *at(xt, ok ? ox + k * sx : 16u * c);
+                if (SGD) pg[k] = *at(gt, ok ? og + k * sg : 16u * c);
+            }
+        } else {
+            const int64_t cc = col0 + 4 * c;
+#pragma unroll
+            for (int k = 0; k < KV; ++k) {
+                int r = s + k * SLOTS;
+                if (r >= R) r = 0;
+                const bool local = !HALO || r < Nr;
+                const float *row = local ? a.x + (int64_t)r * a.ldx
+                                         : a.halo + (int64_t)(r - Nr) * a.ldh;
+                px[k] = ld4(row, cc, P, FAST);
+                if (SGD) pg[k] = local ? ld4(a.g + (int64_t)r * a.ldg, cc, P, FAST) : zero4();
+            }
+        }
+    };
+
+    int tile_id = blockIdx.x;
+    if (tile_id < a.n_tiles) prefetch(tile_id);
+    for (; tile_id < a.n_tiles; tile_id += gridDim.x) {
+        const int64_t col0 = a.col_base + (int64_t)tile_id * T;
+        const int nxt = tile_id + gridDim.x;
+        float4 out[KV];
+        if (MIX) {
+            // stage the (stepped) tile of every source row in LDS
+#pragma unroll
+            for (int k = 0; k < KV; ++k) {
+                const int r = s + k * SLOTS;
+                float4 t = px[k];
+                if (SGD && (!HALO || r < Nr)) t = local_step(t, pg[k], a.lr);
+                if (r < R) tile[r * C + c] = t;
+            }
+            __syncthreads();
+            if (nxt < a.n_tiles) prefetch(nxt);  // lands while we mix from LDS
+            // y_a = sum_e w_e * t_{col_e}, left fold in CSR order from +0.0 (mixer.py:47)
+            float *yt = a.y + col0;
+#pragma unroll
+            for (int k = 0; k < KV; ++k) {
+                const int ag = s + k * SLOTS;
+                float4 acc = zero4();
+                if (ag < Nr) {
+                    int e0, e1;
+                    if (reg) {
+                        e0 = ag * reg;
+                        e1 = e0 + reg;
+                    } else {
+                        e0 = lrp[ag];
+                        e1 = lrp[ag + 1];
+                    }
+                    for (int e = e0; e < e1; ++e) axpy4(acc, lw[e], tile[lcol[e] * C + c]);
+                    if (FAST)
+                        *at(yt, oy + k * sy) = acc;
+                    else
+                        st4(a.y + (int64_t)ag * a.ldy, col0 + 4 * c, P, false, acc);
+                }
+                if (DEV) out[k] = acc;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < KV; ++k) out[k] = (s + k * SLOTS < Nr) ? px[k] : zero4();
+            if (nxt < a.n_tiles) prefetch(nxt);
+        }
+        if (DEV) {
+            // column sums of this tile over all agents: thread -> wave (same c) -> LDS
+            float4 cs = zero4();
+#pragma unroll
+            for (int k = 0; k < KV; ++k) add4(cs, out[k]);  // missing rows hold zeros
+#pragma unroll
+            for (int m = C; m < 64; m <<= 1) cs = shfl_xor4(cs, m);
+            if (MIX) __syncthreads();  // every LDS tile read is done: reuse it as scratch
+            const int wave = tid >> 6, lane = tid & 63;
+            if (lane < C) tile[wave * C + lane] = cs;
+            __syncthreads();
+            float4 mean = zero4();
+#pragma unroll
+            for (int wv = 0; wv < NT / 64; ++wv) add4(mean, tile[wv * C + c]);
+            const float n = (float)Nr;
+            mean.x = mean.x / n;
+            mean.y = mean.y / n;
+            mean.z = mean.z / n;
+            mean.w = mean.w / n;
+            if (a.mean != nullptr && s == 0) st4(a.mean, col0 + 4 * c, P, FAST, mean);
+#pragma unroll
+            for (int k = 0; k < KV; ++k) {
+                if (s + k * SLOTS < Nr) {
+                    const float dx = out[k].x - mean.x, dy = out[k].y - mean.y;
+                    const float dz = out[k].z - mean.z, dw = out[k].w - mean.w;
+                    dacc[k] += (dx * dx + dy * dy) + (dz * dz + dw * dw);
+                }
+            }
+        }
+        __syncthreads();  // LDS reused by the next tile
+    }
+    if (DEV) {
+#pragma unroll
+        for (int k = 0; k < KV; ++k) {
+            float v = dacc[k];
+#pragma unroll
+            for (int m = 1; m < C; m <<= 1) v += __shfl_xor(v, m);
+            const int ag = s + k * SLOTS;
+            if (c == 0 && ag < Nr) a.dev_partial[(int64_t)blockIdx.x * Nr + ag] = v;
+        }
+    }
+}
+
+// General path (graphs whose tile does not fit LDS): one wave per (agent, 256 columns); the
+// agent index is wave-uniform so CSR reads are scalar loads; neighbour rows come from L2/MALL.
+template <bool SGD>
+__global__ void __launch_bounds__(256) mix_gather_kernel(TileArgs a) {
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int ag = blockIdx.y * 4 + wave;
+    if (ag >= a.n_rows) return;
+    const int64_t P = a.n_params;
+    const int64_t c0 = ((int64_t)blockIdx.x * 64 + lane) * 4;
+    if (c0 >= P) return;
+    const bool vec = a.vec != 0;
+    const int Nr = a.n_rows;
+    const int e0 = a.rowptr[ag], e1 = a.rowptr[ag + 1];
+    float4 acc = zero4();
+    for (int e = e0; e < e1; ++e) {
+        const int n = a.col[e];
+        const float wv = a.w[e];
+        const float *row = n < Nr ? a.x + (int64_t)n * a.ldx : a.halo + (int64_t)(n - Nr) * a.ldh;
+        float4 v = ld4(row, c0, P, vec);
+        if (SGD && n < Nr) v = local_step(v, ld4(a.g + (int64_t)n * a.ldg, c0, P, vec), a.lr);
+        axpy4(acc, wv, v);
+    }
+    st4(a.y + (int64_t)ag * a.ldy, c0, P, vec, acc);
+}
+
+// dev_sq[a] = sum_b partial[b][a] (fixed order, fp64); dev_max = max_a sqrt(dev_sq[a]).
+__global__ void __launch_bounds__(1024) dev_reduce_kernel(const float *__restrict__ partial,
+                                                          int nparts, int n_rows,
+                                                          float *__restrict__ dev_sq,
+                                                          float *__restrict__ dev_max) {
+    __shared__ float smax[16];
+    float mx = 0.f;
+    for (int ag = threadIdx.x; ag < n_rows; ag += 1024) {
+        double s = 0.0;
+        for (int b = 0; b < nparts; ++b) s += (double)partial[(int64_t)b * n_rows + ag];
+        const float f = (float)s;
+        if (dev_sq) dev_sq[ag] = f;
+        mx = fmaxf(mx, sqrtf(f));
+    }
+    for (int m = 32; m >= 1; m >>= 1) mx = fmaxf(mx, __shfl_xor(mx, m));
+    if ((threadIdx.x & 63) == 0) smax[threadIdx.x >> 6] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float v = 0.f;
+        for (int i = 0; i < 16; ++i) v = fmaxf(v, smax[i]);
+        if (dev_max) dev_max[0] = v;
+    }
+}
+
+template <int C, int KV, bool SGD, bool DEV, bool MIX, bool HALO, bool FAST>
+hipError_t launch_one(const TileArgs &a, int grid, int lds, hipStream_t s) {
+    auto k = mix_tile_kernel<C, KV, SGD, DEV, MIX, HALO, FAST>;
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k, dim3(grid), dim3(kTileThreads), lds, s, a);
+    return hipGetLastError();
+}
+
+template <int C, int KV, bool FAST>
+hipError_t launch_mode(const TileArgs &a, bool sgd, bool dev, bool mix, int grid, int lds,
+                       hipStream_t s) {
+    if (!mix) return launch_one<C, KV, false, true, false, false, FAST>(a, grid, lds, s);
+    if (a.n_src > a.n_rows)  // halo rows: no fused deviation (needs the global mean)
+        return sgd ? launch_one<C, KV, true, false, true, true, FAST>(a, grid, lds, s)
+                   : launch_one<C, KV, false, false, true, true, FAST>(a, grid, lds, s);
+    if (sgd) return dev ? launch_one<C, KV, true, true, true, false, FAST>(a, grid, lds, s)
+                        : launch_one<C, KV, true, false, true, false, FAST>(a, grid, lds, s);
+    return dev ? launch_one<C, KV, false, true, true, false, FAST>(a, grid, lds, s)
+               : launch_one<C, KV, false, false, true, false, FAST>(a, grid, lds, s);
+}
+
+// FAST kernels: C in {4,8,16,32} x KV in {2,4,8}; guarded kernels: every C, KV = 8.
+template <int C>
+hipError_t launch_fast_c(const TileArgs &a, int kv, bool sgd, bool dev, bool mix, int grid,
+                         int lds, hipStream_t s) {
+    if (kv <= 2) return launch_mode<C, 2, true>(a, sgd, dev, mix, grid, lds, s);
+    if (kv <= 4) return launch_mode<C, 4, true>(a, sgd, dev, mix, grid, lds, s);
+    return launch_mode<C, 8, true>(a, sgd, dev, mix, grid, lds, s);
+}
+
+}  // namespace
+
+int tile_passes(int chunks, int n_src, bool fast) {
+    const int slots = kTileThreads / chunks;
+    const int need = (n_src + slots - 1) / slots;
+    if (!fast || chunks < 4) return kRowsPerThread;
+    return need <= 2 ? 2 : need <= 4 ? 4 : 8;
+}
+
+hipError_t launch_mix_tile(const TileArgs &a, int chunks, bool sgd, bool dev, bool mix, int grid,
+                           int lds, bool fast, hipStream_t s) {
+    if (fast && chunks >= 4) {
+        const int kv = tile_passes(chunks, a.n_src, true);
+        switch (chunks) {
+            case 4: return launch_fast_c<4>(a, kv, sgd, dev, mix, grid, lds, s);
+            case 8: return launch_fast_c<8>(a, kv, sgd, dev, mix, grid, lds, s);
+            case 16: return launch_fast_c<16>(a, kv, sgd, dev, mix, grid, lds, s);
+            case 32: return launch_fast_c<32>(a, kv, sgd, dev, mix, grid, lds, s);
+            default: return hipErrorInvalidValue;
+        }
+    }
+    switch (chunks) {
+        case 1: return launch_mode<1, 8, false>(a, sgd, dev, mix, grid, lds, s);
+        case 2: return launch_mode<2, 8, false>(a, sgd, dev, mix, grid, lds, s);
+        case 4: return launch_mode<4, 8, false>(a, sgd, dev, mix, grid, lds, s);
+        case 8: return launch_mode<8, 8, false>(a, sgd, dev, mix, grid, lds, s);
+        case 16: return launch_mode<16, 8, false>(a, sgd, dev, mix, grid, lds, s);
+        case 32: return launch_mode<32, 8, false>(a, sgd, dev, mix, grid, lds, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+uint32_t csr_lds_bytes(int32_t n_rows, int32_t nnz, int32_t regular) {
+    if (nnz > 65535 || n_rows > 65535) return 0;
+    uint32_t b = 4u * (uint32_t)nnz + 2u * (uint32_t)nnz;
+    if (!regular) b += 2u * (uint32_t)(n_rows + 1);
+    return (b + 15u) & ~15u;
+}
+
+hipError_t launch_mix_gather(const TileArgs &a, bool sgd, hipStream_t s) {
+    dim3 grid((unsigned)((a.n_params + 255) / 256), (unsigned)((a.n_rows + 3) / 4));
+    if (sgd)
+        hipLaunchKernelGGL(mix_gather_kernel<true>, grid, dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL(mix_gather_kernel<false>, grid, dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_dev_reduce(const float *partial, int nparts, int n_rows, float *dev_sq,
+                             float *dev_max, hipStream_t s) {
+    hipLaunchKernelGGL(dev_reduce_kernel, dim3(1), dim3(1024), 0, s, partial, nparts, n_rows,
+                       dev_sq, dev_max);
+    return hipGetLastError();
+}
+
+}  // namespace dl

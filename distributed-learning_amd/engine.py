@@ -1,0 +1,210 @@
+"""Device-resident gossip engine: the agent matrix X[N, P] lives in HBM and every round is one
+call into libdlamd (``dl_mix_round``): fused local step + sparse mix + disagreement.
+
+This replaces, per round, the reference's Python loop of ``Mixer._mix_params_once``
+(utils/consensus_simple/mixer.py:43-49) and ``_get_deviation_dict`` (:57-66), which allocate a
+fresh fp32 array per agent and term.  Flattening models to X happens once per ``mix()`` call
+(mixer.py:26), not per round.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from .graph import Csr
+
+
+class DeviceCsr:
+    """A Csr uploaded to the device (int32 indices, fp32 weights)."""
+
+    def __init__(self, csr: Csr, device):
+        if csr.n_src > 65535 * 4 or csr.nnz >= 2 ** 31:
+            raise ValueError("graph too large for the int32 CSR ABI")
+        self.csr = csr
+        self.device = torch.device(device)
+        self.rowptr = torch.as_tensor(csr.rowptr.astype(np.int32), device=self.device)
+        self.col = torch.as_tensor(csr.col.astype(np.int32), device=self.device)
+        self.w = torch.as_tensor(csr.w.astype(np.float32), device=self.device)
+        self.n_rows = csr.n_rows
+        self.n_src = csr.n_src
+        self.nnz = csr.nnz
+        self.uniform_row_nnz = csr.uniform_row_nnz
+
+    def c_struct(self):
+        return _lib.DlCsr(_lib.ptr(self.rowptr), _lib.ptr(self.col), _lib.ptr(self.w),
+                          self.n_rows, self.nnz, self.uniform_row_nnz)
+
+
+def _ld(t):
+    if t.dim() != 2 or t.stride(1) != 1:
+        raise ValueError("expected a 2-D row-major tensor with unit column stride")
+    return t.stride(0)
+
+
+def _check(t, name, rows, cols, device):
+    if t.dtype != torch.float32:
+        raise ValueError(f"{name} must be float32 (got {t.dtype})")
+    if t.device != device:
+        raise ValueError(f"{name} is on {t.device}, expected {device}")
+    if t.shape[0] != rows or t.shape[1] != cols:
+        raise ValueError(f"{name} has shape {tuple(t.shape)}, expected ({rows}, {cols})")
+
+
+def mix_args(W: DeviceCsr, X, Y, G=None, lr=0.0, halo=None, dev_sq=None, dev_max=None,
+             mean=None):
+    """Build the dl_mix_args struct for X -> Y (shapes checked here, the rest in the ABI)."""
+    n, P = W.n_rows, X.shape[1]
+    _check(X, "X", n, P, W.device)
+    _check(Y, "Y", n, P, W.device)
+    if G is not None:
+        _check(G, "G", n, P, W.device)
+    n_halo = W.n_src - W.n_rows
+    if n_halo > 0:
+        if halo is None:
+            raise ValueError(f"graph has {n_halo} halo rows but no halo buffer was given")
+        _check(halo, "halo", n_halo, P, W.device)
+    return _lib.DlMixArgs(
+        _lib.ptr(X), _ld(X), _lib.ptr(Y), _ld(Y), P, W.c_struct(),
+        _lib.ptr(G), _ld(G) if G is not None else 0, float(lr),
+        _lib.ptr(halo) if n_halo > 0 else None, _ld(halo) if n_halo > 0 else 0, n_halo,
+        _lib.ptr(dev_sq), _lib.ptr(dev_max), _lib.ptr(mean))
+
+
+class Workspace:
+    """Grow-only device scratch buffer handed to the ABI calls."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self.buf = None
+
+    def get(self, nbytes):
+        if self.buf is None or self.buf.numel() < nbytes:
+            self.buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=self.device)
+        return self.buf
+
+    def ptr_size(self, nbytes):
+        b = self.get(nbytes)
+        return _lib.ptr(b), b.numel()
+
+
+def mix_round(W: DeviceCsr, X, Y, G=None, lr=0.0, halo=None, dev_sq=None, dev_max=None,
+              mean=None, workspace: Workspace = None):
+    """One consensus round on the current stream: Y = W (X - lr G) [+ deviation of Y]."""
+    lib = _lib.load()
+    args = mix_args(W, X, Y, G, lr, halo, dev_sq, dev_max, mean)
+    workspace = workspace or Workspace(W.device)
+    wp, wn = workspace.ptr_size(lib.dl_mix_workspace_bytes(W.n_rows, W.n_src - W.n_rows,
+                                                           X.shape[1]))
+    _lib.check(lib.dl_mix_round(ctypes.byref(args), wp, wn, _lib.stream_handle(W.device)),
+               "dl_mix_round")
+
+
+def mix_plan(W: DeviceCsr, X, Y, G=None, deviation=False):
+    lib = _lib.load()
+    dummy = torch.empty(1, dtype=torch.float32, device=W.device) if deviation else None
+    args = mix_args(W, X, Y, G, 0.0, None, dummy, dummy, None)
+    plan = _lib.DlMixPlan()
+    _lib.check(lib.dl_mix_plan_query(ctypes.byref(args), ctypes.byref(plan)), "dl_mix_plan_query")
+    return {f: getattr(plan, f) for f, _ in plan._fields_}
+
+
+def deviation(X, dev_sq=None, dev_max=None, mean_in=None, mean_out=None,
+              workspace: Workspace = None):
+    """dev_sq[a] = ||x_a - mean||^2 and dev_max = max_a ||x_a - mean|| (mixer.py:51-66)."""
+    lib = _lib.load()
+    n, P = X.shape
+    dev = X.device
+    if dev_sq is None:
+        dev_sq = torch.empty(n, dtype=torch.float32, device=dev)
+    if dev_max is None:
+        dev_max = torch.empty(1, dtype=torch.float32, device=dev)
+    workspace = workspace or Workspace(dev)
+    wp, wn = workspace.ptr_size(lib.dl_deviation_workspace_bytes(n, P))
+    _lib.check(lib.dl_deviation(_lib.ptr(X), _ld(X), n, P, _lib.ptr(mean_in), _lib.ptr(dev_sq),
+                                _lib.ptr(dev_max), _lib.ptr(mean_out), wp, wn,
+                                _lib.stream_handle(dev)), "dl_deviation")
+    return dev_sq, dev_max
+
+
+def column_sum(X, out=None):
+    lib = _lib.load()
+    n, P = X.shape
+    out = torch.empty(P, dtype=torch.float32, device=X.device) if out is None else out
+    _lib.check(lib.dl_column_sum(_lib.ptr(X), _ld(X), n, P, _lib.ptr(out),
+                                 _lib.stream_handle(X.device)), "dl_column_sum")
+    return out
+
+
+def max_column_std(X):
+    lib = _lib.load()
+    n, P = X.shape
+    out = torch.empty(1, dtype=torch.float32, device=X.device)
+    _lib.check(lib.dl_max_column_std(_lib.ptr(X), _ld(X), n, P, _lib.ptr(out),
+                                     _lib.stream_handle(X.device)), "dl_max_column_std")
+    return out
+
+
+def step_rows(X, rows, out, G=None, lr=0.0):
+    """out[i] = X[rows[i]] - lr * G[rows[i]] (halo send buffers)."""
+    lib = _lib.load()
+    n_sel = rows.numel()
+    P = X.shape[1]
+    _lib.check(lib.dl_step_rows(_lib.ptr(X), _ld(X), _lib.ptr(G), _ld(G) if G is not None else 0,
+                                float(lr), _lib.ptr(rows), n_sel, P, _lib.ptr(out), _ld(out),
+                                _lib.stream_handle(X.device)), "dl_step_rows")
+    return out
+
+
+def perron_round(Y, rowptr, col, eps, conv_eps, weight=None, mean_weight=1.0, max_iter=1 << 30,
+                 workspace: Workspace = None):
+    """In-place asyncio-style consensus round on Y (fp32 or fp64).  Returns the iteration count."""
+    lib = _lib.load()
+    if Y.dtype not in (torch.float32, torch.float64):
+        raise ValueError("perron_round supports float32 and float64")
+    dtype = 1 if Y.dtype == torch.float64 else 0
+    n, P = Y.shape
+    iters = torch.zeros(1, dtype=torch.int32, device=Y.device)
+    workspace = workspace or Workspace(Y.device)
+    wp, wn = workspace.ptr_size(lib.dl_perron_workspace_bytes(dtype, n, P))
+    args = _lib.DlPerronArgs(dtype, _lib.ptr(Y), _ld(Y), n, P, _lib.ptr(rowptr), _lib.ptr(col),
+                             _lib.ptr(weight), float(mean_weight), float(eps), float(conv_eps),
+                             int(min(max_iter, 2 ** 31 - 1)), _lib.ptr(iters))
+    _lib.check(lib.dl_perron_round(ctypes.byref(args), wp, wn, _lib.stream_handle(Y.device)),
+               "dl_perron_round")
+    return int(iters.item())
+
+
+class GossipEngine:
+    """N agents x P params resident in HBM, mixed by a fixed sparse W.
+
+    ``round(G, lr)`` runs one consensus round  X <- W (X - lr G)  (ping-pong buffers, no host
+    synchronisation); with ``deviation=True`` it also leaves ||x_a - mean||^2 in ``dev_sq`` and
+    max_a ||x_a - mean|| in ``dev_max`` (device tensors).
+    """
+
+    def __init__(self, csr: Csr, n_params, device="cuda", X=None):
+        self.device = torch.device(device)
+        if self.device.type == "cuda" and self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        self.W = DeviceCsr(csr, self.device)
+        self.n, self.P = csr.n_rows, int(n_params)
+        self.X = X if X is not None else torch.zeros(self.n, self.P, device=self.device)
+        self.Y = torch.empty_like(self.X)
+        self.dev_sq = torch.zeros(self.n, dtype=torch.float32, device=self.device)
+        self.dev_max = torch.zeros(1, dtype=torch.float32, device=self.device)
+        self.mean = None
+        self.ws = Workspace(self.device)
+
+    def round(self, G=None, lr=0.0, deviation=False, mean=None, halo=None):
+        mix_round(self.W, self.X, self.Y, G=G, lr=lr, halo=halo,
+                  dev_sq=self.dev_sq if deviation else None,
+                  dev_max=self.dev_max if deviation else None, mean=mean, workspace=self.ws)
+        self.X, self.Y = self.Y, self.X
+
+    def deviation(self, mean_in=None, mean_out=None):
+        return deviation(self.X, self.dev_sq, self.dev_max, mean_in=mean_in, mean_out=mean_out,
+                         workspace=self.ws)
+
+    def plan(self, G=None, deviation=False):
+        return mix_plan(self.W, self.X, self.Y, G, deviation)

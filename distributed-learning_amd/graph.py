@@ -1,0 +1,185 @@
+"""Graph compiler: reference topology formats -> CSR mixing matrices (host side).
+
+The reference feeds the mix from three places, each with its own vertex numbering and entry
+order; the fp32 summation order of the kernel is the CSR entry order, so keeping the reference
+order here is what makes the HIP mix bit-identical to it:
+
+* ``Mixer`` dict-of-dicts (utils/consensus_simple/mixer.py:43-49): rows in ``topology`` key order,
+  entries in ``topology[a].items()`` order, weights as given (cast to fp32 like numpy does).
+* asyncio edge list (utils/consensus_asyncio.py:40, 104): tokens = ``list(set(flatten))``,
+  neighbours in edge-list order, Perron weight ``eps = 0.95 / max_deg``.
+* fast-averaging edge list + per-edge weights (utils/fast_averaging.py:9-14, consensus_tcp
+  agent.py:204-207): vertices by first appearance, row a = ``(1 - sum w) x_a + sum w_j x_j``.
+"""
+from dataclasses import dataclass, field
+
+import numpy as np
+
+
+@dataclass
+class Csr:
+    """Host CSR of a mixing matrix.  Source rows [0, n_rows) are local agents; rows
+    [n_rows, n_src) (multi-GPU only) are halo rows owned by other ranks."""
+    rowptr: np.ndarray          # int64 [n_rows + 1]
+    col: np.ndarray             # int64 [nnz]
+    w: np.ndarray               # float64 [nnz] (cast to fp32 on upload)
+    keys: list = field(default_factory=list)   # agent key of each local row
+    n_src: int = -1
+
+    def __post_init__(self):
+        self.rowptr = np.asarray(self.rowptr, np.int64)
+        self.col = np.asarray(self.col, np.int64)
+        self.w = np.asarray(self.w, np.float64)
+        if self.n_src < 0:
+            self.n_src = self.n_rows
+        if len(self.rowptr) < 1 or self.rowptr[0] != 0 or np.any(np.diff(self.rowptr) < 0):
+            raise ValueError("row_ptr must start at 0 and be non-decreasing")
+        if self.rowptr[-1] != len(self.col) or len(self.col) != len(self.w):
+            raise ValueError("row_ptr[-1], len(col) and len(w) must agree")
+        if len(self.col) and (self.col.min() < 0 or self.col.max() >= self.n_src):
+            raise ValueError(f"column index out of range [0, {self.n_src})")
+
+    @property
+    def n_rows(self):
+        return len(self.rowptr) - 1
+
+    @property
+    def nnz(self):
+        return len(self.col)
+
+    @property
+    def uniform_row_nnz(self):
+        d = np.diff(self.rowptr)
+        return int(d[0]) if len(d) and d[0] > 0 and np.all(d == d[0]) else 0
+
+    def dense(self):
+        W = np.zeros((self.n_rows, self.n_src))
+        for a in range(self.n_rows):
+            for e in range(self.rowptr[a], self.rowptr[a + 1]):
+                W[a, self.col[e]] += self.w[e]
+        return W
+
+
+def from_topology(topology, keys=None):
+    """dict-of-dicts (``Mixer`` format) -> Csr in dict insertion order (mixer.py:46-47).
+
+    A neighbour that is not itself a key raises KeyError, as ``params[neighbor]`` does in the
+    reference."""
+    keys = list(topology) if keys is None else list(keys)
+    index = {k: i for i, k in enumerate(keys)}
+    rowptr, col, w = [0], [], []
+    for a in keys:
+        for n, wt in topology[a].items():
+            if n not in index:
+                raise KeyError(n)
+            col.append(index[n])
+            w.append(float(wt))
+        rowptr.append(len(col))
+    return Csr(rowptr, col, w, keys=keys)
+
+
+def first_appearance_vertices(edges):
+    """Vertex numbering of ``find_optimal_weights`` (fast_averaging.py:9-14)."""
+    v = {}
+    for (a, b) in edges:
+        if a not in v:
+            v[a] = len(v)
+        if b not in v:
+            v[b] = len(v)
+    return list(v)
+
+
+def from_edge_weights(edges, weights, vertices=None):
+    """Fast-averaging weights -> W = I - L(w) (consensus_tcp/agent.py:204-207).
+
+    Row a: diagonal ``1 - sum_j w_aj`` first, then its neighbours in edge-list order.  Self-loop
+    edges carry no weight in L (fast_averaging.py:20) and are skipped."""
+    vertices = first_appearance_vertices(edges) if vertices is None else list(vertices)
+    index = {k: i for i, k in enumerate(vertices)}
+    nbrs = {k: {} for k in vertices}
+    for (u, v), wt in zip(edges, weights):
+        if u == v:
+            continue
+        nbrs[u].setdefault(v, float(wt))
+        nbrs[v].setdefault(u, float(wt))
+    rowptr, col, w = [0], [], []
+    for a in vertices:
+        col.append(index[a])
+        w.append(1.0 - sum(nbrs[a].values()))
+        for n, wt in nbrs[a].items():
+            col.append(index[n])
+            w.append(wt)
+        rowptr.append(len(col))
+    return Csr(rowptr, col, w, keys=vertices)
+
+
+def asyncio_tokens(edges):
+    """``ConsensusNetwork.tokens`` = ``list(set(np.array(topology).flatten()))`` (:40)."""
+    return list(set(np.array(edges).flatten()))
+
+
+def asyncio_adjacency(edges, tokens=None):
+    """Neighbour lists in the order an asyncio agent builds its sockets (:104-114): edge-list
+    order, duplicates collapsed, self loops dropped.  Returns (tokens, rowptr, col)."""
+    tokens = asyncio_tokens(edges) if tokens is None else list(tokens)
+    index = {t: i for i, t in enumerate(tokens)}
+    rowptr, col = [0], []
+    for t in tokens:
+        nb = [u if t == v else v for (u, v) in edges if (t == u or t == v) and u != v]
+        for n in dict.fromkeys(nb):
+            col.append(index[n])
+        rowptr.append(len(col))
+    return tokens, np.asarray(rowptr, np.int64), np.asarray(col, np.int64)
+
+
+def perron_eps(edges, tokens=None):
+    """``ConsensusNetwork.__calc_eps`` (:78-86): 0.95 / max degree of the 0/1 adjacency."""
+    tokens = asyncio_tokens(edges) if tokens is None else tokens
+    E = np.array([[int((u, v) in edges or (v, u) in edges) for v in tokens] for u in tokens])
+    return 0.95 / np.max(np.sum(E, axis=1))
+
+
+def uniform_weights(edges, w, vertices=None):
+    """Every edge weight ``w`` (e.g. the best-constant 2/(l2 + l_max)) -> W = I - w L."""
+    vertices = first_appearance_vertices(edges) if vertices is None else vertices
+    return from_edge_weights(edges, [w] * len(edges), vertices)
+
+
+# ------------------------------------------------------------------ synthetic graphs
+def random_regular_edges(d, n, seed):
+    """Edge list of ``networkx.random_regular_graph(d, n, seed)`` (bench config c2)."""
+    import networkx as nx
+    return [(int(u), int(v)) for u, v in nx.random_regular_graph(d, n, seed=seed).edges()]
+
+
+def torus_edges(rows, cols):
+    """2-D periodic torus (bench config c4): vertex r*cols + c, right and down neighbours."""
+    edges = []
+    for r in range(rows):
+        for c in range(cols):
+            a = r * cols + c
+            edges.append((a, r * cols + (c + 1) % cols))
+            edges.append((a, ((r + 1) % rows) * cols + c))
+    return edges
+
+
+def laplacian(edges, vertices=None):
+    vertices = first_appearance_vertices(edges) if vertices is None else vertices
+    index = {k: i for i, k in enumerate(vertices)}
+    n = len(vertices)
+    L = np.zeros((n, n))
+    for (u, v) in edges:
+        if u == v:
+            continue
+        i, j = index[u], index[v]
+        if L[i, j] == 0:
+            L[i, j] = L[j, i] = -1.0
+    L[np.diag_indices(n)] = -L.sum(1)
+    return L
+
+
+def best_constant_weight(edges, vertices=None):
+    """Best constant edge weight ``2 / (lambda_2 + lambda_max)`` of the unweighted Laplacian
+    (Xiao & Boyd 2004); optimal for edge-transitive graphs (ring, torus)."""
+    ev = np.linalg.eigvalsh(laplacian(edges, vertices))
+    return 2.0 / (ev[1] + ev[-1])

@@ -1,0 +1,153 @@
+/* dlamd.h -- C ABI of the MI355X consensus-mixing engine (libdlamd.so).
+ *
+ * The reference (Malkovsky/distributed-learning) is pure Python; it has no native/FFI boundary.
+ * Each entry point below replaces one reference Python routine on the gossip hot path and is
+ * what a binding (ctypes here) calls in its place:
+ *
+ *   dl_mix_round        <- Mixer._mix_params_once        utils/consensus_simple/mixer.py:43-49
+ *                          (+ the local step x -= lr*g that a training loop runs before mixing,
+ *                           Titanic Consensus GD test.ipynb:903-907, and the deviation pass of
+ *                           Mixer._get_deviation_dict mixer.py:57-66, fused)
+ *   dl_deviation        <- Mixer._get_deviation_dict / _get_max_deviation   mixer.py:51-66
+ *   dl_max_column_std   <- Mixer.get_max_parameters_std                     mixer.py:82-84
+ *   dl_perron_round     <- ConsensusAgent.run_round mixing loop             consensus_asyncio.py:231-310
+ *   dl_step_rows        <- (multi-GPU) boundary rows x - lr*g packed for the halo exchange that
+ *                          replaces the per-neighbour value messages of consensus_asyncio.py:236-284
+ *   dl_column_sum       <- the np.mean numerator of mixer.py:61 (multi-GPU global mean)
+ *
+ * Conventions
+ *   - Every pointer argument is a DEVICE pointer owned by the caller; nothing is allocated inside.
+ *     Scratch comes from the caller's workspace (size from the *_workspace_bytes query).
+ *   - Calls are stream-ordered and asynchronous (no host synchronisation) unless stated.
+ *   - Matrices are row-major: row a = agent a, `ld*` = row stride in elements.
+ *   - No exceptions cross the ABI. Return value: 0 on success, otherwise a dl_status code;
+ *     dl_last_error() returns a thread-local message for the last failure on this thread.
+ *   - Reentrant across streams; the only process-wide state is a per-device property cache.
+ */
+#ifndef DLAMD_H
+#define DLAMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DLAMD_ABI_VERSION 1
+
+typedef void *dl_stream_t; /* hipStream_t; NULL = the legacy default stream */
+
+enum dl_status {
+    DL_OK = 0,
+    DL_ERR_INVALID = 1,   /* bad argument (shape, null pointer, alias, range) */
+    DL_ERR_WORKSPACE = 2, /* workspace too small or misaligned */
+    DL_ERR_HIP = 3,       /* a HIP runtime call failed; message has the hipError string */
+    DL_ERR_UNSUPPORTED = 4
+};
+
+/* Mixing matrix W in CSR form (device pointers).  Row a lists its (source row, weight) pairs in
+ * the reference's dict insertion order (mixer.py:47) -- that order is the fp32 summation order,
+ * and the result is bit-identical to the reference's left fold when it is kept.  Source rows
+ * index [0, n_rows) = local agents, [n_rows, n_rows + n_halo) = halo rows. */
+typedef struct dl_csr {
+    const int32_t *row_ptr; /* [n_rows + 1] */
+    const int32_t *col;     /* [nnz] */
+    const float *w;         /* [nnz] fp32 (the reference casts the Python float to fp32) */
+    int32_t n_rows;
+    int32_t nnz;
+    int32_t uniform_row_nnz; /* > 0 promises row_ptr[a] == a * uniform_row_nnz for every row
+                                (regular graphs); lets the LDS kernel skip staging row_ptr.
+                                0 = general CSR.  Checked: nnz == n_rows * uniform_row_nnz. */
+} dl_csr;
+
+typedef struct dl_mix_args {
+    const float *x;     /* [n_rows, ldx] parameters before the round */
+    int64_t ldx;
+    float *y;           /* [n_rows, ldy] parameters after the round; must not overlap x */
+    int64_t ldy;
+    int64_t n_params;   /* columns per agent */
+    dl_csr W;
+    const float *g;     /* nullable [n_rows, ldg]: fused local step x <- x - lr*g first */
+    int64_t ldg;
+    float lr;
+    const float *halo;  /* nullable [n_halo, ldh]: remote rows, already stepped */
+    int64_t ldh;
+    int32_t n_halo;
+    float *dev_sq;      /* nullable [n_rows]: ||y_a - mean_b(y_b)||^2  (needs n_halo == 0) */
+    float *dev_max;     /* nullable [1]: max_a sqrt(dev_sq[a])          (needs n_halo == 0) */
+    float *mean;        /* nullable [n_params]: mean_b(y_b)              (needs n_halo == 0) */
+} dl_mix_args;
+
+/* Which kernel configuration dl_mix_round picks (introspection for tests and the bench). */
+typedef struct dl_mix_plan {
+    int32_t path;       /* 1 = LDS tile kernel (all agents x T columns per tile), 2 = gather kernel */
+    int32_t tile_cols;  /* T: columns per tile (path 1) */
+    int32_t grid;       /* workgroups launched */
+    int32_t lds_bytes;  /* dynamic LDS per workgroup */
+    int32_t n_tiles;
+    int32_t regular;    /* 1 if every row has the same entry count (CSR row_ptr not staged) */
+} dl_mix_plan;
+
+int dl_abi_version(void);
+const char *dl_last_error(void);
+
+size_t dl_mix_workspace_bytes(int32_t n_rows, int32_t n_halo, int64_t n_params);
+int dl_mix_plan_query(const dl_mix_args *args, dl_mix_plan *plan);
+int dl_mix_round(const dl_mix_args *args, void *workspace, size_t ws_bytes, dl_stream_t stream);
+
+/* Deviation of x from its column mean: dev_sq[a] = ||x_a - mean||^2, dev_max = max sqrt(dev_sq).
+ * mean_in nullable: when given (e.g. a global mean all-reduced across GPUs) it is used instead
+ * of the local column mean.  mean_out nullable.  Returns zeros when n_rows <= 1 (mixer.py:58-59). */
+size_t dl_deviation_workspace_bytes(int32_t n_rows, int64_t n_params);
+int dl_deviation(const float *x, int64_t ldx, int32_t n_rows, int64_t n_params,
+                 const float *mean_in, float *dev_sq, float *dev_max, float *mean_out,
+                 void *workspace, size_t ws_bytes, dl_stream_t stream);
+
+/* colsum[p] = sum_a x[a, p], rows added in order (numerator of np.mean, mixer.py:61). */
+int dl_column_sum(const float *x, int64_t ldx, int32_t n_rows, int64_t n_params, float *colsum,
+                  dl_stream_t stream);
+
+/* out[0] = max_p std_a(x[a, p]) (population std, the intent of mixer.py:82-84). */
+int dl_max_column_std(const float *x, int64_t ldx, int32_t n_rows, int64_t n_params, float *out,
+                      dl_stream_t stream);
+
+/* out[i, :] = x[rows[i], :] - lr * g[rows[i], :]  (g nullable: plain copy).  Packs the boundary
+ * rows a GPU sends to its neighbours in the multi-GPU halo exchange. */
+int dl_step_rows(const float *x, int64_t ldx, const float *g, int64_t ldg, float lr,
+                 const int32_t *rows, int32_t n_sel, int64_t n_params, float *out, int64_t ldo,
+                 dl_stream_t stream);
+
+/* One asyncio consensus round (consensus_asyncio.py:209-312) restated as synchronous Jacobi:
+ *   y0_a = v_a * weight_a / mean_weight                              (:231)
+ *   y_a <- y_a * (1 - eps*deg_a) + eps * sum_{j in N(a)} y_j           (:295, sum then scale)
+ *   flag_a = all_j all_p (y_a - y_j_previous <= conv_eps)              (:297, one-sided)
+ * iterated until every flag is set (master DONE, :170-174) or max_iter.  `y` holds the values on
+ * entry and the result on exit; iters_out (device int32[1]) receives the iteration count.
+ * The adjacency (no self loops) lists neighbours in the agent's socket order (:104-114).
+ * When all columns fit one tile the loop runs inside one launch; otherwise this call iterates on
+ * the host and SYNCHRONISES the stream once per iteration. */
+typedef struct dl_perron_args {
+    int32_t dtype;            /* 0 = fp32, 1 = fp64 */
+    void *y;                  /* [n_rows, ldy] */
+    int64_t ldy;
+    int32_t n_rows;
+    int64_t n_params;
+    const int32_t *row_ptr;   /* [n_rows + 1] adjacency */
+    const int32_t *col;       /* [nnz] */
+    const double *weight;     /* nullable [n_rows]: pre-scale weights (NULL: no pre-scale) */
+    double mean_weight;
+    double eps;
+    double conv_eps;
+    int32_t max_iter;
+    int32_t *iters_out;       /* device [1] */
+} dl_perron_args;
+
+size_t dl_perron_workspace_bytes(int32_t dtype, int32_t n_rows, int64_t n_params);
+int dl_perron_round(const dl_perron_args *args, void *workspace, size_t ws_bytes,
+                    dl_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DLAMD_H */

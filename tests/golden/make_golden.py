@@ -1,0 +1,390 @@
+"""Generate the golden fixtures under tests/golden/ by RUNNING the reference.
+
+Build-container only: it imports Malkovsky/distributed-learning from /root/reference
+(read-only; PYTHONDONTWRITEBYTECODE keeps it clean).  Nothing on the GPU box runs this
+script; the tests only read the .npz/.json files it writes.
+
+What is produced (see SURVEY.md §8c for the list this follows):
+
+* ``mix_rr4_n64.npz``   -- ``Mixer._mix_params_once`` (utils/consensus_simple/mixer.py:43-49)
+  and ``Mixer._get_deviation_dict`` (mixer.py:57-66) on a random 4-regular graph (uniform
+  0.2 weights, shuffled agent keys, self-loop at varying dict positions) and on a
+  Barabasi-Albert graph with Metropolis weights; snapshots after 1, 10 and 200 rounds.
+* ``mix_ring8_fa.npz``  -- ring-8 with the analytic fast-averaging weight, P=7, fp32 and fp64.
+* ``mixer_ann.npz``     -- the full ``Mixer.mix`` (mixer.py:18-38) on 4 ``ANNModel``
+  instances (networks/ann_model.py:4-45): flatten order, ``times`` loop, ``eps`` stop, return
+  value, write-back.
+* ``asyncio_graphs.npz`` -- ``ConsensusAgent.run_round`` (utils/consensus_asyncio.py:209-312)
+  over K4 / ring8 / cycle3 / grid5 / RR4-16 at several convergence eps, plus the mixing
+  iteration count k recovered by matching the synchronous Jacobi iterate.
+* ``titanic.npz``        -- preprocessed Titanic data (notebook cells 2-4), centralised GD
+  (cell 5) and ring-8 asyncio consensus GD for 4000 steps at eps=10 (cells 12-14).
+* ``notebook_outputs.json`` -- values the reference notebooks themselves recorded.
+
+Run:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+"""
+import asyncio
+import hashlib
+import json
+import logging
+import os
+import sys
+
+import numpy as np
+
+REF = "/root/reference"
+OUT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REF)
+
+import networkx as nx  # noqa: E402
+import torch  # noqa: E402
+
+from utils.consensus_simple.mixer import Mixer  # noqa: E402  (reference)
+import utils.consensus_asyncio as ref_async  # noqa: E402  (reference)
+from networks import ANNModel  # noqa: E402  (reference)
+
+LOG = logging.getLogger("golden")
+
+
+def _csr_from_topology(topology, keys):
+    """Flatten a dict-of-dicts topology to CSR in dict insertion order (row = key position)."""
+    index = {k: i for i, k in enumerate(keys)}
+    rowptr, cols, ws = [0], [], []
+    for a in keys:
+        for n, w in topology[a].items():
+            cols.append(index[n])
+            ws.append(float(w))
+        rowptr.append(len(cols))
+    return (np.asarray(rowptr, np.int64), np.asarray(cols, np.int64),
+            np.asarray(ws, np.float64))
+
+
+def _run_reference_mixer_rounds(topology, params, rounds):
+    mixer = Mixer(models=None, topology=topology, logger=LOG)
+    snaps, devs = {}, {}
+    devs[0] = mixer._get_deviation_dict(params)
+    done = 0
+    for r in sorted(rounds):
+        while done < r:
+            params = mixer._mix_params_once(params)
+            done += 1
+        snaps[r] = params
+        devs[r] = mixer._get_deviation_dict(params)
+    return snaps, devs
+
+
+def make_mix_rr4():
+    rng = np.random.default_rng(0)
+    out = {}
+    # --- case A: random 4-regular graph, uniform 0.2 incl. self, shuffled keys -------------
+    g = nx.random_regular_graph(4, 64, seed=0)
+    edges = np.asarray(list(g.edges()), np.int64)
+    keys = [int(k) for k in rng.permutation(64)]
+    topo = {}
+    for a in keys:
+        nbrs = [int(n) for n in g.adj[a]]
+        pos = a % (len(nbrs) + 1)
+        order = nbrs[:pos] + [a] + nbrs[pos:]
+        topo[a] = {n: 0.2 for n in order}
+    X0 = rng.standard_normal((64, 512), dtype=np.float32)
+    params = {a: X0[i].copy() for i, a in enumerate(keys)}
+    snaps, devs = _run_reference_mixer_rounds(topo, params, [1, 10, 200])
+    rp, cols, ws = _csr_from_topology(topo, keys)
+    out.update(a_edges=edges, a_keys=np.asarray(keys), a_rowptr=rp, a_cols=cols, a_w=ws, a_X0=X0)
+    for r, p in snaps.items():
+        out[f"a_X{r}"] = np.stack([p[a] for a in keys])
+    for r, d in devs.items():
+        out[f"a_dev{r}"] = np.asarray([d[a] for a in keys], np.float32)
+    # --- case B: Barabasi-Albert graph, Metropolis weights, self first, string keys -------
+    g = nx.barabasi_albert_graph(64, 2, seed=1)
+    deg = dict(g.degree())
+    keys_b = [f"agent{i:02d}" for i in range(64)]
+    name = {i: keys_b[i] for i in range(64)}
+    topo_b = {}
+    for i in range(64):
+        row = {}
+        off = 0.0
+        for j in g.adj[i]:
+            w = 1.0 / (1.0 + max(deg[i], deg[j]))
+            row[name[j]] = w
+            off += w
+        topo_b[name[i]] = {name[i]: 1.0 - off, **row}
+    X0b = rng.standard_normal((64, 384), dtype=np.float32)
+    params = {name[i]: X0b[i].copy() for i in range(64)}
+    snaps, devs = _run_reference_mixer_rounds(topo_b, params, [1, 10])
+    rp, cols, ws = _csr_from_topology(topo_b, keys_b)
+    out.update(b_rowptr=rp, b_cols=cols, b_w=ws, b_X0=X0b)
+    for r, p in snaps.items():
+        out[f"b_X{r}"] = np.stack([p[a] for a in keys_b])
+    for r, d in devs.items():
+        out[f"b_dev{r}"] = np.asarray([d[a] for a in keys_b], np.float32)
+    np.savez_compressed(os.path.join(OUT, "mix_rr4_n64.npz"), **out)
+
+
+def make_ring8_fa():
+    n = 8
+    # Python float on purpose: an np.float64 weight would promote the fp32 fold to fp64 (NEP 50)
+    w = float(1.0 / (3.0 - np.cos(2 * np.pi / n)))
+    topo = {a: {(a - 1) % n: w, a: 1.0 - 2.0 * w, (a + 1) % n: w} for a in range(n)}
+    keys = list(range(n))
+    rng = np.random.default_rng(1)
+    X64 = rng.standard_normal((n, 7))
+    out = {"w": np.float64(w)}
+    for tag, X0 in (("f32", X64.astype(np.float32)), ("f64", X64)):
+        params = {a: X0[a].copy() for a in keys}
+        snaps, devs = _run_reference_mixer_rounds(topo, params, [1, 50])
+        out[f"{tag}_X0"] = X0
+        for r, p in snaps.items():
+            out[f"{tag}_X{r}"] = np.stack([p[a] for a in keys])
+            out[f"{tag}_dev{r}"] = np.asarray([devs[r][a] for a in keys])
+    rp, cols, ws = _csr_from_topology(topo, keys)
+    out.update(rowptr=rp, cols=cols, wts=ws)
+    np.savez_compressed(os.path.join(OUT, "mix_ring8_fa.npz"), **out)
+
+
+def _flat(model):
+    return torch.cat([p.data.to(torch.float32).view(-1) for p in model.parameters()]).numpy().copy()
+
+
+def make_mixer_ann():
+    torch.manual_seed(0)
+    topo = {
+        "a": {"a": 0.5, "b": 0.25, "d": 0.25},
+        "b": {"a": 0.25, "c": 0.25, "b": 0.5},
+        "c": {"d": 0.3, "c": 0.4, "b": 0.3},
+        "d": {"c": 0.3, "a": 0.25, "d": 0.45},
+    }
+    keys = list(topo)
+    models = {k: ANNModel(20, 15, 3) for k in keys}
+    init = np.stack([_flat(models[k]) for k in keys])
+    out = {"init": init}
+    mixer = Mixer(models, topo, LOG)
+    out["dev_init"] = np.asarray([mixer.get_parameters_deviation()[k] for k in keys], np.float32)
+    out["ret_times3"] = np.int64(mixer.mix(times=3))
+    out["after_times3"] = np.stack([_flat(models[k]) for k in keys])
+    # restart from the same init and stop on eps
+    for i, k in enumerate(keys):
+        _load(models[k], init[i])
+    out["ret_eps"] = np.int64(mixer.mix(times=1, eps=1e-3))
+    out["after_eps"] = np.stack([_flat(models[k]) for k in keys])
+    out["dev_after_eps"] = np.asarray([mixer.get_parameters_deviation()[k] for k in keys], np.float32)
+    # eps with times larger than needed: loop continues until times reached
+    for i, k in enumerate(keys):
+        _load(models[k], init[i])
+    out["ret_eps_times20"] = np.int64(mixer.mix(times=20, eps=1e-1))
+    out["after_eps_times20"] = np.stack([_flat(models[k]) for k in keys])
+    rp, cols, ws = _csr_from_topology(topo, keys)
+    out.update(rowptr=rp, cols=cols, wts=ws)
+    big = ANNModel(784, 150, 10)
+    out["ann784_numel"] = np.int64(sum(p.numel() for p in big.parameters()))
+    out["ann784_shapes"] = np.asarray([list(p.shape) + [0] * (2 - p.dim()) for p in big.parameters()])
+    np.savez_compressed(os.path.join(OUT, "mixer_ann.npz"), **out)
+
+
+def _load(model, flat):
+    used = 0
+    for p in model.parameters():
+        c = p.numel()
+        p.data.copy_(torch.from_numpy(flat[used:used + c].copy()).view(p.shape))
+        used += c
+
+
+# ---------------------------------------------------------------- asyncio reference runs
+async def _async_rounds(topology, values_per_round, weights, conv_eps):
+    shutdown = asyncio.Queue()
+    net = ref_async.ConsensusNetwork(topology, shutdown)
+    agents = [ref_async.ConsensusAgent(t, convergence_eps=conv_eps) for t in net.tokens]
+    for a in agents:
+        net.register_agent(a)
+    serve = asyncio.create_task(net.serve())
+    results = []
+    for values in values_per_round:
+        tasks = [asyncio.create_task(a.run_round(values[a.token], weights[a.token])) for a in agents]
+        res = await asyncio.gather(*tasks)
+        results.append({a.token: r for a, r in zip(agents, res)})
+    await shutdown.put(ref_async.SHUTDOWN)
+    await serve
+    return [int(t) for t in net.tokens], results
+
+
+def _jacobi_match(topology, tokens, y0, target, kmax=5000):
+    """Recover k such that target == (I - eps L)^k y0 (restated Jacobi, consensus_asyncio.py:295)."""
+    idx = {t: i for i, t in enumerate(tokens)}
+    n = len(tokens)
+    A = np.zeros((n, n))
+    for u, v in topology:
+        A[idx[u], idx[v]] = A[idx[v], idx[u]] = 1
+    deg = A.sum(1)
+    eps = 0.95 / deg.max()
+    y = y0.copy()
+    best = (np.inf, -1)
+    for k in range(kmax + 1):
+        err = np.max(np.abs(y - target))
+        if err < best[0]:
+            best = (err, k)
+        if err == 0.0:
+            break
+        y = y * (1 - eps * deg)[:, None] + eps * (A @ y)
+    return best
+
+
+def make_asyncio():
+    graphs = {
+        "k4": [(0, 1), (0, 2), (0, 3), (1, 2), (1, 3), (2, 3)],
+        "ring8": [(i, (i + 1) % 8) for i in range(8)],
+        "cycle3": [(0, 1), (1, 2), (2, 0)],
+        "grid5": [(0, 1), (0, 2), (0, 3), (0, 4), (1, 3), (3, 2), (2, 4), (1, 4)],
+        "rr4_16": [(int(u), int(v)) for u, v in nx.random_regular_graph(4, 16, seed=0).edges()],
+    }
+    eps_list = {"k4": [10, 1e-1, 1e-4], "ring8": [10, 1e-1, 1e-4, 1e-10], "cycle3": [10, 1e-4],
+                "grid5": [10, 1e-1, 1e-4], "rr4_16": [10, 1e-4]}
+    out = {}
+    rng = np.random.default_rng(7)
+    for name, topo in graphs.items():
+        out[f"{name}_edges"] = np.asarray(topo, np.int64)
+        toks = sorted(set(np.array(topo).flatten().tolist()))
+        for ei, ce in enumerate(eps_list[name]):
+            rounds = 2 if name == "ring8" else 1
+            vals = [{t: rng.standard_normal(7) for t in toks} for _ in range(rounds)]
+            wts = {t: int(rng.integers(1, 10)) for t in toks}
+            tokens, res = asyncio.run(_async_rounds(topo, vals, wts, ce))
+            key = f"{name}_e{ei}"
+            out[key + "_conv_eps"] = np.float64(ce)
+            out[key + "_tokens"] = np.asarray(tokens)
+            out[key + "_weights"] = np.asarray([wts[t] for t in tokens], np.float64)
+            for r in range(rounds):
+                v0 = np.stack([vals[r][t] for t in tokens])
+                got = np.stack([res[r][t] for t in tokens])
+                w = out[key + "_weights"]
+                y0 = v0 * w[:, None] / w.mean()
+                err, k = _jacobi_match(topo, tokens, y0, got)
+                out[key + f"_r{r}_values"] = v0
+                out[key + f"_r{r}_out"] = got
+                out[key + f"_r{r}_k"] = np.int64(k)
+                out[key + f"_r{r}_jacobi_err"] = np.float64(err)
+                print(f"asyncio {key} round {r}: k={k} jacobi err={err:.3e}")
+    np.savez_compressed(os.path.join(OUT, "asyncio_graphs.npz"), **out)
+
+
+# ---------------------------------------------------------------- Titanic (config 1)
+def _prepare_titanic():
+    import pandas as pd
+    train_data = pd.read_csv(os.path.join(REF, "data/titanic/train.csv"))
+    df = train_data.drop(["Name", "Ticket", "Cabin", "Embarked"], axis=1)
+    df["Sex"] = (train_data["Sex"] == "male").astype(int) * 2 - 1   # nb used np.int (removed)
+    df = df.fillna({"Age": df["Age"].mean()})
+    df["Age"] /= 100
+    df["Fare"] /= 100
+    df["_bias"] = 1
+    feats, ans = df.drop(["Survived"], axis=1), (df["Survived"] * 2 - 1)
+    features = ["Pclass", "Sex", "Age", "SibSp", "Parch", "Fare", "_bias"]
+    X = feats[features].to_numpy().astype(np.float64)
+    y = ans.to_numpy().astype(np.float64)
+    return X, y
+
+
+def _sigmoid(x):
+    return 1.0 / (1.0 + np.exp(-x))
+
+
+def _grad(X, y, w, tau):
+    return -np.array([np.dot(y * _sigmoid(-y * (X @ w)), X[:, j]) for j in range(X.shape[1])]) \
+        / X.shape[0] + tau * w
+
+
+def make_titanic():
+    Xall, yall = _prepare_titanic()
+    nt = Xall.shape[0] // 10
+    tX, ty = Xall[:nt], yall[:nt]
+    X, y = Xall[nt:], yall[nt:]
+    # centralised GD (nb cell 5)
+    alpha, tau = 1e-1, 1e-4
+    w = np.zeros(X.shape[1])
+    best_w, best_err = w, None
+    for it in range(4000):
+        err = tau / 2 * np.sum(w ** 2) + -np.mean(np.log(_sigmoid(y * (X @ w))))
+        if best_err is None or err < best_err:
+            best_w, best_err = w, err
+        w -= alpha * np.power(it + 1, -0.5) * _grad(X, y, w, tau)
+    score = np.mean(((_sigmoid(tX @ w) >= 0.5).astype(int) * 2 - 1) == ty)
+    print("titanic centralised best_err", repr(best_err), "score", score)
+
+    # ring-8 asyncio consensus GD, eps=10 (1 mix per step), 4000 steps (nb cells 12, 14)
+    topo = [(i, (i + 1) % 8) for i in range(8)]
+    tokens = list(set(np.array(topo).flatten()))
+    shards, tmpX, tmpy = {}, X.copy(), y.copy()
+    for i in range(len(tokens)):
+        ln = len(tmpX) // (len(tokens) - i)
+        shards[tokens[i]] = (tmpX[:ln], tmpy[:ln])
+        tmpX, tmpy = tmpX[ln:], tmpy[ln:]
+    steps = 4000
+
+    async def learning_instance(Xs, ys, agent):
+        w = np.zeros(Xs.shape[1])
+        for it in range(steps):
+            g = _grad(Xs, ys, w, tau)
+            w -= alpha * np.power(it + 1, -0.5) * g
+            w = await agent.run_round(w, Xs.shape[0])
+        return w
+
+    async def main():
+        shutdown = asyncio.Queue()
+        net = ref_async.ConsensusNetwork(topo, shutdown)
+        agents = [ref_async.ConsensusAgent(t, convergence_eps=10) for t in net.tokens]
+        for a in agents:
+            net.register_agent(a)
+        serve = asyncio.create_task(net.serve())
+        res = await asyncio.gather(*[learning_instance(*shards[a.token], a) for a in agents])
+        await shutdown.put(ref_async.SHUTDOWN)
+        await serve
+        return [int(a.token) for a in agents], res
+
+    toks, ws = asyncio.run(main())
+    ws = np.stack(ws)
+    print("titanic ring8 eps=10 agent0", ws[toks.index(0)])
+    np.savez_compressed(
+        os.path.join(OUT, "titanic.npz"), X=Xall, y=yall, n_test=np.int64(nt),
+        central_best_err=np.float64(best_err), central_best_w=np.asarray(best_w),
+        central_final_w=w, central_score=np.float64(score),
+        ring8_tokens=np.asarray(toks), ring8_shard_sizes=np.asarray([len(shards[t][0]) for t in toks]),
+        ring8_eps10_final_w=ws, ring8_steps=np.int64(steps))
+
+
+def make_notebook_outputs():
+    rec = {
+        "source": "values printed in the reference notebooks (file:line of the .ipynb JSON)",
+        "titanic_central_best_err": 0.47854136193060065,          # Titanic...ipynb:159
+        "titanic_central_w_printed": [-0.331237, -1.044771, 0.012158, -0.116727, 0.031288,
+                                      0.425351, 0.271490],      # cell 6 (6 decimals)
+        "titanic_score": 0.797752808988764,                      # :257
+        "titanic_consensus_w_4000": [-0.33123728, -1.0447714, 0.01215817, -0.11672705,
+                                     0.03128755, 0.42535079, 0.27149002],   # cells 15-17
+        "titanic_grid5_10k_w": [-0.37763244, -1.15170579, 0.01359448, -0.15597462,
+                                -0.02271425, 0.54880775, 0.41782704],       # cell 18
+        "titanic_grid5_10k_score": 0.8089887640449438,
+        "grid5_perron_eps": 0.2375,                              # :860-869
+        "grid5_laplacian_eigs": [0.0, 3.0, 3.0, 5.0, 5.0],
+        "grid5_perron_eigs": [-0.1875, -0.1875, 0.2875, 0.2875, 1.0],
+        "grid5_convergence_speed": 0.18749999999999978,
+        "fa_kat_edges": [[0, 1], [0, 2], [0, 3], [1, 4], [4, 2]],  # Fast Averaging.ipynb:42-52
+        "fa_kat_w": [1 / 3, 1 / 3, 0.5, 1 / 3, 1 / 3],
+        "fa_kat_gamma": 0.6666666665339431,
+        "fa_hex_lattice_2_2_periodic_gamma": 0.5,                # :221,237
+        "fa_ring8_w": 1.0 / (3.0 - np.cos(2 * np.pi / 8)),       # analytic
+        "fa_ring8_gamma": (1.0 + np.cos(2 * np.pi / 8)) / (3.0 - np.cos(2 * np.pi / 8)),
+    }
+    with open(os.path.join(OUT, "notebook_outputs.json"), "w") as f:
+        json.dump(rec, f, indent=1)
+
+
+if __name__ == "__main__":
+    make_notebook_outputs()
+    make_mix_rr4()
+    make_ring8_fa()
+    make_mixer_ann()
+    make_asyncio()
+    make_titanic()
+    for fn in sorted(os.listdir(OUT)):
+        p = os.path.join(OUT, fn)
+        if fn.endswith((".npz", ".json")):
+            print(fn, os.path.getsize(p), hashlib.sha256(open(p, "rb").read()).hexdigest()[:16])

@@ -1,0 +1,65 @@
+"""CPU checks of the C-ABI boundary: libdlamd.so loads, exports every entry point that
+include/dlamd.h declares, and the ctypes struct layouts match the C compiler's."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "dlamd.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(dl_[a-z_]+)\s*\(", src)))
+
+
+def test_library_loads_and_exports_every_declared_symbol():
+    import distributed_learning_amd  # noqa: F401
+    from distributed_learning_amd import _lib
+    lib = _lib.load()
+    names = declared_functions()
+    assert len(names) >= 10
+    for n in names:
+        assert hasattr(lib, n), f"{n} declared in dlamd.h but not exported"
+        assert n in _lib.SIGNATURES, f"{n} has no ctypes signature"
+    assert lib.dl_abi_version() == _lib.ABI_VERSION
+    assert set(_lib.SIGNATURES) == set(names)
+
+
+def test_struct_layout_matches_c(tmp_path):
+    from distributed_learning_amd import _lib
+    prog = tmp_path / "layout.c"
+    prog.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "dlamd.h"\n'
+                    'int main(void){printf("%zu %zu %zu %zu %zu %zu %zu\\n",'
+                    'sizeof(dl_csr), sizeof(dl_mix_args), offsetof(dl_mix_args, W),'
+                    'offsetof(dl_mix_args, lr), offsetof(dl_mix_args, mean),'
+                    'sizeof(dl_mix_plan), sizeof(dl_perron_args));return 0;}\n')
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(prog), "-o", str(exe)],
+                   check=True)
+    c = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True,
+                                        check=True).stdout.split()]
+    py = [ctypes.sizeof(_lib.DlCsr), ctypes.sizeof(_lib.DlMixArgs), _lib.DlMixArgs.W.offset,
+          _lib.DlMixArgs.lr.offset, _lib.DlMixArgs.mean.offset, ctypes.sizeof(_lib.DlMixPlan),
+          ctypes.sizeof(_lib.DlPerronArgs)]
+    assert c == py
+
+
+def test_invalid_arguments_are_reported_not_crashed():
+    """Validation runs before any device call, so it is testable without a GPU."""
+    from distributed_learning_amd import _lib
+    lib = _lib.load()
+    args = _lib.DlMixArgs()  # all NULL / zero
+    rc = lib.dl_mix_round(ctypes.byref(args), None, 0, None)
+    assert rc == _lib.DL_ERR_INVALID
+    assert b"n_rows" in lib.dl_last_error()
+    with pytest.raises(ValueError):
+        _lib.check(rc, "dl_mix_round")
+    rc = lib.dl_deviation(None, 0, 0, 0, None, None, None, None, None, 0, None)
+    assert rc == _lib.DL_ERR_INVALID
+    rc = lib.dl_step_rows(None, 0, None, 0, 0.0, None, -1, 0, None, 0, None)
+    assert rc == _lib.DL_ERR_INVALID

@@ -54,15 +54,22 @@ def build_graph(n):
 
 
 def copy_ceiling(dev, nbytes=4 << 30, reps=10):
-    """Measured HBM ceiling: device-to-device copy of a 4 GiB buffer (read + write bytes)."""
-    a = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
+    """Measured HBM ceiling: float4 streaming copy (libdlamd dl_stream_copy) of a 4 GiB buffer,
+    counting read + write bytes."""
+    from distributed_learning_amd import _lib
+    lib = _lib.load()
+    a = torch.zeros(nbytes // 4, dtype=torch.float32, device=dev)
     b = torch.empty_like(a)
-    b.copy_(a)
+
+    def cp():
+        _lib.check(lib.dl_stream_copy(_lib.ptr(a), _lib.ptr(b), a.numel(),
+                                      _lib.stream_handle(dev)), "dl_stream_copy")
+    cp()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     s.record()
     for _ in range(reps):
-        b.copy_(a)
+        cp()
     e.record()
     torch.cuda.synchronize()
     t = s.elapsed_time(e) / 1e3 / reps

@@ -65,6 +65,7 @@ struct Plan {
     dl_mix_plan pub;
     int chunks;
     bool dev;
+    uint32_t csr_off, scratch_off;
 };
 
 int next_pow2_chunks(int64_t n_params) {
@@ -90,10 +91,9 @@ int plan_mix(const dl_mix_args *a, Plan *pl) {
     if (csr > 0 && R <= 65535 && !force_gather) {
         for (int c = cmax; c >= 1; c >>= 1) {
             if ((int64_t)R * c > (int64_t)dl::kRowsPerThread * dl::kTileThreads) continue;
-            int64_t tile = (int64_t)R * c * 16;
+            const int64_t tile = (int64_t)R * c * 16;
             const int64_t scratch = want_dev ? (int64_t)(dl::kTileThreads / 64) * c * 16 : 0;
-            if (tile < scratch) tile = scratch;
-            const int64_t lds = tile + csr;
+            const int64_t lds = tile + csr + scratch;
             if (lds > dl::kLdsBytes) continue;
             const int64_t T = 4 * c;
             const int64_t n_tiles = (a->n_params + T - 1) / T;
@@ -109,6 +109,8 @@ int plan_mix(const dl_mix_args *a, Plan *pl) {
             pl->pub.n_tiles = (int32_t)n_tiles;
             pl->pub.regular = reg;
             pl->chunks = c;
+            pl->csr_off = (uint32_t)tile;
+            pl->scratch_off = (uint32_t)(tile + csr);
             return DL_OK;
         }
     }
@@ -178,8 +180,8 @@ dl::TileArgs tile_args(const dl_mix_args *a) {
     // the float4 kernel addresses rows with 32-bit byte offsets from the tile base
     const int64_t lim = (int64_t)1 << 32;
     const int64_t R = a->W.n_rows;
-    if ((R * a->ldx + 128) * 4 >= lim || (R * a->ldy + 128) * 4 >= lim ||
-        (a->g && (R * a->ldg + 128) * 4 >= lim))
+    if (((R - 1) * a->ldx + 128) * 4 >= lim || ((R - 1) * a->ldy + 128) * 4 >= lim ||
+        (a->g && ((R - 1) * a->ldg + 128) * 4 >= lim))
         vec = false;
     t.vec = vec ? 1 : 0;
     t.mean = a->mean;
@@ -279,7 +281,8 @@ int dl_mix_round(const dl_mix_args *args, void *workspace, size_t ws_bytes, dl_s
         const size_t need = align_up((size_t)(grid_full + grid_tail) * Nr * 4);
         if (pl.dev && ws_bytes < need)
             return fail(DL_ERR_WORKSPACE, "dl_mix_round: workspace %zu < %zu bytes", ws_bytes, need);
-        t.csr_off = (uint32_t)(pl.pub.lds_bytes - (int)dl::csr_lds_bytes(Nr, t.nnz, t.regular > 0));
+        t.csr_off = pl.csr_off;
+        t.scratch_off = pl.scratch_off;
         float *partial = pl.dev ? reinterpret_cast<float *>(ws) : nullptr;
         if (grid_full > 0) {
             t.n_tiles = (int32_t)n_full;
@@ -348,7 +351,7 @@ int dl_deviation(const float *x, int64_t ldx, int32_t n_rows, int64_t n_params,
             const int lds = (dl::kTileThreads / 64) * c * 16;
             const int64_t T = 4 * c;
             const bool vec = aligned16(x) && ldx % 4 == 0 && (!mean_out || aligned16(mean_out)) &&
-                             ((int64_t)n_rows * ldx + 128) * 4 < ((int64_t)1 << 32);
+                             ((int64_t)(n_rows - 1) * ldx + 128) * 4 < ((int64_t)1 << 32);
             const int64_t n_tiles = (n_params + T - 1) / T;
             const int64_t n_full = vec ? n_params / T : 0;
             const int64_t n_tail = n_tiles - n_full;
@@ -421,6 +424,14 @@ int dl_step_rows(const float *x, int64_t ldx, const float *g, int64_t ldg, float
     hipError_t e = dl::launch_step_rows(x, ldx, g, ldg, lr, rows, n_sel, n_params, out, ldo,
                                         static_cast<hipStream_t>(stream));
     return e == hipSuccess ? DL_OK : hip_fail(e, "step_rows launch");
+}
+
+int dl_stream_copy(const float *src, float *dst, int64_t n_floats, dl_stream_t stream) {
+    g_err.clear();
+    if (!src || !dst || n_floats < 0 || (n_floats & 3) || !aligned16(src) || !aligned16(dst))
+        return fail(DL_ERR_INVALID, "dl_stream_copy: needs 16-byte aligned buffers, n %% 4 == 0");
+    hipError_t e = dl::launch_stream_copy(src, dst, n_floats, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? DL_OK : hip_fail(e, "stream_copy launch");
 }
 
 size_t dl_perron_workspace_bytes(int32_t dtype, int32_t n_rows, int64_t n_params) {

@@ -32,6 +32,7 @@ struct TileArgs {
     float lr;
     int32_t vec;      // 1: x/g/y/halo 16-byte aligned and ld % 4 == 0
     uint32_t csr_off; // byte offset of the staged CSR in LDS
+    uint32_t scratch_off; // byte offset of the 16 x C float4 mean scratch in LDS
     float *dev_partial;  // [gridDim.x][n_rows] per-workgroup partial ||y_a - mean||^2
     float *mean;         // [n_params] nullable
 };
@@ -49,6 +50,7 @@ hipError_t launch_column_sum(const float *x, int64_t ldx, int n_rows, int64_t n_
 hipError_t launch_dev_rows(const float *x, int64_t ldx, int n_rows, int64_t n_params,
                            const float *mean, float *partial, int nparts, hipStream_t s);
 int dev_rows_parts(int64_t n_params);
+hipError_t launch_stream_copy(const float *src, float *dst, int64_t n_floats, hipStream_t s);
 hipError_t launch_max_column_std(const float *x, int64_t ldx, int n_rows, int64_t n_params,
                                  float *out, hipStream_t s);
 hipError_t launch_step_rows(const float *x, int64_t ldx, const float *g, int64_t ldg, float lr,

@@ -127,17 +127,22 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
     const int reg = a.regular;
 
     // FAST-path byte offsets: lane row s / chunk c; pass k adds k * step
-    const uint32_t ox = (uint32_t)(((int64_t)s * a.ldx + 4 * c) * 4);
+    uint32_t ox = (uint32_t)(((int64_t)s * a.ldx + 4 * c) * 4);
     const uint32_t sx = (uint32_t)((int64_t)SLOTS * a.ldx * 4);
-    const uint32_t og = SGD ? (uint32_t)(((int64_t)s * a.ldg + 4 * c) * 4) : 0u;
+    uint32_t og = SGD ? (uint32_t)(((int64_t)s * a.ldg + 4 * c) * 4) : 0u;
     const uint32_t sg = SGD ? (uint32_t)((int64_t)SLOTS * a.ldg * 4) : 0u;
-    const uint32_t oy = (uint32_t)(((int64_t)s * a.ldy + 4 * c) * 4);
+    uint32_t oy = (uint32_t)(((int64_t)s * a.ldy + 4 * c) * 4);
     const uint32_t sy = (uint32_t)((int64_t)SLOTS * a.ldy * 4);
+    float4 *scratch = reinterpret_cast<float4 *>(smem + a.scratch_off);
 
     float4 px[KV], pg[KV];
-    float dacc[KV];
+    // per-agent ||y - mean||^2 accumulators.  When KV <= C they are spread over the C lanes of a
+    // row group (lane c keeps pass k == c): one register instead of KV.
+    constexpr bool DIST = KV <= C;
+    constexpr int ND = DIST ? 1 : KV;
+    float dacc[ND];
 #pragma unroll
-    for (int k = 0; k < KV; ++k) dacc[k] = 0.f;
+    for (int k = 0; k < ND; ++k) dacc[k] = 0.f;
 
     auto prefetch = [&](int tile_id) {
         const int64_t col0 = a.col_base + (int64_t)tile_id * T;
@@ -165,12 +170,62 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
         }
     };
 
+    // y_a = sum_e w_e * t_{col_e} for agent ag, chunk c: left fold in CSR order from +0.0
+    // (mixer.py:47); reads only LDS.
+    auto mix_row = [&](int ag) {
+        int e0, e1;
+        if (reg) {
+            e0 = ag * reg;
+            e1 = e0 + reg;
+        } else {
+            e0 = lrp[ag];
+            e1 = lrp[ag + 1];
+        }
+        float4 acc = zero4();
+        for (int e = e0; e < e1; ++e) axpy4(acc, lw[e], tile[lcol[e] * C + c]);
+        return acc;
+    };
+
+    // column mean of the tile over all agents from per-thread partial sums: thread -> wave
+    // (lanes with the same c) -> LDS scratch -> every thread sums the 16 wave partials in order
+    auto tile_mean = [&](float4 cs) {
+#pragma unroll
+        for (int m = C; m < 64; m <<= 1) cs = shfl_xor4(cs, m);
+        const int wave = tid >> 6, lane = tid & 63;
+        if (lane < C) scratch[wave * C + lane] = cs;
+        __syncthreads();
+        float4 mean = zero4();
+#pragma unroll
+        for (int wv = 0; wv < NT / 64; ++wv) add4(mean, scratch[wv * C + c]);
+        const float n = (float)Nr;
+        mean.x = mean.x / n;
+        mean.y = mean.y / n;
+        mean.z = mean.z / n;
+        mean.w = mean.w / n;
+        return mean;
+    };
+
+    auto dev_add = [&](int k, float4 y, float4 mean) {  // k may be a runtime pass index
+        const float dx = y.x - mean.x, dy = y.y - mean.y;
+        const float dz = y.z - mean.z, dw = y.w - mean.w;
+        float v = (dx * dx + dy * dy) + (dz * dz + dw * dw);
+        if (DIST) {
+#pragma unroll
+            for (int m = 1; m < C; m <<= 1) v += __shfl_xor(v, m);  // sum over the row group
+            dacc[0] += (c == k) ? v : 0.f;
+        } else {
+#pragma unroll
+            for (int j = 0; j < ND; ++j) dacc[j] += (j == k) ? v : 0.f;
+        }
+    };
+
     int tile_id = blockIdx.x;
     if (tile_id < a.n_tiles) prefetch(tile_id);
     for (; tile_id < a.n_tiles; tile_id += gridDim.x) {
+        // opaque per tile: keeps LICM from hoisting one offset register per pass
+        asm volatile("" : "+v"(ox), "+v"(og), "+v"(oy));
         const int64_t col0 = a.col_base + (int64_t)tile_id * T;
         const int nxt = tile_id + gridDim.x;
-        float4 out[KV];
         if (MIX) {
             // stage the (stepped) tile of every source row in LDS
 #pragma unroll
@@ -182,73 +237,62 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
             }
             __syncthreads();
             if (nxt < a.n_tiles) prefetch(nxt);  // lands while we mix from LDS
-            // y_a = sum_e w_e * t_{col_e}, left fold in CSR order from +0.0 (mixer.py:47)
             float *yt = a.y + col0;
-#pragma unroll
+            float4 cs = zero4();
+            // passes stay rolled: interleaving them would hold KV accumulators at once on top
+            // of the 2*KV prefetch registers
+#pragma unroll 1
             for (int k = 0; k < KV; ++k) {
                 const int ag = s + k * SLOTS;
-                float4 acc = zero4();
                 if (ag < Nr) {
-                    int e0, e1;
-                    if (reg) {
-                        e0 = ag * reg;
-                        e1 = e0 + reg;
-                    } else {
-                        e0 = lrp[ag];
-                        e1 = lrp[ag + 1];
-                    }
-                    for (int e = e0; e < e1; ++e) axpy4(acc, lw[e], tile[lcol[e] * C + c]);
+                    const float4 acc = mix_row(ag);
                     if (FAST)
-                        *at(yt, oy + k * sy) = acc;
+                        *at(yt, oy + (uint32_t)k * sy) = acc;
                     else
                         st4(a.y + (int64_t)ag * a.ldy, col0 + 4 * c, P, false, acc);
+                    if (DEV) add4(cs, acc);
                 }
-                if (DEV) out[k] = acc;
+            }
+            if (DEV) {
+                const float4 mean = tile_mean(cs);
+                if (a.mean != nullptr && s == 0) st4(a.mean, col0 + 4 * c, P, FAST, mean);
+                // second LDS pass: recompute y (same order, same bits) instead of holding it
+#pragma unroll 1
+                for (int k = 0; k < KV; ++k) {
+                    const int ag = s + k * SLOTS;
+                    if (ag < Nr) dev_add(k, mix_row(ag), mean);
+                }
             }
         } else {
-#pragma unroll
-            for (int k = 0; k < KV; ++k) out[k] = (s + k * SLOTS < Nr) ? px[k] : zero4();
-            if (nxt < a.n_tiles) prefetch(nxt);
-        }
-        if (DEV) {
-            // column sums of this tile over all agents: thread -> wave (same c) -> LDS
+            float4 cur[KV];
             float4 cs = zero4();
 #pragma unroll
-            for (int k = 0; k < KV; ++k) add4(cs, out[k]);  // missing rows hold zeros
-#pragma unroll
-            for (int m = C; m < 64; m <<= 1) cs = shfl_xor4(cs, m);
-            if (MIX) __syncthreads();  // every LDS tile read is done: reuse it as scratch
-            const int wave = tid >> 6, lane = tid & 63;
-            if (lane < C) tile[wave * C + lane] = cs;
-            __syncthreads();
-            float4 mean = zero4();
-#pragma unroll
-            for (int wv = 0; wv < NT / 64; ++wv) add4(mean, tile[wv * C + c]);
-            const float n = (float)Nr;
-            mean.x = mean.x / n;
-            mean.y = mean.y / n;
-            mean.z = mean.z / n;
-            mean.w = mean.w / n;
+            for (int k = 0; k < KV; ++k) {
+                cur[k] = px[k];
+                if (s + k * SLOTS < Nr) add4(cs, cur[k]);
+            }
+            if (nxt < a.n_tiles) prefetch(nxt);
+            const float4 mean = tile_mean(cs);
             if (a.mean != nullptr && s == 0) st4(a.mean, col0 + 4 * c, P, FAST, mean);
 #pragma unroll
-            for (int k = 0; k < KV; ++k) {
-                if (s + k * SLOTS < Nr) {
-                    const float dx = out[k].x - mean.x, dy = out[k].y - mean.y;
-                    const float dz = out[k].z - mean.z, dw = out[k].w - mean.w;
-                    dacc[k] += (dx * dx + dy * dy) + (dz * dz + dw * dw);
-                }
-            }
+            for (int k = 0; k < KV; ++k)
+                if (s + k * SLOTS < Nr) dev_add(k, cur[k], mean);
         }
-        __syncthreads();  // LDS reused by the next tile
+        __syncthreads();  // tile and scratch are rewritten by the next iteration
     }
     if (DEV) {
+        if (DIST) {
+            const int ag = s + c * SLOTS;
+            if (c < KV && ag < Nr) a.dev_partial[(int64_t)blockIdx.x * Nr + ag] = dacc[0];
+        } else {
 #pragma unroll
-        for (int k = 0; k < KV; ++k) {
-            float v = dacc[k];
+            for (int k = 0; k < ND; ++k) {
+                float v = dacc[k];
 #pragma unroll
-            for (int m = 1; m < C; m <<= 1) v += __shfl_xor(v, m);
-            const int ag = s + k * SLOTS;
-            if (c == 0 && ag < Nr) a.dev_partial[(int64_t)blockIdx.x * Nr + ag] = v;
+                for (int m = 1; m < C; m <<= 1) v += __shfl_xor(v, m);
+                const int ag = s + k * SLOTS;
+                if (c == 0 && ag < Nr) a.dev_partial[(int64_t)blockIdx.x * Nr + ag] = v;
+            }
         }
     }
 }
@@ -279,28 +323,43 @@ __global__ void __launch_bounds__(256) mix_gather_kernel(TileArgs a) {
     st4(a.y + (int64_t)ag * a.ldy, c0, P, vec, acc);
 }
 
-// dev_sq[a] = sum_b partial[b][a] (fixed order, fp64); dev_max = max_a sqrt(dev_sq[a]).
+// dev_sq[a] = sum_b partial[b][a] (fixed order per lane group, fp64), dev_max = max sqrt.
+// Block = 64 agents x 16 part-lanes; each lane sums parts j, j+16, ... then LDS combine in a
+// fixed order, so the result is deterministic.  dev_max (zeroed by the launcher) takes one
+// atomicMax per block on the bits of a non-negative float.
 __global__ void __launch_bounds__(1024) dev_reduce_kernel(const float *__restrict__ partial,
                                                           int nparts, int n_rows,
                                                           float *__restrict__ dev_sq,
-                                                          float *__restrict__ dev_max) {
+                                                          unsigned int *__restrict__ dev_max) {
+    __shared__ double red[16][64];
     __shared__ float smax[16];
-    float mx = 0.f;
-    for (int ag = threadIdx.x; ag < n_rows; ag += 1024) {
-        double s = 0.0;
-        for (int b = 0; b < nparts; ++b) s += (double)partial[(int64_t)b * n_rows + ag];
-        const float f = (float)s;
-        if (dev_sq) dev_sq[ag] = f;
-        mx = fmaxf(mx, sqrtf(f));
-    }
-    for (int m = 32; m >= 1; m >>= 1) mx = fmaxf(mx, __shfl_xor(mx, m));
-    if ((threadIdx.x & 63) == 0) smax[threadIdx.x >> 6] = mx;
+    const int ai = threadIdx.x & 63, j = threadIdx.x >> 6;
+    const int ag = blockIdx.x * 64 + ai;
+    double s = 0.0;
+    if (ag < n_rows)
+        for (int b = j; b < nparts; b += 16) s += (double)partial[(int64_t)b * n_rows + ag];
+    red[j][ai] = s;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        float v = 0.f;
-        for (int i = 0; i < 16; ++i) v = fmaxf(v, smax[i]);
-        if (dev_max) dev_max[0] = v;
+    float f = 0.f;
+    if (j == 0 && ag < n_rows) {
+        double t = red[0][ai];
+        for (int k = 1; k < 16; ++k) t += red[k][ai];
+        f = (float)t;
+        if (dev_sq) dev_sq[ag] = f;
     }
+    if (j == 0) {
+        float mx = sqrtf(f);
+        for (int m = 32; m >= 1; m >>= 1) mx = fmaxf(mx, __shfl_xor(mx, m));
+        if (ai == 0 && dev_max) atomicMax(dev_max, __float_as_uint(mx));
+    }
+}
+
+// Streaming copy (HBM ceiling measurement): float4, grid-stride.
+__global__ void __launch_bounds__(256) stream_copy_kernel(const float4 *__restrict__ src,
+                                                          float4 *__restrict__ dst, int64_t n4) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4;
+         i += (int64_t)gridDim.x * 256)
+        dst[i] = src[i];
 }
 
 template <int C, int KV, bool SGD, bool DEV, bool MIX, bool HALO, bool FAST>
@@ -385,8 +444,22 @@ hipError_t launch_mix_gather(const TileArgs &a, bool sgd, hipStream_t s) {
 
 hipError_t launch_dev_reduce(const float *partial, int nparts, int n_rows, float *dev_sq,
                              float *dev_max, hipStream_t s) {
-    hipLaunchKernelGGL(dev_reduce_kernel, dim3(1), dim3(1024), 0, s, partial, nparts, n_rows,
-                       dev_sq, dev_max);
+    if (dev_max) {
+        hipError_t e = hipMemsetAsync(dev_max, 0, sizeof(float), s);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(dev_reduce_kernel, dim3((n_rows + 63) / 64), dim3(1024), 0, s, partial,
+                       nparts, n_rows, dev_sq, reinterpret_cast<unsigned int *>(dev_max));
+    return hipGetLastError();
+}
+
+hipError_t launch_stream_copy(const float *src, float *dst, int64_t n_floats, hipStream_t s) {
+    const int64_t n4 = n_floats / 4;
+    int64_t grid = (n4 + 255) / 256;
+    if (grid > 256 * 16) grid = 256 * 16;
+    if (grid < 1) grid = 1;
+    hipLaunchKernelGGL(stream_copy_kernel, dim3((unsigned)grid), dim3(256), 0, s,
+                       reinterpret_cast<const float4 *>(src), reinterpret_cast<float4 *>(dst), n4);
     return hipGetLastError();
 }
 

@@ -131,8 +131,10 @@ def main():
     X = torch.randn(n, P, device=dev, generator=g)
     G = torch.randn(n, P, device=dev, generator=g) if sgd else None
     eng = engine.GossipEngine(csr, P, device=dev, X=X)
-    plan = eng.plan(G=G, deviation=True)
-    dev_sq_all = torch.empty(n, dtype=torch.float32, device=dev)
+    if G is not None:
+        G = eng.layout_like(G)        # synthetic gradient resident in the engine's layout
+    del X
+    plan = eng.plan(deviation=True)
 
     def step():
         eng.round(G=G, lr=lr, deviation=True)

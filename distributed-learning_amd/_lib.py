@@ -29,7 +29,7 @@ class DlMixArgs(ctypes.Structure):
     _fields_ = [("x", _vp), ("ldx", _i64), ("y", _vp), ("ldy", _i64), ("n_params", _i64),
                 ("W", DlCsr), ("g", _vp), ("ldg", _i64), ("lr", _f32), ("halo", _vp),
                 ("ldh", _i64), ("n_halo", _i32), ("dev_sq", _vp), ("dev_max", _vp),
-                ("mean", _vp)]
+                ("mean", _vp), ("tile_cols", _i32)]
 
 
 class DlMixPlan(ctypes.Structure):
@@ -40,7 +40,8 @@ class DlMixPlan(ctypes.Structure):
 class DlPerronArgs(ctypes.Structure):
     _fields_ = [("dtype", _i32), ("y", _vp), ("ldy", _i64), ("n_rows", _i32), ("n_params", _i64),
                 ("row_ptr", _vp), ("col", _vp), ("weight", _vp), ("mean_weight", _f64),
-                ("eps", _f64), ("conv_eps", _f64), ("max_iter", _i32), ("iters_out", _vp)]
+                ("eps", _f64), ("conv_eps", _f64), ("max_iter", _i32), ("iters_out", _vp),
+                ("conv_eps_rows", _vp)]
 
 
 # exported symbol -> (restype, argtypes); tests check every one is exported
@@ -49,9 +50,13 @@ SIGNATURES = {
     "dl_last_error": (ctypes.c_char_p, []),
     "dl_mix_workspace_bytes": (_sz, [_i32, _i32, _i64]),
     "dl_mix_plan_query": (_i32, [ctypes.POINTER(DlMixArgs), ctypes.POINTER(DlMixPlan)]),
+    "dl_mix_plan_shape": (_i32, [_i32, _i32, _i64, _i32, _i32, _i32, ctypes.POINTER(DlMixPlan)]),
     "dl_mix_round": (_i32, [ctypes.POINTER(DlMixArgs), _vp, _sz, _vp]),
     "dl_deviation_workspace_bytes": (_sz, [_i32, _i64]),
     "dl_deviation": (_i32, [_vp, _i64, _i32, _i64, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "dl_deviation_tiled": (_i32, [_vp, _i32, _i64, _i32, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "dl_to_tiled": (_i32, [_vp, _i64, _i32, _i64, _i32, _vp, _vp]),
+    "dl_from_tiled": (_i32, [_vp, _i32, _i64, _i32, _vp, _i64, _vp]),
     "dl_column_sum": (_i32, [_vp, _i64, _i32, _i64, _vp, _vp]),
     "dl_max_column_std": (_i32, [_vp, _i64, _i32, _i64, _vp, _vp]),
     "dl_step_rows": (_i32, [_vp, _i64, _vp, _i64, _f32, _vp, _i32, _i64, _vp, _i64, _vp]),

@@ -95,7 +95,7 @@ template <typename DT>
 __device__ __forceinline__ DT perron_update(const DT *cur, int r, int p, int TP,
                                             const int32_t *__restrict__ rp,
                                             const int32_t *__restrict__ col, double eps,
-                                            DT conv, bool &fail) {
+                                            DT conv, const double *conv_rows, bool &fail) {
     const int e0 = rp[r], e1 = rp[r + 1];
     const int cnt = e1 - e0;
     DT s = (DT)0;
@@ -107,6 +107,7 @@ __device__ __forceinline__ DT perron_update(const DT *cur, int r, int p, int TP,
     const DT t1 = cur[r * TP + p] * dcoef;
     const DT t2 = (DT)eps * s;
     const DT yn = t1 + t2;
+    if (conv_rows) conv = (DT)conv_rows[r];
     for (int e = e0; e < e1; ++e) {
         const DT v = cur[col[e] * TP + p];
         if (!((yn - v) <= conv)) fail = true;
@@ -146,7 +147,7 @@ __global__ void __launch_bounds__(1024) perron_single_kernel(PerronArgs a) {
         bool fail = false;
         for (int i = threadIdx.x; i < E; i += 1024) {
             const int r = i / TP, p = i - r * TP;
-            nxt[i] = perron_update<DT>(cur, r, p, TP, a.rowptr, a.col, a.eps, conv, fail);
+            nxt[i] = perron_update<DT>(cur, r, p, TP, a.rowptr, a.col, a.eps, conv, a.conv_rows, fail);
         }
         if (__any(fail) && (threadIdx.x & 63) == 0) atomicOr(&flags[it & 1], 1);
         __syncthreads();
@@ -192,14 +193,45 @@ __global__ void __launch_bounds__(1024) perron_step_kernel(PerronArgs a, int TP,
         const int r = i / TP, p = i - r * TP;
         if (p0 + p >= P) continue;
         bool f = false;
-        const DT yn = perron_update<DT>(cur, r, p, TP, a.rowptr, a.col, a.eps, conv, f);
+        const DT yn = perron_update<DT>(cur, r, p, TP, a.rowptr, a.col, a.eps, conv, a.conv_rows, f);
         fail |= f;
         yout[(int64_t)r * ldout + p0 + p] = yn;
     }
     if (__any(fail) && (threadIdx.x & 63) == 0) atomicOr(a.notconv, 1);
 }
 
+// row-major [n_rows][ld] <-> column-tiled [n_tiles][n_rows][T] (tail columns of the last tile
+// are zero-filled when packing and skipped when unpacking)
+__global__ void __launch_bounds__(256) tile_convert_kernel(const float *__restrict__ src,
+                                                           float *__restrict__ dst, int64_t ld,
+                                                           int n_rows, int64_t n_params, int T,
+                                                           int to_tiled) {
+    const int64_t n_tiles = (n_params + T - 1) / T;
+    const int64_t total = n_tiles * n_rows * T;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * 256) {
+        const int64_t t = i / ((int64_t)n_rows * T);
+        const int64_t rem = i - t * n_rows * T;
+        const int64_t r = rem / T;
+        const int64_t col = t * T + (rem - r * T);
+        if (to_tiled)
+            dst[i] = col < n_params ? src[r * ld + col] : 0.f;
+        else if (col < n_params)
+            dst[r * ld + col] = src[i];
+    }
+}
+
 }  // namespace
+
+hipError_t launch_tile_convert(const float *src, float *dst, int64_t ld, int n_rows, int64_t n_params,
+                               int tile_cols, bool to_tiled, hipStream_t s) {
+    const int64_t total = ((n_params + tile_cols - 1) / tile_cols) * n_rows * tile_cols;
+    int64_t grid = (total + 255) / 256;
+    if (grid > 8192) grid = 8192;
+    hipLaunchKernelGGL(tile_convert_kernel, dim3((unsigned)grid), dim3(256), 0, s, src, dst, ld,
+                       n_rows, n_params, tile_cols, (int)to_tiled);
+    return hipGetLastError();
+}
 
 int dev_rows_parts(int64_t n_params) {
     int64_t parts = (n_params + 8191) / 8192;

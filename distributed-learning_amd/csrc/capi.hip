@@ -88,6 +88,30 @@ int plan_mix(const dl_mix_args *a, Plan *pl) {
     // DLAMD_FORCE_GATHER=1 (tests only) forces the general gather kernel
     const char *force = getenv("DLAMD_FORCE_GATHER");
     const bool force_gather = force && force[0] == '1';
+    if (a->tile_cols > 0) {  // column-tiled layout: the tile width is fixed by the data
+        const int c = a->tile_cols / 4;
+        const int64_t tile = (int64_t)R * c * 16;
+        const int64_t scratch = want_dev ? (int64_t)(dl::kTileThreads / 64) * c * 16 : 0;
+        const int64_t lds = tile + csr + scratch;
+        if (csr == 0 || R > 65535 || (int64_t)R * c > (int64_t)dl::kRowsPerThread * dl::kTileThreads ||
+            lds > dl::kLdsBytes)
+            return fail(DL_ERR_INVALID, "dl_mix_round: tile_cols %d does not fit this graph "
+                                        "(%d rows); query dl_mix_plan_query on row-major args",
+                        a->tile_cols, R);
+        const int64_t n_tiles = (a->n_params + a->tile_cols - 1) / a->tile_cols;
+        int64_t grid = (int64_t)device_cus() * ((dl::kLdsBytes / lds) >= 2 ? 2 : 1);
+        if (grid > n_tiles) grid = n_tiles;
+        pl->pub.path = 1;
+        pl->pub.tile_cols = a->tile_cols;
+        pl->pub.grid = (int32_t)grid;
+        pl->pub.lds_bytes = (int32_t)lds;
+        pl->pub.n_tiles = (int32_t)n_tiles;
+        pl->pub.regular = reg;
+        pl->chunks = c;
+        pl->csr_off = (uint32_t)tile;
+        pl->scratch_off = (uint32_t)(tile + csr);
+        return DL_OK;
+    }
     if (csr > 0 && R <= 65535 && !force_gather) {
         for (int c = cmax; c >= 1; c >>= 1) {
             if ((int64_t)R * c > (int64_t)dl::kRowsPerThread * dl::kTileThreads) continue;
@@ -132,11 +156,19 @@ int check_mix_args(const dl_mix_args *a) {
     if (W.nnz < 0) return fail(DL_ERR_INVALID, "dl_mix_round: nnz < 0");
     if (!a->x || !a->y || !W.row_ptr || (W.nnz > 0 && (!W.col || !W.w)))
         return fail(DL_ERR_INVALID, "dl_mix_round: null x/y/row_ptr/col/w");
-    if (a->ldx < a->n_params || a->ldy < a->n_params)
+    if (a->tile_cols == 0 && (a->ldx < a->n_params || a->ldy < a->n_params))
         return fail(DL_ERR_INVALID, "dl_mix_round: ldx/ldy smaller than n_params");
-    if (a->g && a->ldg < a->n_params) return fail(DL_ERR_INVALID, "dl_mix_round: ldg < n_params");
+    if (a->tile_cols == 0 && a->g && a->ldg < a->n_params)
+        return fail(DL_ERR_INVALID, "dl_mix_round: ldg < n_params");
     if (a->n_halo > 0 && (!a->halo || a->ldh < a->n_params))
         return fail(DL_ERR_INVALID, "dl_mix_round: n_halo > 0 needs halo with ldh >= n_params");
+    if (a->tile_cols < 0 || (a->tile_cols > 0 && (a->tile_cols % 4 || a->tile_cols < 16 ||
+                                                   a->tile_cols > 4 * dl::kMaxChunks ||
+                                                   (a->tile_cols & (a->tile_cols - 1)))))
+        return fail(DL_ERR_INVALID, "dl_mix_round: tile_cols must be 0 or a power of two in [16, %d]",
+                    4 * dl::kMaxChunks);
+    if (a->tile_cols > 0 && a->n_halo > 0)
+        return fail(DL_ERR_INVALID, "dl_mix_round: the column-tiled layout takes no halo rows");
     if (W.uniform_row_nnz < 0 ||
         (W.uniform_row_nnz > 0 && (int64_t)W.uniform_row_nnz * W.n_rows != W.nnz))
         return fail(DL_ERR_INVALID, "dl_mix_round: uniform_row_nnz * n_rows != nnz");
@@ -144,11 +176,14 @@ int check_mix_args(const dl_mix_args *a) {
         return fail(DL_ERR_INVALID,
                     "dl_mix_round: fused deviation needs every agent local (n_halo == 0); use "
                     "dl_column_sum + dl_deviation with a global mean");
-    const size_t xb = ((size_t)(W.n_rows - 1) * a->ldx + a->n_params) * 4;
-    const size_t yb = ((size_t)(W.n_rows - 1) * a->ldy + a->n_params) * 4;
+    const size_t tiled_b = a->tile_cols > 0 ? (size_t)((a->n_params + a->tile_cols - 1) /
+                                                       a->tile_cols) * a->tile_cols * W.n_rows * 4
+                                            : 0;
+    const size_t xb = a->tile_cols ? tiled_b : ((size_t)(W.n_rows - 1) * a->ldx + a->n_params) * 4;
+    const size_t yb = a->tile_cols ? tiled_b : ((size_t)(W.n_rows - 1) * a->ldy + a->n_params) * 4;
     if (overlaps(a->x, xb, a->y, yb)) return fail(DL_ERR_INVALID, "dl_mix_round: y overlaps x");
     if (a->g) {
-        const size_t gb = ((size_t)(W.n_rows - 1) * a->ldg + a->n_params) * 4;
+        const size_t gb = a->tile_cols ? tiled_b : ((size_t)(W.n_rows - 1) * a->ldg + a->n_params) * 4;
         if (overlaps(a->g, gb, a->y, yb)) return fail(DL_ERR_INVALID, "dl_mix_round: y overlaps g");
     }
     return DL_OK;
@@ -180,9 +215,14 @@ dl::TileArgs tile_args(const dl_mix_args *a) {
     // the float4 kernel addresses rows with 32-bit byte offsets from the tile base
     const int64_t lim = (int64_t)1 << 32;
     const int64_t R = a->W.n_rows;
-    if (((R - 1) * a->ldx + 128) * 4 >= lim || ((R - 1) * a->ldy + 128) * 4 >= lim ||
-        (a->g && ((R - 1) * a->ldg + 128) * 4 >= lim))
+    if (a->tile_cols > 0) {
+        vec = aligned16(a->x) && aligned16(a->y) && (!a->g || aligned16(a->g)) &&
+              (!a->mean || aligned16(a->mean));
+        t.tiled = 1;
+    } else if (((R - 1) * a->ldx + 128) * 4 >= lim || ((R - 1) * a->ldy + 128) * 4 >= lim ||
+               (a->g && ((R - 1) * a->ldg + 128) * 4 >= lim)) {
         vec = false;
+    }
     t.vec = vec ? 1 : 0;
     t.mean = a->mean;
     return t;
@@ -255,6 +295,26 @@ int dl_mix_plan_query(const dl_mix_args *args, dl_mix_plan *plan) {
     return DL_OK;
 }
 
+int dl_mix_plan_shape(int32_t n_rows, int32_t n_halo, int64_t n_params, int32_t nnz,
+                      int32_t uniform_row_nnz, int32_t deviation, dl_mix_plan *plan) {
+    g_err.clear();
+    if (!plan || n_rows <= 0 || n_halo < 0 || n_params <= 0 || nnz < 0)
+        return fail(DL_ERR_INVALID, "dl_mix_plan_shape: bad arguments");
+    dl_mix_args a{};
+    a.W.n_rows = n_rows;
+    a.W.nnz = nnz;
+    a.W.uniform_row_nnz = uniform_row_nnz;
+    a.n_halo = n_halo;
+    a.n_params = n_params;
+    float dummy;
+    if (deviation) a.dev_max = &dummy;
+    Plan pl;
+    int rc = plan_mix(&a, &pl);
+    if (rc) return rc;
+    *plan = pl.pub;
+    return DL_OK;
+}
+
 int dl_mix_round(const dl_mix_args *args, void *workspace, size_t ws_bytes, dl_stream_t stream) {
     g_err.clear();
     int rc = check_mix_args(args);
@@ -274,7 +334,18 @@ int dl_mix_round(const dl_mix_args *args, void *workspace, size_t ws_bytes, dl_s
         // full tiles on the branch-free float4 kernel, the ragged tail tile (and unaligned
         // operands) on the guarded one; each launch writes its own deviation partial rows
         const int64_t T = pl.pub.tile_cols;
-        const int64_t n_full = t.vec ? args->n_params / T : 0;
+        if (t.tiled) {
+            if (!t.vec)
+                return fail(DL_ERR_INVALID, "dl_mix_round: tiled operands must be 16-byte aligned");
+            t.xts = t.gts = t.yts = (int64_t)Nr * T * 4;
+            t.xrs = t.grs = t.yrs = (uint32_t)(T * 4);
+        } else {
+            t.xts = t.gts = t.yts = T * 4;
+            t.xrs = (uint32_t)(args->ldx * 4);
+            t.grs = (uint32_t)(args->ldg * 4);
+            t.yrs = (uint32_t)(args->ldy * 4);
+        }
+        const int64_t n_full = t.tiled ? pl.pub.n_tiles : (t.vec ? args->n_params / T : 0);
         const int64_t n_tail = pl.pub.n_tiles - n_full;  // 0 or 1 when vec, else all tiles
         int grid_full = (int)(n_full < pl.pub.grid ? n_full : pl.pub.grid);
         int grid_tail = (int)(n_tail < pl.pub.grid ? n_tail : pl.pub.grid);
@@ -322,6 +393,73 @@ size_t dl_deviation_workspace_bytes(int32_t n_rows, int64_t n_params) {
     return dl_mix_workspace_bytes(n_rows, 0, n_params);
 }
 
+}  // extern "C"
+
+namespace {
+
+// One-pass deviation on the tile kernel (MIX = false): every agent of a column tile in one
+// workgroup, column mean in LDS scratch.  tile_cols > 0: x in the column-tiled layout.
+// Returns DL_ERR_UNSUPPORTED (without launching) when the agents do not fit one tile.
+int deviation_one_pass(const float *x, int64_t ldx, int32_t tile_cols, int32_t n_rows,
+                       int64_t n_params, float *dev_sq, float *dev_max, float *mean_out, char *ws,
+                       size_t ws_bytes, hipStream_t s) {
+    int c = tile_cols > 0 ? tile_cols / 4 : next_pow2_chunks(n_params);
+    for (; c >= 1; c >>= 1) {
+        if ((int64_t)n_rows * c <= (int64_t)dl::kRowsPerThread * dl::kTileThreads) break;
+        if (tile_cols > 0) return DL_ERR_UNSUPPORTED;
+    }
+    if (c < 1) return DL_ERR_UNSUPPORTED;
+    const int lds = (dl::kTileThreads / 64) * c * 16;
+    const int64_t T = 4 * c;
+    bool vec = aligned16(x) && (!mean_out || aligned16(mean_out));
+    if (tile_cols == 0)
+        vec = vec && ldx % 4 == 0 && ((int64_t)(n_rows - 1) * ldx + 128) * 4 < ((int64_t)1 << 32);
+    else if (!vec)
+        return fail(DL_ERR_INVALID, "dl_deviation_tiled: x must be 16-byte aligned");
+    const int64_t n_tiles = (n_params + T - 1) / T;
+    const int64_t n_full = tile_cols > 0 ? n_tiles : (vec ? n_params / T : 0);
+    const int64_t n_tail = n_tiles - n_full;
+    const int64_t gmax = (int64_t)device_cus() * 2;
+    const int grid_full = (int)(n_full < gmax ? n_full : gmax);
+    const int grid_tail = (int)(n_tail < gmax ? n_tail : gmax);
+    if (ws_bytes < align_up((size_t)(grid_full + grid_tail) * n_rows * 4))
+        return fail(DL_ERR_WORKSPACE, "dl_deviation: workspace too small");
+    dl::TileArgs t{};
+    t.x = x;
+    t.ldx = ldx;
+    t.n_rows = n_rows;
+    t.n_src = n_rows;
+    t.n_params = n_params;
+    t.vec = vec ? 1 : 0;
+    t.mean = mean_out;
+    t.tiled = tile_cols > 0 ? 1 : 0;
+    t.xts = tile_cols > 0 ? (int64_t)n_rows * T * 4 : T * 4;
+    t.xrs = (uint32_t)(tile_cols > 0 ? T * 4 : ldx * 4);
+    t.scratch_off = 0;
+    float *partial = reinterpret_cast<float *>(ws);
+    if (grid_full > 0) {
+        t.n_tiles = (int32_t)n_full;
+        t.col_base = 0;
+        t.dev_partial = partial;
+        hipError_t e = dl::launch_mix_tile(t, c, false, true, false, grid_full, lds, true, s);
+        if (e != hipSuccess) return hip_fail(e, "dev tile launch");
+    }
+    if (grid_tail > 0) {
+        t.n_tiles = (int32_t)n_tail;
+        t.col_base = n_full * T;
+        t.dev_partial = partial + (size_t)grid_full * n_rows;
+        hipError_t e = dl::launch_mix_tile(t, c, false, true, false, grid_tail, lds, false, s);
+        if (e != hipSuccess) return hip_fail(e, "dev tile (tail) launch");
+    }
+    hipError_t e = dl::launch_dev_reduce(partial, grid_full + grid_tail, n_rows, dev_sq, dev_max, s);
+    if (e != hipSuccess) return hip_fail(e, "dev_reduce launch");
+    return DL_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
 int dl_deviation(const float *x, int64_t ldx, int32_t n_rows, int64_t n_params,
                  const float *mean_in, float *dev_sq, float *dev_max, float *mean_out,
                  void *workspace, size_t ws_bytes, dl_stream_t stream) {
@@ -344,53 +482,58 @@ int dl_deviation(const float *x, int64_t ldx, int32_t n_rows, int64_t n_params,
         return zero_deviation(n_rows, dev_sq, dev_max, s);
     }
     if (!mean_in) {
-        // one pass: every agent of a column tile in one workgroup (registers + LDS scratch)
-        const int cmax = next_pow2_chunks(n_params);
-        for (int c = cmax; c >= 1; c >>= 1) {
-            if ((int64_t)n_rows * c > (int64_t)dl::kRowsPerThread * dl::kTileThreads) continue;
-            const int lds = (dl::kTileThreads / 64) * c * 16;
-            const int64_t T = 4 * c;
-            const bool vec = aligned16(x) && ldx % 4 == 0 && (!mean_out || aligned16(mean_out)) &&
-                             ((int64_t)(n_rows - 1) * ldx + 128) * 4 < ((int64_t)1 << 32);
-            const int64_t n_tiles = (n_params + T - 1) / T;
-            const int64_t n_full = vec ? n_params / T : 0;
-            const int64_t n_tail = n_tiles - n_full;
-            const int64_t gmax = (int64_t)device_cus() * 2;
-            const int grid_full = (int)(n_full < gmax ? n_full : gmax);
-            const int grid_tail = (int)(n_tail < gmax ? n_tail : gmax);
-            if (ws_bytes < align_up((size_t)(grid_full + grid_tail) * n_rows * 4))
-                return fail(DL_ERR_WORKSPACE, "dl_deviation: workspace too small");
-            dl::TileArgs t{};
-            t.x = x;
-            t.ldx = ldx;
-            t.n_rows = n_rows;
-            t.n_src = n_rows;
-            t.n_params = n_params;
-            t.vec = vec ? 1 : 0;
-            t.mean = mean_out;
-            float *partial = reinterpret_cast<float *>(ws);
-            if (grid_full > 0) {
-                t.n_tiles = (int32_t)n_full;
-                t.col_base = 0;
-                t.dev_partial = partial;
-                hipError_t e = dl::launch_mix_tile(t, c, false, true, false, grid_full, lds, true, s);
-                if (e != hipSuccess) return hip_fail(e, "dev tile launch");
-            }
-            if (grid_tail > 0) {
-                t.n_tiles = (int32_t)n_tail;
-                t.col_base = n_full * T;
-                t.dev_partial = partial + (size_t)grid_full * n_rows;
-                hipError_t e = dl::launch_mix_tile(t, c, false, true, false, grid_tail, lds, false, s);
-                if (e != hipSuccess) return hip_fail(e, "dev tile (tail) launch");
-            }
-            hipError_t e = dl::launch_dev_reduce(partial, grid_full + grid_tail, n_rows, dev_sq,
-                                                 dev_max, s);
-            if (e != hipSuccess) return hip_fail(e, "dev_reduce launch");
-            return DL_OK;
-        }
+        int rc = deviation_one_pass(x, ldx, 0, n_rows, n_params, dev_sq, dev_max, mean_out, ws,
+                                    ws_bytes, s);
+        if (rc != DL_ERR_UNSUPPORTED) return rc;
     }
     return deviation_two_pass(x, ldx, n_rows, n_params, mean_in, dev_sq, dev_max, mean_out, ws,
                               ws_bytes, s);
+}
+
+int dl_deviation_tiled(const float *x, int32_t n_rows, int64_t n_params, int32_t tile_cols,
+                       float *dev_sq, float *dev_max, float *mean_out, void *workspace,
+                       size_t ws_bytes, dl_stream_t stream) {
+    g_err.clear();
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (!x || n_rows <= 0 || n_params <= 0 || tile_cols < 16 || tile_cols > 4 * dl::kMaxChunks ||
+        (tile_cols & (tile_cols - 1)))
+        return fail(DL_ERR_INVALID, "dl_deviation_tiled: bad x/n_rows/n_params/tile_cols");
+    char *ws = static_cast<char *>(workspace);
+    if (!ws || (reinterpret_cast<uintptr_t>(ws) & 15u))
+        return fail(DL_ERR_WORKSPACE, "dl_deviation_tiled: needs a 16-byte aligned workspace");
+    if (n_rows <= 1) {
+        if (mean_out) {
+            hipError_t e = dl::launch_tile_convert(x, mean_out, n_params, 1, n_params, tile_cols,
+                                                   false, s);
+            if (e != hipSuccess) return hip_fail(e, "dl_deviation_tiled mean copy");
+        }
+        return zero_deviation(n_rows, dev_sq, dev_max, s);
+    }
+    int rc = deviation_one_pass(x, 0, tile_cols, n_rows, n_params, dev_sq, dev_max, mean_out, ws,
+                                ws_bytes, s);
+    if (rc == DL_ERR_UNSUPPORTED)
+        return fail(DL_ERR_UNSUPPORTED, "dl_deviation_tiled: %d rows exceed one tile", n_rows);
+    return rc;
+}
+
+int dl_to_tiled(const float *src, int64_t ld, int32_t n_rows, int64_t n_params, int32_t tile_cols,
+                float *dst, dl_stream_t stream) {
+    g_err.clear();
+    if (!src || !dst || n_rows <= 0 || n_params <= 0 || ld < n_params || tile_cols <= 0)
+        return fail(DL_ERR_INVALID, "dl_to_tiled: bad arguments");
+    hipError_t e = dl::launch_tile_convert(src, dst, ld, n_rows, n_params, tile_cols, true,
+                                           static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? DL_OK : hip_fail(e, "tile_convert launch");
+}
+
+int dl_from_tiled(const float *src, int32_t n_rows, int64_t n_params, int32_t tile_cols, float *dst,
+                  int64_t ld, dl_stream_t stream) {
+    g_err.clear();
+    if (!src || !dst || n_rows <= 0 || n_params <= 0 || ld < n_params || tile_cols <= 0)
+        return fail(DL_ERR_INVALID, "dl_from_tiled: bad arguments");
+    hipError_t e = dl::launch_tile_convert(src, dst, ld, n_rows, n_params, tile_cols, false,
+                                           static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? DL_OK : hip_fail(e, "tile_convert launch");
 }
 
 int dl_column_sum(const float *x, int64_t ldx, int32_t n_rows, int64_t n_params, float *colsum,
@@ -465,6 +608,7 @@ int dl_perron_round(const dl_perron_args *a, void *workspace, size_t ws_bytes,
     p.conv_eps = a->conv_eps;
     p.max_iter = a->max_iter;
     p.iters_out = a->iters_out;
+    p.conv_rows = a->conv_eps_rows;
     if (tp == a->n_params) {
         hipError_t e = dl::launch_perron_single(p, a->dtype, tp, s);
         return e == hipSuccess ? DL_OK : hip_fail(e, "perron_single launch");

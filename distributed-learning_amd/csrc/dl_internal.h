@@ -33,6 +33,12 @@ struct TileArgs {
     int32_t vec;      // 1: x/g/y/halo 16-byte aligned and ld % 4 == 0
     uint32_t csr_off; // byte offset of the staged CSR in LDS
     uint32_t scratch_off; // byte offset of the 16 x C float4 mean scratch in LDS
+    // FAST-path strides in bytes: tile stride (next tile's row 0) and row stride.
+    //   row-major:      xts = T*4,          xrs = ldx*4   (tile base also offset by col_base)
+    //   column-tiled:   xts = n_rows*T*4,   xrs = T*4     (block [n_rows][T] per tile)
+    int32_t tiled;
+    int64_t xts, gts, yts;
+    uint32_t xrs, grs, yrs;
     float *dev_partial;  // [gridDim.x][n_rows] per-workgroup partial ||y_a - mean||^2
     float *mean;         // [n_params] nullable
 };
@@ -51,6 +57,8 @@ hipError_t launch_dev_rows(const float *x, int64_t ldx, int n_rows, int64_t n_pa
                            const float *mean, float *partial, int nparts, hipStream_t s);
 int dev_rows_parts(int64_t n_params);
 hipError_t launch_stream_copy(const float *src, float *dst, int64_t n_floats, hipStream_t s);
+hipError_t launch_tile_convert(const float *src, float *dst, int64_t ld, int n_rows, int64_t n_params,
+                               int tile_cols, bool to_tiled, hipStream_t s);
 hipError_t launch_max_column_std(const float *x, int64_t ldx, int n_rows, int64_t n_params,
                                  float *out, hipStream_t s);
 hipError_t launch_step_rows(const float *x, int64_t ldx, const float *g, int64_t ldg, float lr,
@@ -72,6 +80,7 @@ struct PerronArgs {
     int32_t max_iter;
     int32_t *iters_out;
     int32_t *notconv;  // workspace flag (multi-tile)
+    const double *conv_rows;  // nullable per-row conv eps
 };
 int perron_tile_cols(int dtype, int n_rows, int64_t n_params);
 hipError_t launch_perron_single(const PerronArgs &a, int dtype, int tile_cols, hipStream_t s);

@@ -127,12 +127,18 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
     const int reg = a.regular;
 
     // FAST-path byte offsets: lane row s / chunk c; pass k adds k * step
-    uint32_t ox = (uint32_t)(((int64_t)s * a.ldx + 4 * c) * 4);
-    const uint32_t sx = (uint32_t)((int64_t)SLOTS * a.ldx * 4);
-    uint32_t og = SGD ? (uint32_t)(((int64_t)s * a.ldg + 4 * c) * 4) : 0u;
-    const uint32_t sg = SGD ? (uint32_t)((int64_t)SLOTS * a.ldg * 4) : 0u;
-    uint32_t oy = (uint32_t)(((int64_t)s * a.ldy + 4 * c) * 4);
-    const uint32_t sy = (uint32_t)((int64_t)SLOTS * a.ldy * 4);
+    // (row stride = ld*4 in the row-major layout, T*4 in the column-tiled one)
+    uint32_t ox = (uint32_t)s * a.xrs + 16u * c;
+    const uint32_t sx = (uint32_t)SLOTS * a.xrs;
+    uint32_t og = SGD ? (uint32_t)s * a.grs + 16u * c : 0u;
+    const uint32_t sg = SGD ? (uint32_t)SLOTS * a.grs : 0u;
+    uint32_t oy = (uint32_t)s * a.yrs + 16u * c;
+    const uint32_t sy = (uint32_t)SLOTS * a.yrs;
+    // byte address of tile t's first element (row 0) in x / g / y
+    auto tile_base = [&](const void *p, int64_t ts, int tile_id) {
+        return reinterpret_cast<const char *>(p) + (a.tiled ? 0 : a.col_base * 4) +
+               (int64_t)tile_id * ts;
+    };
     float4 *scratch = reinterpret_cast<float4 *>(smem + a.scratch_off);
 
     float4 px[KV], pg[KV];
@@ -147,8 +153,9 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
     auto prefetch = [&](int tile_id) {
         const int64_t col0 = a.col_base + (int64_t)tile_id * T;
         if (FAST && !HALO) {
-            const float *xt = a.x + col0;
-            const float *gt = SGD ? a.g + col0 : nullptr;
+            const float *xt = reinterpret_cast<const float *>(tile_base(a.x, a.xts, tile_id));
+            const float *gt =
+                SGD ? reinterpret_cast<const float *>(tile_base(a.g, a.gts, tile_id)) : nullptr;
 #pragma unroll
             for (int k = 0; k < KV; ++k) {
                 const bool ok = s + k * SLOTS < R;
@@ -237,7 +244,8 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
             }
             __syncthreads();
             if (nxt < a.n_tiles) prefetch(nxt);  // lands while we mix from LDS
-            float *yt = a.y + col0;
+            float *yt = const_cast<float *>(
+                reinterpret_cast<const float *>(tile_base(a.y, a.yts, tile_id)));
             float4 cs = zero4();
             // passes stay rolled: interleaving them would hold KV accumulators at once on top
             // of the 2*KV prefetch registers
@@ -332,7 +340,6 @@ __global__ void __launch_bounds__(1024) dev_reduce_kernel(const float *__restric
                                                           float *__restrict__ dev_sq,
                                                           unsigned int *__restrict__ dev_max) {
     __shared__ double red[16][64];
-    __shared__ float smax[16];
     const int ai = threadIdx.x & 63, j = threadIdx.x >> 6;
     const int ag = blockIdx.x * 64 + ai;
     double s = 0.0;
@@ -354,12 +361,20 @@ __global__ void __launch_bounds__(1024) dev_reduce_kernel(const float *__restric
     }
 }
 
-// Streaming copy (HBM ceiling measurement): float4, grid-stride.
+// Streaming copy (HBM ceiling measurement): float4, 4 loads in flight per thread per step.
 __global__ void __launch_bounds__(256) stream_copy_kernel(const float4 *__restrict__ src,
                                                           float4 *__restrict__ dst, int64_t n4) {
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4;
-         i += (int64_t)gridDim.x * 256)
-        dst[i] = src[i];
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    for (; i + 3 * stride < n4; i += 4 * stride) {
+        const float4 a = src[i], b = src[i + stride], c = src[i + 2 * stride],
+                     d = src[i + 3 * stride];
+        dst[i] = a;
+        dst[i + stride] = b;
+        dst[i + 2 * stride] = c;
+        dst[i + 3 * stride] = d;
+    }
+    for (; i < n4; i += stride) dst[i] = src[i];
 }
 
 template <int C, int KV, bool SGD, bool DEV, bool MIX, bool HALO, bool FAST>
@@ -456,7 +471,7 @@ hipError_t launch_dev_reduce(const float *partial, int nparts, int n_rows, float
 hipError_t launch_stream_copy(const float *src, float *dst, int64_t n_floats, hipStream_t s) {
     const int64_t n4 = n_floats / 4;
     int64_t grid = (n4 + 255) / 256;
-    if (grid > 256 * 16) grid = 256 * 16;
+    if (grid > 256 * 8) grid = 256 * 8;
     if (grid < 1) grid = 1;
     hipLaunchKernelGGL(stream_copy_kernel, dim3((unsigned)grid), dim3(256), 0, s,
                        reinterpret_cast<const float4 *>(src), reinterpret_cast<float4 *>(dst), n4);

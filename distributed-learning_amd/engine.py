@@ -51,6 +51,62 @@ def _check(t, name, rows, cols, device):
         raise ValueError(f"{name} has shape {tuple(t.shape)}, expected ({rows}, {cols})")
 
 
+def plan_shape(W: DeviceCsr, n_params, deviation=True):
+    """dl_mix_plan_shape: the kernel configuration for these sizes (no tensors needed)."""
+    lib = _lib.load()
+    plan = _lib.DlMixPlan()
+    _lib.check(lib.dl_mix_plan_shape(W.n_rows, W.n_src - W.n_rows, int(n_params), W.nnz,
+                                     W.uniform_row_nnz, int(bool(deviation)), ctypes.byref(plan)),
+               "dl_mix_plan_shape")
+    return {f: getattr(plan, f) for f, _ in plan._fields_}
+
+
+def tiled_shape(n_rows, n_params, tile_cols):
+    return ((n_params + tile_cols - 1) // tile_cols, n_rows, tile_cols)
+
+
+def to_tiled(X, tile_cols, out=None):
+    """Row-major [n, P] -> column-tiled [ceil(P/T), n, T] (zero-padded last tile)."""
+    lib = _lib.load()
+    n, P = X.shape
+    out = torch.empty(tiled_shape(n, P, tile_cols), dtype=torch.float32,
+                      device=X.device) if out is None else out
+    _lib.check(lib.dl_to_tiled(_lib.ptr(X), _ld(X), n, P, tile_cols, _lib.ptr(out),
+                               _lib.stream_handle(X.device)), "dl_to_tiled")
+    return out
+
+
+def from_tiled(Xt, n_params, out=None):
+    """Column-tiled [tiles, n, T] -> row-major [n, P]."""
+    lib = _lib.load()
+    _, n, T = Xt.shape
+    out = torch.empty(n, n_params, dtype=torch.float32, device=Xt.device) if out is None else out
+    _lib.check(lib.dl_from_tiled(_lib.ptr(Xt), n, n_params, T, _lib.ptr(out), _ld(out),
+                                 _lib.stream_handle(Xt.device)), "dl_from_tiled")
+    return out
+
+
+def _check_tiled(t, name, shape, device):
+    if t.dtype != torch.float32 or t.device != device or tuple(t.shape) != tuple(shape) or \
+            not t.is_contiguous():
+        raise ValueError(f"{name} must be a contiguous float32 tensor of shape {tuple(shape)} "
+                         f"on {device} (got {tuple(t.shape)}, {t.dtype}, {t.device})")
+
+
+def mix_args_tiled(W: DeviceCsr, n_params, tile_cols, X, Y, G=None, lr=0.0, dev_sq=None,
+                   dev_max=None, mean=None):
+    shape = tiled_shape(W.n_rows, n_params, tile_cols)
+    _check_tiled(X, "X", shape, W.device)
+    _check_tiled(Y, "Y", shape, W.device)
+    if G is not None:
+        _check_tiled(G, "G", shape, W.device)
+    if W.n_src != W.n_rows:
+        raise ValueError("the column-tiled layout takes no halo rows")
+    return _lib.DlMixArgs(
+        _lib.ptr(X), 0, _lib.ptr(Y), 0, int(n_params), W.c_struct(), _lib.ptr(G), 0, float(lr),
+        None, 0, 0, _lib.ptr(dev_sq), _lib.ptr(dev_max), _lib.ptr(mean), int(tile_cols))
+
+
 def mix_args(W: DeviceCsr, X, Y, G=None, lr=0.0, halo=None, dev_sq=None, dev_max=None,
              mean=None):
     """Build the dl_mix_args struct for X -> Y (shapes checked here, the rest in the ABI)."""
@@ -89,13 +145,18 @@ class Workspace:
 
 
 def mix_round(W: DeviceCsr, X, Y, G=None, lr=0.0, halo=None, dev_sq=None, dev_max=None,
-              mean=None, workspace: Workspace = None):
-    """One consensus round on the current stream: Y = W (X - lr G) [+ deviation of Y]."""
+              mean=None, workspace: Workspace = None, tiled=None):
+    """One consensus round on the current stream: Y = W (X - lr G) [+ deviation of Y].
+    ``tiled=(n_params, tile_cols)``: X, G, Y are in the column-tiled layout."""
     lib = _lib.load()
-    args = mix_args(W, X, Y, G, lr, halo, dev_sq, dev_max, mean)
+    if tiled is not None:
+        P = tiled[0]
+        args = mix_args_tiled(W, tiled[0], tiled[1], X, Y, G, lr, dev_sq, dev_max, mean)
+    else:
+        P = X.shape[1]
+        args = mix_args(W, X, Y, G, lr, halo, dev_sq, dev_max, mean)
     workspace = workspace or Workspace(W.device)
-    wp, wn = workspace.ptr_size(lib.dl_mix_workspace_bytes(W.n_rows, W.n_src - W.n_rows,
-                                                           X.shape[1]))
+    wp, wn = workspace.ptr_size(lib.dl_mix_workspace_bytes(W.n_rows, W.n_src - W.n_rows, P))
     _lib.check(lib.dl_mix_round(ctypes.byref(args), wp, wn, _lib.stream_handle(W.device)),
                "dl_mix_round")
 
@@ -124,6 +185,23 @@ def deviation(X, dev_sq=None, dev_max=None, mean_in=None, mean_out=None,
     _lib.check(lib.dl_deviation(_lib.ptr(X), _ld(X), n, P, _lib.ptr(mean_in), _lib.ptr(dev_sq),
                                 _lib.ptr(dev_max), _lib.ptr(mean_out), wp, wn,
                                 _lib.stream_handle(dev)), "dl_deviation")
+    return dev_sq, dev_max
+
+
+def deviation_tiled(Xt, n_params, dev_sq=None, dev_max=None, mean_out=None,
+                    workspace: Workspace = None):
+    lib = _lib.load()
+    _, n, T = Xt.shape
+    dev = Xt.device
+    if dev_sq is None:
+        dev_sq = torch.empty(n, dtype=torch.float32, device=dev)
+    if dev_max is None:
+        dev_max = torch.empty(1, dtype=torch.float32, device=dev)
+    workspace = workspace or Workspace(dev)
+    wp, wn = workspace.ptr_size(lib.dl_deviation_workspace_bytes(n, n_params))
+    _lib.check(lib.dl_deviation_tiled(_lib.ptr(Xt), n, int(n_params), T, _lib.ptr(dev_sq),
+                                      _lib.ptr(dev_max), _lib.ptr(mean_out), wp, wn,
+                                      _lib.stream_handle(dev)), "dl_deviation_tiled")
     return dev_sq, dev_max
 
 
@@ -157,7 +235,7 @@ def step_rows(X, rows, out, G=None, lr=0.0):
 
 
 def perron_round(Y, rowptr, col, eps, conv_eps, weight=None, mean_weight=1.0, max_iter=1 << 30,
-                 workspace: Workspace = None):
+                 workspace: Workspace = None, conv_eps_rows=None):
     """In-place asyncio-style consensus round on Y (fp32 or fp64).  Returns the iteration count."""
     lib = _lib.load()
     if Y.dtype not in (torch.float32, torch.float64):
@@ -169,7 +247,8 @@ def perron_round(Y, rowptr, col, eps, conv_eps, weight=None, mean_weight=1.0, ma
     wp, wn = workspace.ptr_size(lib.dl_perron_workspace_bytes(dtype, n, P))
     args = _lib.DlPerronArgs(dtype, _lib.ptr(Y), _ld(Y), n, P, _lib.ptr(rowptr), _lib.ptr(col),
                              _lib.ptr(weight), float(mean_weight), float(eps), float(conv_eps),
-                             int(min(max_iter, 2 ** 31 - 1)), _lib.ptr(iters))
+                             int(min(max_iter, 2 ** 31 - 1)), _lib.ptr(iters),
+                             _lib.ptr(conv_eps_rows))
     _lib.check(lib.dl_perron_round(ctypes.byref(args), wp, wn, _lib.stream_handle(Y.device)),
                "dl_perron_round")
     return int(iters.item())
@@ -181,30 +260,67 @@ class GossipEngine:
     ``round(G, lr)`` runs one consensus round  X <- W (X - lr G)  (ping-pong buffers, no host
     synchronisation); with ``deviation=True`` it also leaves ||x_a - mean||^2 in ``dev_sq`` and
     max_a ||x_a - mean|| in ``dev_max`` (device tensors).
+
+    layout="tiled" (default when the graph fits the LDS tile kernel) keeps X, Y and G in the
+    column-tiled layout [ceil(P/T)][N][T]: every tile the kernel stages is one contiguous HBM
+    block, so the stream runs at copy speed even when T*4 bytes is a short row segment.
+    Row-major data goes in and out through ``load_rows`` / ``rows`` / ``layout_like``.
     """
 
-    def __init__(self, csr: Csr, n_params, device="cuda", X=None):
+    def __init__(self, csr: Csr, n_params, device="cuda", X=None, layout="auto"):
         self.device = torch.device(device)
         if self.device.type == "cuda" and self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
         self.W = DeviceCsr(csr, self.device)
         self.n, self.P = csr.n_rows, int(n_params)
-        self.X = X if X is not None else torch.zeros(self.n, self.P, device=self.device)
-        self.Y = torch.empty_like(self.X)
+        plan = plan_shape(self.W, self.P, deviation=True)
+        tiled_ok = plan["path"] == 1 and plan["tile_cols"] >= 16 and self.W.n_src == self.n
+        if layout == "auto":
+            layout = "tiled" if tiled_ok else "rows"
+        if layout == "tiled" and not tiled_ok:
+            raise ValueError("this graph does not fit the LDS tile kernel; use layout='rows'")
+        self.layout = layout
+        self.T = plan["tile_cols"] if layout == "tiled" else 0
         self.dev_sq = torch.zeros(self.n, dtype=torch.float32, device=self.device)
         self.dev_max = torch.zeros(1, dtype=torch.float32, device=self.device)
-        self.mean = None
         self.ws = Workspace(self.device)
+        self.X = self.layout_like(X) if X is not None else self._empty()
+        self.Y = self._empty()
+
+    def _empty(self):
+        if self.layout == "tiled":
+            return torch.zeros(tiled_shape(self.n, self.P, self.T), dtype=torch.float32,
+                               device=self.device)
+        return torch.zeros(self.n, self.P, dtype=torch.float32, device=self.device)
+
+    def layout_like(self, A):
+        """A row-major [N, P] tensor in this engine's resident layout (G, X, ...)."""
+        if A.shape != (self.n, self.P):
+            raise ValueError(f"expected shape ({self.n}, {self.P}), got {tuple(A.shape)}")
+        A = A.to(self.device, torch.float32)
+        return to_tiled(A, self.T) if self.layout == "tiled" else A.contiguous()
+
+    def load_rows(self, X):
+        self.X = self.layout_like(X)
+
+    def rows(self):
+        """The agent matrix as a row-major [N, P] tensor (a conversion in the tiled layout)."""
+        return from_tiled(self.X, self.P) if self.layout == "tiled" else self.X
 
     def round(self, G=None, lr=0.0, deviation=False, mean=None, halo=None):
+        """G must already be in the resident layout (``layout_like``)."""
         mix_round(self.W, self.X, self.Y, G=G, lr=lr, halo=halo,
                   dev_sq=self.dev_sq if deviation else None,
-                  dev_max=self.dev_max if deviation else None, mean=mean, workspace=self.ws)
+                  dev_max=self.dev_max if deviation else None, mean=mean, workspace=self.ws,
+                  tiled=(self.P, self.T) if self.layout == "tiled" else None)
         self.X, self.Y = self.Y, self.X
 
-    def deviation(self, mean_in=None, mean_out=None):
-        return deviation(self.X, self.dev_sq, self.dev_max, mean_in=mean_in, mean_out=mean_out,
-                         workspace=self.ws)
+    def deviation(self, mean_out=None):
+        if self.layout == "tiled":
+            return deviation_tiled(self.X, self.P, self.dev_sq, self.dev_max, mean_out, self.ws)
+        return deviation(self.X, self.dev_sq, self.dev_max, mean_out=mean_out, workspace=self.ws)
 
-    def plan(self, G=None, deviation=False):
-        return mix_plan(self.W, self.X, self.Y, G, deviation)
+    def plan(self, deviation=True):
+        p = plan_shape(self.W, self.P, deviation)
+        p["layout"] = self.layout
+        return p

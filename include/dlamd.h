@@ -77,6 +77,10 @@ typedef struct dl_mix_args {
     float *dev_sq;      /* nullable [n_rows]: ||y_a - mean_b(y_b)||^2  (needs n_halo == 0) */
     float *dev_max;     /* nullable [1]: max_a sqrt(dev_sq[a])          (needs n_halo == 0) */
     float *mean;        /* nullable [n_params]: mean_b(y_b)              (needs n_halo == 0) */
+    int32_t tile_cols;  /* 0: x, g, y row-major with ld*.  T > 0: x, g, y in the column-tiled
+                           layout [ceil(n_params/T)][n_rows][T] (each tile one contiguous block,
+                           last tile zero-padded; ld* ignored); T must be the plan's tile_cols
+                           (dl_mix_plan_query on the row-major args).  No halo rows. */
 } dl_mix_args;
 
 /* Which kernel configuration dl_mix_round picks (introspection for tests and the bench). */
@@ -93,6 +97,11 @@ int dl_abi_version(void);
 const char *dl_last_error(void);
 
 size_t dl_mix_workspace_bytes(int32_t n_rows, int32_t n_halo, int64_t n_params);
+/* Plan from shapes only (no pointers): what dl_mix_round would pick for a row-major round with
+ * these sizes, with (sgd) / without a local step and with (deviation) / without the fused
+ * deviation.  plan->tile_cols is the width the column-tiled layout must use. */
+int dl_mix_plan_shape(int32_t n_rows, int32_t n_halo, int64_t n_params, int32_t nnz,
+                      int32_t uniform_row_nnz, int32_t deviation, dl_mix_plan *plan);
 int dl_mix_plan_query(const dl_mix_args *args, dl_mix_plan *plan);
 int dl_mix_round(const dl_mix_args *args, void *workspace, size_t ws_bytes, dl_stream_t stream);
 
@@ -103,6 +112,18 @@ size_t dl_deviation_workspace_bytes(int32_t n_rows, int64_t n_params);
 int dl_deviation(const float *x, int64_t ldx, int32_t n_rows, int64_t n_params,
                  const float *mean_in, float *dev_sq, float *dev_max, float *mean_out,
                  void *workspace, size_t ws_bytes, dl_stream_t stream);
+
+/* Deviation of x held in the column-tiled layout (see dl_mix_args.tile_cols). */
+int dl_deviation_tiled(const float *x, int32_t n_rows, int64_t n_params, int32_t tile_cols,
+                       float *dev_sq, float *dev_max, float *mean_out, void *workspace,
+                       size_t ws_bytes, dl_stream_t stream);
+
+/* Layout conversion between row-major [n_rows][ld] and column-tiled [ceil(P/T)][n_rows][T]
+ * (the resident layout of the engine: one HBM-contiguous block per LDS tile). */
+int dl_to_tiled(const float *src, int64_t ld, int32_t n_rows, int64_t n_params, int32_t tile_cols,
+                float *dst, dl_stream_t stream);
+int dl_from_tiled(const float *src, int32_t n_rows, int64_t n_params, int32_t tile_cols, float *dst,
+                  int64_t ld, dl_stream_t stream);
 
 /* colsum[p] = sum_a x[a, p], rows added in order (numerator of np.mean, mixer.py:61). */
 int dl_column_sum(const float *x, int64_t ldx, int32_t n_rows, int64_t n_params, float *colsum,
@@ -145,6 +166,8 @@ typedef struct dl_perron_args {
     double conv_eps;
     int32_t max_iter;
     int32_t *iters_out;       /* device [1] */
+    const double *conv_eps_rows; /* nullable [n_rows]: per-agent convergence eps (an agent's own
+                                    ConsensusAgent(convergence_eps=...)); overrides conv_eps */
 } dl_perron_args;
 
 size_t dl_perron_workspace_bytes(int32_t dtype, int32_t n_rows, int64_t n_params);

@@ -1,0 +1,57 @@
+"""Kernel-level timing of dl_mix_round variants (HIP events), one JSON line per variant.
+python scripts/kbench.py [--reps R]"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from distributed_learning_amd import engine  # noqa: E402
+from distributed_learning_amd.graph import from_edge_weights, random_regular_edges  # noqa: E402
+import bench  # noqa: E402
+
+
+def time_it(fn, reps):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--cases", default="all")
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    print(json.dumps({"copy_ceiling_GBs": bench.copy_ceiling(dev)}), flush=True)
+    for n, P in [(1024, 1 << 20), (512, 1 << 21), (256, 1 << 22), (2048, 1 << 19)]:
+        edges = random_regular_edges(4, n, seed=0)
+        csr = from_edge_weights(edges, [0.2] * len(edges), sorted(set(u for e in edges for u in e)))
+        X = torch.randn(n, P, device=dev)
+        G = torch.randn(n, P, device=dev)
+        for layout in ("tiled", "rows"):
+            eng = engine.GossipEngine(csr, P, device=dev, X=X, layout=layout)
+            Gl = eng.layout_like(G)
+            for sgd in (False, True):
+                for dv in (False, True):
+                    g = Gl if sgd else None
+                    ms = time_it(lambda: eng.round(G=g, lr=1e-3, deviation=dv), args.reps)
+                    nbytes = (12 if sgd else 8) * n * P
+                    print(json.dumps({"n": n, "P": P, "layout": layout, "sgd": sgd, "dev": dv,
+                                      "ms": ms, "GBs": nbytes / ms / 1e6,
+                                      "plan": eng.plan(deviation=dv)}), flush=True)
+            del eng, Gl
+        del X, G
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

@@ -78,14 +78,14 @@ def test_reference_fixture_rounds(golden, cuda, case, rounds):
     csr = Csr(d[f"{case}_rowptr"], d[f"{case}_cols"], d[f"{case}_w"])
     eng = E.GossipEngine(csr, d[f"{case}_X0"].shape[1], device=cuda,
                          X=torch.from_numpy(d[f"{case}_X0"]).to(cuda))
-    assert eng.plan()["path"] == 1
+    assert eng.plan()["path"] == 1 and eng.layout == "tiled"
     done = 0
     for r in rounds:
         while done < r:
             eng.round(deviation=True)
             done += 1
         torch.cuda.synchronize()
-        got = eng.X.cpu().numpy()
+        got = eng.rows().cpu().numpy()
         assert np.array_equal(bits(got), bits(d[f"{case}_X{r}"])), f"round {r}"
         np.testing.assert_allclose(np.sqrt(eng.dev_sq.cpu().numpy()), d[f"{case}_dev{r}"],
                                    rtol=DEV_RTOL, atol=dev_floor(M.column_mean(got), got.shape[1]))
@@ -122,10 +122,11 @@ def test_regular_graph_skips_rowptr(cuda):
     csr = Csr(rp, cl, np.full(cl.size, 0.2))
     assert csr.uniform_row_nnz == 5
     X = rng.standard_normal((n, P), dtype=np.float32)
-    eng = E.GossipEngine(csr, P, device=cuda, X=torch.from_numpy(X).to(cuda))
-    assert eng.plan()["regular"] == 1
-    eng.round()
-    assert np.array_equal(bits(eng.X.cpu().numpy()), bits(M.mix_once(X, rp, cl, csr.w)))
+    for layout in ("rows", "tiled"):
+        eng = E.GossipEngine(csr, P, device=cuda, X=torch.from_numpy(X).to(cuda), layout=layout)
+        assert eng.plan()["regular"] == 1
+        eng.round()
+        assert np.array_equal(bits(eng.rows().cpu().numpy()), bits(M.mix_once(X, rp, cl, csr.w)))
 
 
 def test_unaligned_operands_use_guarded_path(cuda):
@@ -222,12 +223,12 @@ def test_full_size_round_column_slices(cuda):
     g = torch.Generator(device=cuda).manual_seed(0)
     X = torch.randn(n, P, device=cuda, generator=g)
     G = torch.randn(n, P, device=cuda, generator=g)
-    eng = E.GossipEngine(csr, P, device=cuda, X=X.clone())
-    plan = eng.plan(G=G, deviation=True)
-    assert plan["path"] == 1 and plan["tile_cols"] >= 32
-    eng.round(G=G, lr=1e-3, deviation=True)
+    eng = E.GossipEngine(csr, P, device=cuda, X=X)
+    plan = eng.plan(deviation=True)
+    assert plan["path"] == 1 and plan["tile_cols"] >= 32 and eng.layout == "tiled"
+    eng.round(G=eng.layout_like(G), lr=1e-3, deviation=True)
     torch.cuda.synchronize()
-    Y = eng.X
+    Y = eng.rows()
     for c0, c1 in [(0, 4096), (P - 4096, P), (123456, 123456 + 999)]:
         want = cref.mix_round(X[:, c0:c1].cpu().numpy(), csr.rowptr, csr.col, csr.w,
                               G=G[:, c0:c1].cpu().numpy(), lr=1e-3)
@@ -236,3 +237,29 @@ def test_full_size_round_column_slices(cuda):
     want_dsq = cref.deviation_sq(Yh)
     np.testing.assert_allclose(np.sqrt(eng.dev_sq.cpu().numpy()), np.sqrt(want_dsq),
                                rtol=DEV_RTOL)
+
+
+@pytest.mark.parametrize("n,P,deg", [(64, 4096, 4), (100, 1000, 5), (1024, 4100, 4), (7, 33, 3),
+                                     (300, 777, 8)])
+def test_tiled_layout_round_trip_and_parity(cuda, n, P, deg):
+    """Resident column-tiled layout: same bits as the row-major round and the oracle, padded
+    tail columns stay zero, deviation matches, conversions round-trip."""
+    E = eng_mod()
+    rng = np.random.default_rng(n + 3 * P)
+    csr = graph_csr(n, deg, seed=n * P)
+    X = rng.standard_normal((n, P), dtype=np.float32)
+    G = rng.standard_normal((n, P), dtype=np.float32)
+    eng = E.GossipEngine(csr, P, device=cuda, X=torch.from_numpy(X).to(cuda), layout="tiled")
+    assert np.array_equal(bits(eng.rows().cpu().numpy()), bits(X))
+    mean = torch.empty(P, device=cuda)
+    eng.round(G=eng.layout_like(torch.from_numpy(G).to(cuda)), lr=0.03, deviation=True,
+              mean=mean)
+    torch.cuda.synchronize()
+    want = cref.mix_round(X, csr.rowptr, csr.col, csr.w, G=G, lr=0.03)
+    assert np.array_equal(bits(eng.rows().cpu().numpy()), bits(want))
+    check_dev(want, eng.dev_sq.cpu().numpy(), float(eng.dev_max.item()), mean.cpu().numpy())
+    T = eng.T
+    if P % T:
+        assert torch.all(eng.X[-1, :, P % T:] == 0)
+    dsq, dmax = eng.deviation()
+    check_dev(want, dsq.cpu().numpy(), float(dmax.item()), M.column_mean(want))

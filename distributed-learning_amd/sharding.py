@@ -1,0 +1,376 @@
+"""Multi-GPU execution of the consensus round (one process per GPU, torch.distributed / RCCL).
+
+Two decompositions of the agent matrix X[N, P]:
+
+* ``StripeShard`` -- column stripes.  The mix is column-independent, so every rank owns
+  X[:, p0:p1] for ALL agents and mixes it with no data exchange; the only collective per round is
+  the all-reduce of the N per-agent squared-deviation partials (the stop test of
+  Mixer.mix, mixer.py:40-66).  This is the weak-scaling decomposition bench.py uses.
+
+* ``HaloShard`` -- agent partition (BASELINE config c4, 2-D torus).  Every rank owns a block of
+  agents; cut edges become a halo exchange: each round a rank packs the stepped rows
+  (x - lr*g) its neighbours need (``dl_step_rows``), exchanges them point-to-point
+  (batched isend/irecv -> RCCL send/recv over xGMI), and mixes its rows with the received halo
+  (``dl_mix_round`` with n_halo > 0).  The column range is processed in chunks so the exchange of
+  chunk j+1 overlaps the mix of chunk j.  This replaces the per-neighbour value messages of the
+  reference (consensus_asyncio.py:236-284, consensus_tcp/agent.py:174-201).
+
+The transport is pluggable: ``DistTransport`` (torch.distributed, RCCL on GPU / gloo on CPU) and
+``LocalTransport`` (in-process virtual ranks, used to test the halo logic on one device).
+"""
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from .graph import Csr
+
+
+# ------------------------------------------------------------------ partitioning (host)
+def contiguous_partition(n, world):
+    """Agents [r*n/world, (r+1)*n/world) to rank r."""
+    bounds = [(r * n) // world for r in range(world + 1)]
+    return [np.arange(bounds[r], bounds[r + 1]) for r in range(world)]
+
+
+def torus_block_partition(rows, cols, world):
+    """2-D block partition of a rows x cols torus (vertex r*cols + c) into a pr x pc grid of
+    blocks with pr * pc == world, choosing the grid with the smallest block perimeter."""
+    best = None
+    for pr in range(1, world + 1):
+        if world % pr:
+            continue
+        pc = world // pr
+        if rows % pr or cols % pc:
+            continue
+        per = 2 * (rows // pr + cols // pc)
+        if best is None or per < best[0]:
+            best = (per, pr, pc)
+    if best is None:
+        return contiguous_partition(rows * cols, world)
+    _, pr, pc = best
+    br, bc = rows // pr, cols // pc
+    parts = []
+    for q in range(world):
+        qr, qc = divmod(q, pc)
+        rr, cc = np.meshgrid(np.arange(qr * br, (qr + 1) * br), np.arange(qc * bc, (qc + 1) * bc),
+                             indexing="ij")
+        parts.append((rr * cols + cc).ravel())
+    return parts
+
+
+def greedy_bfs_partition(csr: Csr, world):
+    """Balanced BFS-grown partition for general graphs (keeps neighbourhoods together)."""
+    n = csr.n_rows
+    target = [(r + 1) * n // world - r * n // world for r in range(world)]
+    owner = -np.ones(n, np.int64)
+    parts = []
+    for r in range(world):
+        seed = int(np.flatnonzero(owner < 0)[0])
+        frontier, members = [seed], []
+        owner[seed] = r
+        while frontier and len(members) < target[r]:
+            a = frontier.pop(0)
+            members.append(a)
+            for e in range(csr.rowptr[a], csr.rowptr[a + 1]):
+                b = int(csr.col[e])
+                if owner[b] < 0 and len(members) + len(frontier) < target[r]:
+                    owner[b] = r
+                    frontier.append(b)
+            if not frontier and len(members) < target[r]:
+                rest = np.flatnonzero(owner < 0)
+                if len(rest):
+                    owner[rest[0]] = r
+                    frontier.append(int(rest[0]))
+        for a in frontier:
+            owner[a] = -1
+        parts.append(np.asarray(sorted(members), np.int64))
+    left = np.flatnonzero(owner < 0)
+    if len(left):
+        parts[-1] = np.asarray(sorted(list(parts[-1]) + list(left)), np.int64)
+    return parts
+
+
+@dataclass
+class RankPlan:
+    """Everything one rank needs for halo rounds."""
+    rank: int
+    local: np.ndarray                 # global ids of my agents (my row order)
+    csr: Csr                          # rows = my agents; cols: [0, n_local) local, then halo
+    halo_from: dict = field(default_factory=dict)   # peer -> global ids I receive (halo order)
+    send_to: dict = field(default_factory=dict)     # peer -> my local row indices I send
+    halo_offset: dict = field(default_factory=dict)  # peer -> first halo row of its block
+
+    @property
+    def n_local(self):
+        return len(self.local)
+
+    @property
+    def n_halo(self):
+        return self.csr.n_src - self.csr.n_rows
+
+
+def halo_plans(csr: Csr, parts):
+    """Per-rank local CSR + halo lists for a partition of the agents of ``csr``.
+
+    Entry order within a row is preserved (so the fp32 fold is identical to the single-device
+    round); remote columns are renumbered into the halo block of their owner, blocks ordered by
+    peer rank and, inside a block, by global id."""
+    world = len(parts)
+    owner = np.empty(csr.n_rows, np.int64)
+    pos = np.empty(csr.n_rows, np.int64)
+    for r, p in enumerate(parts):
+        owner[p] = r
+        pos[p] = np.arange(len(p))
+    plans = []
+    need = [[set() for _ in range(world)] for _ in range(world)]   # need[r][q]: ids r wants
+    for r, p in enumerate(parts):
+        for a in p:
+            for e in range(csr.rowptr[a], csr.rowptr[a + 1]):
+                b = int(csr.col[e])
+                if owner[b] != r:
+                    need[r][owner[b]].add(b)
+    for r, p in enumerate(parts):
+        halo_from, halo_offset, hidx = {}, {}, {}
+        off = 0
+        for q in range(world):
+            if need[r][q]:
+                ids = np.asarray(sorted(need[r][q]), np.int64)
+                halo_from[q] = ids
+                halo_offset[q] = off
+                for i, b in enumerate(ids):
+                    hidx[int(b)] = len(p) + off + i
+                off += len(ids)
+        rowptr, col, w = [0], [], []
+        for a in p:
+            for e in range(csr.rowptr[a], csr.rowptr[a + 1]):
+                b = int(csr.col[e])
+                col.append(int(pos[b]) if owner[b] == r else hidx[b])
+                w.append(float(csr.w[e]))
+            rowptr.append(len(col))
+        local_csr = Csr(rowptr, col, w, keys=[csr.keys[a] for a in p] if csr.keys else [],
+                        n_src=len(p) + off)
+        send_to = {q: pos[np.asarray(sorted(need[q][r]), np.int64)]
+                   for q in range(world) if need[q][r]}
+        plans.append(RankPlan(r, np.asarray(p), local_csr, halo_from, send_to, halo_offset))
+    return plans
+
+
+# ------------------------------------------------------------------ transports
+class DistTransport:
+    """Point-to-point halo exchange over torch.distributed (RCCL on GPU, gloo on CPU)."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+        self.dist = dist
+        self.group = group
+
+    @property
+    def rank(self):
+        return self.dist.get_rank(self.group)
+
+    def exchange(self, sends, recvs):
+        """sends: {peer: tensor}, recvs: {peer: tensor}; returns a waitable handle list."""
+        ops = []
+        for q, t in sorted(recvs.items()):
+            ops.append(self.dist.P2POp(self.dist.irecv, t, q, self.group))
+        for q, t in sorted(sends.items()):
+            ops.append(self.dist.P2POp(self.dist.isend, t, q, self.group))
+        return self.dist.batch_isend_irecv(ops) if ops else []
+
+    def all_reduce_(self, t, op="sum"):
+        o = self.dist.ReduceOp.SUM if op == "sum" else self.dist.ReduceOp.MAX
+        self.dist.all_reduce(t, op=o, group=self.group)
+        return t
+
+
+class LocalTransport:
+    """In-process virtual ranks (threads) sharing one device: tests and single-GPU rehearsal of
+    the halo protocol.  ``endpoint(r)`` gives rank r a transport with the DistTransport API."""
+
+    def __init__(self, world):
+        import threading
+        self.world = world
+        self.cv = threading.Condition()
+        self.box = {}        # (src, dst, seq) -> tensor
+        self.seq = {}        # (src, dst) -> next sequence number (send side)
+        self.rseq = {}       # (src, dst) -> next sequence number (recv side)
+        self.red = {}        # all-reduce rendezvous: seq -> list of tensors
+
+    def endpoint(self, rank):
+        return _LocalEndpoint(self, rank)
+
+
+class _LocalWork:
+    def __init__(self, tr, key, dst):
+        self.tr, self.key, self.dst = tr, key, dst
+
+    def wait(self):
+        with self.tr.cv:
+            self.tr.cv.wait_for(lambda: self.key in self.tr.box, timeout=120)
+            src = self.tr.box.pop(self.key)
+        self.dst.copy_(src)
+
+
+class _LocalEndpoint:
+    def __init__(self, tr, rank):
+        self.tr, self.rank_ = tr, rank
+        self.ar = 0
+
+    @property
+    def rank(self):
+        return self.rank_
+
+    def exchange(self, sends, recvs):
+        tr, me = self.tr, self.rank_
+        with tr.cv:
+            for q, t in sends.items():
+                k = tr.seq.get((me, q), 0)
+                tr.seq[(me, q)] = k + 1
+                tr.box[(me, q, k)] = t.clone()
+            tr.cv.notify_all()
+        works = []
+        for q, t in recvs.items():
+            k = tr.rseq.get((q, me), 0)
+            tr.rseq[(q, me)] = k + 1
+            works.append(_LocalWork(tr, (q, me, k), t))
+        return works
+
+    def all_reduce_(self, t, op="sum"):
+        tr = self.tr
+        k = self.ar
+        self.ar += 1
+        with tr.cv:
+            lst = tr.red.setdefault(k, [None] * tr.world)
+            lst[self.rank_] = t.clone()
+            tr.cv.notify_all()
+            tr.cv.wait_for(lambda: all(x is not None for x in tr.red[k]), timeout=120)
+            parts = list(tr.red[k])
+        acc = parts[0].clone()
+        for x in parts[1:]:
+            acc = acc + x if op == "sum" else torch.maximum(acc, x)
+        t.copy_(acc)
+        return t
+
+
+class HipOps:
+    """Device compute of a shard: libdlamd kernels (the product path)."""
+
+    def __init__(self, device):
+        from . import engine as E
+        self.E = E
+        self.device = torch.device(device)
+        self.ws = E.Workspace(self.device)
+
+    def csr(self, csr):
+        return self.E.DeviceCsr(csr, self.device)
+
+    def step_rows(self, X, rows, out, G=None, lr=0.0):
+        return self.E.step_rows(X, rows, out, G=G, lr=lr)
+
+    def mix(self, W, X, Y, G=None, lr=0.0, halo=None):
+        self.E.mix_round(W, X, Y, G=G, lr=lr, halo=halo, workspace=self.ws)
+
+    def column_sum(self, X):
+        return self.E.column_sum(X)
+
+    def deviation(self, X, mean):
+        return self.E.deviation(X, mean_in=mean, workspace=self.ws)
+
+
+# ------------------------------------------------------------------ execution
+class StripeShard:
+    """Column stripe of a GossipEngine-style state on this rank (all agents, P_local columns)."""
+
+    def __init__(self, engine, transport=None):
+        self.engine = engine
+        self.transport = transport
+
+    def round(self, G=None, lr=0.0, deviation=False):
+        self.engine.round(G=G, lr=lr, deviation=deviation)
+        if deviation and self.transport is not None:
+            self.transport.all_reduce_(self.engine.dev_sq, "sum")
+        return self.engine.dev_sq if deviation else None
+
+    def max_deviation(self):
+        return torch.sqrt(self.engine.dev_sq.max())
+
+
+class HaloShard:
+    """One rank's agent block with halo exchange (row-major X[n_local, P])."""
+
+    def __init__(self, plan: RankPlan, n_params, device, transport, chunk_cols=None,
+                 n_agents_total=None, ops=None):
+        self.plan = plan
+        self.P = int(n_params)
+        self.device = torch.device(device)
+        self.transport = transport
+        self.ops = ops if ops is not None else HipOps(self.device)
+        self.W = self.ops.csr(plan.csr)
+        self.n_total = n_agents_total
+        self.chunk = int(chunk_cols or self.P)
+        self.send_rows = {q: torch.as_tensor(rows.astype(np.int32), device=self.device)
+                          for q, rows in plan.send_to.items()}
+        self.X = torch.zeros(plan.n_local, self.P, device=self.device)
+        self.Y = torch.empty_like(self.X)
+        self._bufs = {}
+
+    def _buffers(self, slot, width):
+        """Send/halo buffers of one pipeline slot; chunks alternate between two slots so the
+        exchange of chunk j+1 never lands in the halo chunk j is being mixed from."""
+        key = (slot, width)
+        if key not in self._bufs:
+            send = {q: torch.empty(len(r), width, device=self.device)
+                    for q, r in self.plan.send_to.items()}
+            halo = torch.empty(self.plan.n_halo, width, device=self.device)
+            recv = {q: halo[self.plan.halo_offset[q]:self.plan.halo_offset[q] + len(ids)]
+                    for q, ids in self.plan.halo_from.items()}
+            self._bufs[key] = (send, halo, recv)
+        return self._bufs[key]
+
+    def pack(self, slot, c0, c1, G=None, lr=0.0):
+        """Stepped boundary rows x - lr*g of columns [c0, c1) for every peer."""
+        send, halo, recv = self._buffers(slot, c1 - c0)
+        Gc = G[:, c0:c1] if G is not None else None
+        for q, rows in self.send_rows.items():
+            self.ops.step_rows(self.X[:, c0:c1], rows, send[q], G=Gc, lr=lr)
+        return send, halo, recv
+
+    def mix_chunk(self, c0, c1, halo, G=None, lr=0.0):
+        Gc = G[:, c0:c1] if G is not None else None
+        self.ops.mix(self.W, self.X[:, c0:c1], self.Y[:, c0:c1], G=Gc, lr=lr,
+                     halo=halo if self.plan.n_halo else None)
+
+    def chunks(self):
+        return [(c, min(c + self.chunk, self.P)) for c in range(0, self.P, self.chunk)]
+
+    def round(self, G=None, lr=0.0):
+        """One round: the halo exchange of chunk j+1 is in flight while chunk j is mixed.
+        (Stream order makes the reuse safe: a slot's next exchange is posted after the mix that
+        read it, and the collective waits for the current stream.)"""
+        chunks = self.chunks()
+
+        def post(j):
+            c0, c1 = chunks[j]
+            send, halo, recv = self.pack(j % 2, c0, c1, G, lr)
+            return self.transport.exchange(send, recv), halo
+
+        pend = post(0)
+        for j, (c0, c1) in enumerate(chunks):
+            nxt = post(j + 1) if j + 1 < len(chunks) else None
+            works, halo = pend
+            for w in works:
+                w.wait()
+            self.mix_chunk(c0, c1, halo, G, lr)
+            pend = nxt
+        self.X, self.Y = self.Y, self.X
+
+    def deviation(self):
+        """Global ||x_a - mean||: column sums all-reduced into the global mean, then the local
+        rows against it; returns (local dev_sq, global max deviation)."""
+        colsum = self.ops.column_sum(self.X)
+        self.transport.all_reduce_(colsum, "sum")
+        mean = colsum / float(self.n_total)
+        dev_sq, dev_max = self.ops.deviation(self.X, mean)
+        self.transport.all_reduce_(dev_max, "max")
+        return dev_sq, dev_max

@@ -1,0 +1,103 @@
+"""Multi-GPU decomposition logic on the CPU: partitions, halo plans, and the real halo protocol
+over torch.distributed gloo with world_size 2 (oracle ops stand in for the device kernels)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from distributed_learning_amd import sharding
+from distributed_learning_amd.graph import (best_constant_weight, from_edge_weights,
+                                            random_regular_edges, torus_edges)
+from oracle import mixer_ref as M
+
+
+def torus_csr(r, c):
+    edges = torus_edges(r, c)
+    verts = list(range(r * c))
+    return from_edge_weights(edges, [best_constant_weight(edges, verts)] * len(edges), verts)
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_torus_block_partition(world):
+    parts = sharding.torus_block_partition(16, 16, world)
+    allv = np.sort(np.concatenate(parts))
+    assert np.array_equal(allv, np.arange(256))
+    assert len({len(p) for p in parts}) == 1
+
+
+@pytest.mark.parametrize("kind", ["torus", "rr4", "bfs"])
+def test_halo_plans_reconstruct_the_graph(kind):
+    if kind == "torus":
+        csr = torus_csr(8, 8)
+        parts = sharding.torus_block_partition(8, 8, 4)
+    else:
+        edges = random_regular_edges(4, 60, seed=1)
+        csr = from_edge_weights(edges, [0.2] * len(edges), list(range(60)))
+        parts = (sharding.contiguous_partition(60, 3) if kind == "rr4"
+                 else sharding.greedy_bfs_partition(csr, 3))
+    assert np.array_equal(np.sort(np.concatenate(parts)), np.arange(csr.n_rows))
+    plans = sharding.halo_plans(csr, parts)
+    for pl in plans:
+        back = np.concatenate([pl.local] + [pl.halo_from[q] for q in sorted(pl.halo_from)])
+        for i, a in enumerate(pl.local):
+            e0, e1 = csr.rowptr[a], csr.rowptr[a + 1]
+            f0, f1 = pl.csr.rowptr[i], pl.csr.rowptr[i + 1]
+            assert np.array_equal(back[pl.csr.col[f0:f1]], csr.col[e0:e1])   # same order
+            assert np.array_equal(pl.csr.w[f0:f1], csr.w[e0:e1])
+        for q, rows in pl.send_to.items():      # what I send is exactly what q expects
+            assert np.array_equal(pl.local[rows], plans[q].halo_from[pl.rank])
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, P, chunk, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from shard_oracle_ops import OracleOps
+    csr = torus_csr(8, 8)
+    parts = sharding.torus_block_partition(8, 8, world)
+    plan = sharding.halo_plans(csr, parts)[rank]
+    rng = np.random.default_rng(0)
+    X = rng.standard_normal((64, P), dtype=np.float32)
+    G = rng.standard_normal((64, P), dtype=np.float32)
+    sh = sharding.HaloShard(plan, P, "cpu", sharding.DistTransport(), chunk_cols=chunk,
+                            n_agents_total=64, ops=OracleOps())
+    sh.X = torch.from_numpy(X[plan.local].copy())
+    Gl = torch.from_numpy(G[plan.local].copy())
+    for _ in range(3):
+        sh.round(G=Gl, lr=0.05)
+    dev_sq, dev_max = sh.deviation()
+    np.save(os.path.join(out_dir, f"x{rank}.npy"), sh.X.numpy())
+    np.save(os.path.join(out_dir, f"ids{rank}.npy"), plan.local)
+    np.save(os.path.join(out_dir, f"dmax{rank}.npy"), dev_max.numpy())
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("chunk", [None, 7])
+def test_halo_rounds_over_gloo_equal_single_process(tmp_path, chunk):
+    world, P = 2, 24
+    mp.spawn(_worker, args=(world, _free_port(), P, chunk, str(tmp_path)), nprocs=world,
+             join=True)
+    csr = torus_csr(8, 8)
+    rng = np.random.default_rng(0)
+    X = rng.standard_normal((64, P), dtype=np.float32)
+    G = rng.standard_normal((64, P), dtype=np.float32)
+    for _ in range(3):
+        X = M.mix_once(M.sgd_step(X, G, 0.05), csr.rowptr, csr.col, csr.w)
+    for r in range(world):
+        ids = np.load(tmp_path / f"ids{r}.npy")
+        got = np.load(tmp_path / f"x{r}.npy")
+        assert np.array_equal(got.view(np.uint32), X[ids].view(np.uint32))
+        np.testing.assert_allclose(np.load(tmp_path / f"dmax{r}.npy")[0], M.deviation(X).max(),
+                                   rtol=1e-5)

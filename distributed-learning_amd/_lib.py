@@ -22,7 +22,7 @@ _i32, _i64, _f32, _f64, _sz = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ct
 
 class DlCsr(ctypes.Structure):
     _fields_ = [("row_ptr", _vp), ("col", _vp), ("w", _vp), ("n_rows", _i32), ("nnz", _i32),
-                ("uniform_row_nnz", _i32)]
+                ("uniform_row_nnz", _i32), ("doubly_stochastic", _i32)]
 
 
 class DlMixArgs(ctypes.Structure):

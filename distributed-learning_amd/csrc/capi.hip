@@ -206,6 +206,7 @@ dl::TileArgs tile_args(const dl_mix_args *a) {
     t.n_src = a->W.n_rows + a->n_halo;
     t.nnz = a->W.nnz;
     t.regular = a->W.uniform_row_nnz;
+    t.mean_from_inputs = (a->W.doubly_stochastic && a->n_halo == 0) ? 1 : 0;
     t.n_params = a->n_params;
     t.lr = a->lr;
     bool vec = aligned16(a->x) && aligned16(a->y) && a->ldx % 4 == 0 && a->ldy % 4 == 0;

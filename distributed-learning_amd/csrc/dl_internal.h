@@ -26,6 +26,7 @@ struct TileArgs {
     int32_t n_src;    // rows staged in LDS = n_rows + n_halo
     int32_t nnz;
     int32_t regular;  // >0: every row has exactly `regular` entries (row_ptr not staged)
+    int32_t mean_from_inputs;  // 1: W doubly stochastic -> tile mean taken from the staged t
     int64_t n_params;
     int32_t n_tiles;
     int64_t col_base; // first column of tile 0

@@ -235,14 +235,36 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
         const int nxt = tile_id + gridDim.x;
         if (MIX) {
             // stage the (stepped) tile of every source row in LDS
+            float4 cst = zero4();  // column partial sums of t (doubly stochastic W only)
 #pragma unroll
             for (int k = 0; k < KV; ++k) {
                 const int r = s + k * SLOTS;
                 float4 t = px[k];
                 if (SGD && (!HALO || r < Nr)) t = local_step(t, pg[k], a.lr);
-                if (r < R) tile[r * C + c] = t;
+                if (r < R) {
+                    tile[r * C + c] = t;
+                    if (DEV) add4(cst, t);
+                }
+            }
+            // mean(W t) = mean(t) when W is doubly stochastic: reduce the column sums of the
+            // inputs under the staging barrier instead of re-mixing the tile afterwards
+            const bool mfi = DEV && a.mean_from_inputs;
+            if (mfi) {
+#pragma unroll
+                for (int m = C; m < 64; m <<= 1) cst = shfl_xor4(cst, m);
+                if ((tid & 63) < C) scratch[(tid >> 6) * C + (tid & 63)] = cst;
             }
             __syncthreads();
+            float4 mean_t = zero4();
+            if (mfi) {
+#pragma unroll
+                for (int wv = 0; wv < NT / 64; ++wv) add4(mean_t, scratch[wv * C + c]);
+                const float n = (float)Nr;
+                mean_t.x = mean_t.x / n;
+                mean_t.y = mean_t.y / n;
+                mean_t.z = mean_t.z / n;
+                mean_t.w = mean_t.w / n;
+            }
             if (nxt < a.n_tiles) prefetch(nxt);  // lands while we mix from LDS
             float *yt = const_cast<float *>(
                 reinterpret_cast<const float *>(tile_base(a.y, a.yts, tile_id)));
@@ -258,10 +280,16 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
                         *at(yt, oy + (uint32_t)k * sy) = acc;
                     else
                         st4(a.y + (int64_t)ag * a.ldy, col0 + 4 * c, P, false, acc);
-                    if (DEV) add4(cs, acc);
+                    if (DEV) {
+                        if (mfi)
+                            dev_add(k, acc, mean_t);
+                        else
+                            add4(cs, acc);
+                    }
                 }
             }
-            if (DEV) {
+            if (mfi && a.mean != nullptr && s == 0) st4(a.mean, col0 + 4 * c, P, FAST, mean_t);
+            if (DEV && !mfi) {
                 const float4 mean = tile_mean(cs);
                 if (a.mean != nullptr && s == 0) st4(a.mean, col0 + 4 * c, P, FAST, mean);
                 // second LDS pass: recompute y (same order, same bits) instead of holding it

@@ -30,10 +30,11 @@ class DeviceCsr:
         self.n_src = csr.n_src
         self.nnz = csr.nnz
         self.uniform_row_nnz = csr.uniform_row_nnz
+        self.doubly_stochastic = int(csr.doubly_stochastic)
 
     def c_struct(self):
         return _lib.DlCsr(_lib.ptr(self.rowptr), _lib.ptr(self.col), _lib.ptr(self.w),
-                          self.n_rows, self.nnz, self.uniform_row_nnz)
+                          self.n_rows, self.nnz, self.uniform_row_nnz, self.doubly_stochastic)
 
 
 def _ld(t):

@@ -52,6 +52,17 @@ class Csr:
         d = np.diff(self.rowptr)
         return int(d[0]) if len(d) and d[0] > 0 and np.all(d == d[0]) else 0
 
+    @property
+    def doubly_stochastic(self):
+        """Every row and column of W sums to 1 (fp32 weights, 1e-6): mean(W x) = mean(x)."""
+        if self.n_src != self.n_rows or self.n_rows == 0:
+            return False
+        w32 = self.w.astype(np.float32).astype(np.float64)
+        row_id = np.repeat(np.arange(self.n_rows), np.diff(self.rowptr))
+        rows = np.bincount(row_id, weights=w32, minlength=self.n_rows)
+        cols = np.bincount(self.col, weights=w32, minlength=self.n_src)
+        return bool(np.all(np.abs(rows - 1) < 1e-6) and np.all(np.abs(cols - 1) < 1e-6))
+
     def dense(self):
         W = np.zeros((self.n_rows, self.n_src))
         for a in range(self.n_rows):

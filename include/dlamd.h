@@ -59,6 +59,10 @@ typedef struct dl_csr {
     int32_t uniform_row_nnz; /* > 0 promises row_ptr[a] == a * uniform_row_nnz for every row
                                 (regular graphs); lets the LDS kernel skip staging row_ptr.
                                 0 = general CSR.  Checked: nnz == n_rows * uniform_row_nnz. */
+    int32_t doubly_stochastic; /* 1 promises every column of W sums to 1 (as rows do for the
+                                  reference's mixing matrices), so mean(W t) = mean(t): the fused
+                                  deviation then takes the column mean from the staged inputs and
+                                  needs one LDS pass instead of two.  0 = general W. */
 } dl_csr;
 
 typedef struct dl_mix_args {

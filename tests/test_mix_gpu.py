@@ -263,3 +263,31 @@ def test_tiled_layout_round_trip_and_parity(cuda, n, P, deg):
         assert torch.all(eng.X[-1, :, P % T:] == 0)
     dsq, dmax = eng.deviation()
     check_dev(want, dsq.cpu().numpy(), float(dmax.item()), M.column_mean(want))
+
+
+@pytest.mark.parametrize("layout", ["tiled", "rows"])
+def test_doubly_stochastic_mean_from_inputs(cuda, layout):
+    """For doubly stochastic W the fused deviation takes the column mean from the round's inputs
+    (one LDS pass); it must agree with the general two-pass path and with the oracle."""
+    from distributed_learning_amd.graph import from_edge_weights, random_regular_edges
+    E = eng_mod()
+    n, P = 512, 8192 + 40
+    edges = random_regular_edges(4, n, seed=3)
+    csr = from_edge_weights(edges, [0.19] * len(edges), list(range(n)))
+    assert csr.doubly_stochastic
+    rng = np.random.default_rng(8)
+    X = rng.standard_normal((n, P), dtype=np.float32)
+    G = rng.standard_normal((n, P), dtype=np.float32)
+    want = cref.mix_round(X, csr.rowptr, csr.col, csr.w, G=G, lr=0.02)
+    out = {}
+    for ds in (1, 0):
+        eng = E.GossipEngine(csr, P, device=cuda, X=torch.from_numpy(X).to(cuda), layout=layout)
+        eng.W.doubly_stochastic = ds
+        mean = torch.empty(P, device=cuda)
+        eng.round(G=eng.layout_like(torch.from_numpy(G).to(cuda)), lr=0.02, deviation=True,
+                  mean=mean)
+        torch.cuda.synchronize()
+        assert np.array_equal(bits(eng.rows().cpu().numpy()), bits(want))
+        check_dev(want, eng.dev_sq.cpu().numpy(), float(eng.dev_max.item()), mean.cpu().numpy())
+        out[ds] = eng.dev_sq.cpu().numpy()
+    np.testing.assert_allclose(out[1], out[0], rtol=1e-5)

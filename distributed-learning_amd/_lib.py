@@ -60,7 +60,7 @@ SIGNATURES = {
     "dl_column_sum": (_i32, [_vp, _i64, _i32, _i64, _vp, _vp]),
     "dl_max_column_std": (_i32, [_vp, _i64, _i32, _i64, _vp, _vp]),
     "dl_step_rows": (_i32, [_vp, _i64, _vp, _i64, _f32, _vp, _i32, _i64, _vp, _i64, _vp]),
-    "dl_stream_copy": (_i32, [_vp, _vp, _i64, _vp]),
+    "dl_stream_copy": (_i32, [_vp, _vp, _i64, _i32, _vp]),
     "dl_perron_workspace_bytes": (_sz, [_i32, _i32, _i64]),
     "dl_perron_round": (_i32, [ctypes.POINTER(DlPerronArgs), _vp, _sz, _vp]),
 }

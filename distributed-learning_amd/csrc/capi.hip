@@ -207,6 +207,10 @@ dl::TileArgs tile_args(const dl_mix_args *a) {
     t.nnz = a->W.nnz;
     t.regular = a->W.uniform_row_nnz;
     t.mean_from_inputs = (a->W.doubly_stochastic && a->n_halo == 0) ? 1 : 0;
+    {
+        const char *nt = getenv("DLAMD_NT_STORE");  // experiment knob: non-temporal y stores
+        t.nt_store = (nt && nt[0] == '1') ? 1 : 0;
+    }
     t.n_params = a->n_params;
     t.lr = a->lr;
     bool vec = aligned16(a->x) && aligned16(a->y) && a->ldx % 4 == 0 && a->ldy % 4 == 0;
@@ -570,11 +574,15 @@ int dl_step_rows(const float *x, int64_t ldx, const float *g, int64_t ldg, float
     return e == hipSuccess ? DL_OK : hip_fail(e, "step_rows launch");
 }
 
-int dl_stream_copy(const float *src, float *dst, int64_t n_floats, dl_stream_t stream) {
+int dl_stream_copy(const float *src, float *dst, int64_t n_floats, int32_t variant,
+                   dl_stream_t stream) {
     g_err.clear();
-    if (!src || !dst || n_floats < 0 || (n_floats & 3) || !aligned16(src) || !aligned16(dst))
-        return fail(DL_ERR_INVALID, "dl_stream_copy: needs 16-byte aligned buffers, n %% 4 == 0");
-    hipError_t e = dl::launch_stream_copy(src, dst, n_floats, static_cast<hipStream_t>(stream));
+    if (!src || !dst || n_floats < 0 || (n_floats & 3) || !aligned16(src) || !aligned16(dst) ||
+        variant < 0 || variant > 2)
+        return fail(DL_ERR_INVALID, "dl_stream_copy: needs 16-byte aligned buffers, n %% 4 == 0, "
+                                    "variant 0..2");
+    hipError_t e = dl::launch_stream_copy(src, dst, n_floats, variant,
+                                          static_cast<hipStream_t>(stream));
     return e == hipSuccess ? DL_OK : hip_fail(e, "stream_copy launch");
 }
 

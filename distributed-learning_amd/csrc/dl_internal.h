@@ -27,6 +27,7 @@ struct TileArgs {
     int32_t nnz;
     int32_t regular;  // >0: every row has exactly `regular` entries (row_ptr not staged)
     int32_t mean_from_inputs;  // 1: W doubly stochastic -> tile mean taken from the staged t
+    int32_t nt_store;          // 1: non-temporal stores of y (FAST path)
     int64_t n_params;
     int32_t n_tiles;
     int64_t col_base; // first column of tile 0
@@ -57,7 +58,8 @@ hipError_t launch_column_sum(const float *x, int64_t ldx, int n_rows, int64_t n_
 hipError_t launch_dev_rows(const float *x, int64_t ldx, int n_rows, int64_t n_params,
                            const float *mean, float *partial, int nparts, hipStream_t s);
 int dev_rows_parts(int64_t n_params);
-hipError_t launch_stream_copy(const float *src, float *dst, int64_t n_floats, hipStream_t s);
+hipError_t launch_stream_copy(const float *src, float *dst, int64_t n_floats, int variant,
+                              hipStream_t s);
 hipError_t launch_tile_convert(const float *src, float *dst, int64_t ld, int n_rows, int64_t n_params,
                                int tile_cols, bool to_tiled, hipStream_t s);
 hipError_t launch_max_column_std(const float *x, int64_t ldx, int n_rows, int64_t n_params,

@@ -21,6 +21,14 @@ namespace {
 
 __device__ __forceinline__ float4 zero4() { return make_float4(0.f, 0.f, 0.f, 0.f); }
 
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// 16-byte non-temporal store (global_store_dwordx4 ... nt)
+__device__ __forceinline__ void nt_store4(float4 v, float4 *p) {
+    f32x4 x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, reinterpret_cast<f32x4 *>(p));
+}
+
 // Load 4 consecutive floats starting at column c0 of `row`; columns >= P read as 0.
 __device__ __forceinline__ float4 ld4(const float *__restrict__ row, int64_t c0, int64_t P,
                                       bool vec) {
@@ -276,8 +284,12 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
                 const int ag = s + k * SLOTS;
                 if (ag < Nr) {
                     const float4 acc = mix_row(ag);
-                    if (FAST)
-                        *at(yt, oy + (uint32_t)k * sy) = acc;
+                    if (FAST) {
+                        if (a.nt_store)
+                            nt_store4(acc, at(yt, oy + (uint32_t)k * sy));
+                        else
+                            *at(yt, oy + (uint32_t)k * sy) = acc;
+                    }
                     else
                         st4(a.y + (int64_t)ag * a.ldy, col0 + 4 * c, P, false, acc);
                     if (DEV) {
@@ -389,20 +401,30 @@ __global__ void __launch_bounds__(1024) dev_reduce_kernel(const float *__restric
     }
 }
 
-// Streaming copy (HBM ceiling measurement): float4, 4 loads in flight per thread per step.
+// Streaming copy (HBM ceiling measurement), float4.  Each workgroup moves 256 x U float4 per
+// step with all U loads of a thread in flight before its stores; NT = non-temporal stores.
+template <int U, bool NT>
 __global__ void __launch_bounds__(256) stream_copy_kernel(const float4 *__restrict__ src,
                                                           float4 *__restrict__ dst, int64_t n4) {
-    const int64_t stride = (int64_t)gridDim.x * 256;
-    int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    for (; i + 3 * stride < n4; i += 4 * stride) {
-        const float4 a = src[i], b = src[i + stride], c = src[i + 2 * stride],
-                     d = src[i + 3 * stride];
-        dst[i] = a;
-        dst[i + stride] = b;
-        dst[i + 2 * stride] = c;
-        dst[i + 3 * stride] = d;
+    const int64_t step = (int64_t)gridDim.x * 256 * U;
+    for (int64_t base = (int64_t)blockIdx.x * 256 * U; base < n4; base += step) {
+        float4 v[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const int64_t i = base + j * 256 + threadIdx.x;
+            if (i < n4) v[j] = src[i];
+        }
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const int64_t i = base + j * 256 + threadIdx.x;
+            if (i < n4) {
+                if (NT)
+                    nt_store4(v[j], dst + i);
+                else
+                    dst[i] = v[j];
+            }
+        }
     }
-    for (; i < n4; i += stride) dst[i] = src[i];
 }
 
 template <int C, int KV, bool SGD, bool DEV, bool MIX, bool HALO, bool FAST>
@@ -496,13 +518,21 @@ hipError_t launch_dev_reduce(const float *partial, int nparts, int n_rows, float
     return hipGetLastError();
 }
 
-hipError_t launch_stream_copy(const float *src, float *dst, int64_t n_floats, hipStream_t s) {
+hipError_t launch_stream_copy(const float *src, float *dst, int64_t n_floats, int variant,
+                              hipStream_t s) {
     const int64_t n4 = n_floats / 4;
-    int64_t grid = (n4 + 255) / 256;
-    if (grid > 256 * 8) grid = 256 * 8;
+    const int U = variant == 0 ? 1 : 8;
+    int64_t grid = (n4 + 256 * U - 1) / (256 * U);
+    const int64_t gmax = variant == 0 ? 256 * 8 : 256 * 4;
+    if (grid > gmax) grid = gmax;
     if (grid < 1) grid = 1;
-    hipLaunchKernelGGL(stream_copy_kernel, dim3((unsigned)grid), dim3(256), 0, s,
-                       reinterpret_cast<const float4 *>(src), reinterpret_cast<float4 *>(dst), n4);
+    auto f4s = reinterpret_cast<const float4 *>(src);
+    auto f4d = reinterpret_cast<float4 *>(dst);
+    switch (variant) {
+        case 0: hipLaunchKernelGGL((stream_copy_kernel<1, false>), dim3((unsigned)grid), dim3(256), 0, s, f4s, f4d, n4); break;
+        case 1: hipLaunchKernelGGL((stream_copy_kernel<8, false>), dim3((unsigned)grid), dim3(256), 0, s, f4s, f4d, n4); break;
+        default: hipLaunchKernelGGL((stream_copy_kernel<8, true>), dim3((unsigned)grid), dim3(256), 0, s, f4s, f4d, n4); break;
+    }
     return hipGetLastError();
 }
 

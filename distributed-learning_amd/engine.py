@@ -299,7 +299,9 @@ class GossipEngine:
         if A.shape != (self.n, self.P):
             raise ValueError(f"expected shape ({self.n}, {self.P}), got {tuple(A.shape)}")
         A = A.to(self.device, torch.float32)
-        return to_tiled(A, self.T) if self.layout == "tiled" else A.contiguous()
+        # always a buffer of its own: the engine ping-pongs X/Y and must never write into the
+        # caller's tensor
+        return to_tiled(A, self.T) if self.layout == "tiled" else A.contiguous().clone()
 
     def load_rows(self, X):
         self.X = self.layout_like(X)

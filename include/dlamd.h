@@ -143,9 +143,11 @@ int dl_step_rows(const float *x, int64_t ldx, const float *g, int64_t ldg, float
                  const int32_t *rows, int32_t n_sel, int64_t n_params, float *out, int64_t ldo,
                  dl_stream_t stream);
 
-/* dst[i] = src[i] for n_floats floats (float4 streaming copy).  Not on the reference path: the
- * bench uses it to measure the HBM copy ceiling next to the mix kernel's achieved bandwidth. */
-int dl_stream_copy(const float *src, float *dst, int64_t n_floats, dl_stream_t stream);
+/* dst[i] = src[i] for n_floats floats (float4 streaming copy; variant 0: one load in flight
+ * per thread, 1: eight, 2: eight + non-temporal stores).  Not on the reference path: the bench
+ * uses it to measure the HBM copy ceiling next to the mix kernel's achieved bandwidth. */
+int dl_stream_copy(const float *src, float *dst, int64_t n_floats, int32_t variant,
+                   dl_stream_t stream);
 
 /* One asyncio consensus round (consensus_asyncio.py:209-312) restated as synchronous Jacobi:
  *   y0_a = v_a * weight_a / mean_weight                              (:231)

@@ -32,6 +32,19 @@ def main():
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     print(json.dumps({"copy_ceiling_GBs": bench.copy_ceiling(dev)}), flush=True)
+    if args.cases == "nt":
+        edges = random_regular_edges(4, 1024, seed=0)
+        csr = from_edge_weights(edges, [0.2] * len(edges), list(range(1024)))
+        X = torch.randn(1024, 1 << 20, device=dev)
+        G = torch.randn(1024, 1 << 20, device=dev)
+        eng = engine.GossipEngine(csr, 1 << 20, device=dev, X=X)
+        Gl = eng.layout_like(G)
+        for nt in ("0", "1", "0", "1"):
+            os.environ["DLAMD_NT_STORE"] = nt
+            ms = time_it(lambda: eng.round(G=Gl, lr=1e-3, deviation=True), args.reps)
+            print(json.dumps({"nt_store": nt, "ms": ms, "GBs": 12 * 1024 * (1 << 20) / ms / 1e6}),
+                  flush=True)
+        return
     for n, P in [(1024, 1 << 20), (512, 1 << 21), (256, 1 << 22), (2048, 1 << 19)]:
         edges = random_regular_edges(4, n, seed=0)
         csr = from_edge_weights(edges, [0.2] * len(edges), sorted(set(u for e in edges for u in e)))

@@ -79,6 +79,29 @@ def copy_ceiling(dev, nbytes=4 << 30, reps=10):
     return max(best.values()), best
 
 
+def kernel_name(plan, sgd, dev, n_src):
+    """The mix_tile_kernel instantiation dl_mix_round launches for this plan (FAST path)."""
+    c = plan["tile_cols"] // 4
+    need = -(-n_src // (1024 // c))
+    kv = 2 if need <= 2 else 4 if need <= 4 else 8
+    b = lambda v: "true" if v else "false"  # noqa: E731
+    return f"mix_tile_kernel<{c}, {kv}, {b(sgd)}, {b(dev)}, true, false, true>"
+
+
+def traffic_from_profile(kname, path=os.path.join(ROOT, "profiles", "r01", "summary.json")):
+    """HBM bytes per launch of this kernel from the committed rocprofv3 PMC summary
+    (FETCH_SIZE x 2 + WRITE_SIZE, gfx950 correction), or None if it was not profiled."""
+    try:
+        with open(path) as f:
+            kernels = json.load(f)["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None, None
+    for name, e in kernels.items():
+        if kname in name and "hbm_bytes_per_launch" in e:
+            return e["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
+    return None, None
+
+
 def cpu_baseline(csr, n, P, cols, sgd, lr):
     """Bounded sample of the same round on the host: the reference algorithm restated in numpy
     (Mixer._mix_params_once + _get_deviation_dict, single thread) on all agents x `cols`
@@ -180,6 +203,8 @@ def main():
     achieved = bytes_per_round / (launch_ms / 1e3) / 1e9  # GB/s of the fused round launch
 
     if rank == 0:
+        kname = kernel_name(plan, sgd, True, n)
+        traffic, traffic_src = traffic_from_profile(kname)
         ceiling, ceiling_variants = copy_ceiling(dev)
         cpu = None
         if not args.no_cpu:
@@ -214,7 +239,8 @@ def main():
                            else "single GPU",
                        "plan": plan},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_source": traffic_src, "kernel_instance": kname,
                          "kernel": "mix_tile_kernel (+dev_reduce) per-round HIP-event time",
                          "bytes_per_launch": bytes_per_round, "launch_ms": launch_ms,
                          "measured_copy_ceiling_GBs": ceiling,

@@ -62,7 +62,7 @@ def copy_ceiling(dev, nbytes=4 << 30, reps=10):
     b = torch.empty_like(a)
 
     best = {}
-    for variant in (0, 1, 2):
+    for variant in (0, 1, 2, 3):
         def cp():
             _lib.check(lib.dl_stream_copy(_lib.ptr(a), _lib.ptr(b), a.numel(), variant,
                                           _lib.stream_handle(dev)), "dl_stream_copy")

@@ -44,6 +44,18 @@ class DlPerronArgs(ctypes.Structure):
                 ("conv_eps_rows", _vp)]
 
 
+class DlBgemmArgs(ctypes.Structure):
+    _fields_ = [("batch", _i32), ("M", _i32), ("N", _i32), ("K", _i32),
+                ("A", _vp), ("lda", _i64), ("sA", _i64), ("ta", _i32),
+                ("B", _vp), ("ldb", _i64), ("sB", _i64), ("tb", _i32),
+                ("C", _vp), ("ldc", _i64), ("sC", _i64), ("epi", _i32),
+                ("bias", _vp), ("s_bias", _i64), ("H", _vp), ("ldh", _i64), ("sH", _i64),
+                ("rowsum", _vp), ("s_rowsum", _i64)]
+
+
+EPI = {"none": 0, "bias": 1, "bias_relu": 2, "bias_tanh": 3, "bias_elu": 4, "drelu": 5,
+       "dtanh": 6, "delu": 7}
+
 # exported symbol -> (restype, argtypes); tests check every one is exported
 SIGNATURES = {
     "dl_abi_version": (_i32, []),
@@ -61,6 +73,8 @@ SIGNATURES = {
     "dl_max_column_std": (_i32, [_vp, _i64, _i32, _i64, _vp, _vp]),
     "dl_step_rows": (_i32, [_vp, _i64, _vp, _i64, _f32, _vp, _i32, _i64, _vp, _i64, _vp]),
     "dl_stream_copy": (_i32, [_vp, _vp, _i64, _i32, _vp]),
+    "dl_bgemm": (_i32, [ctypes.POINTER(DlBgemmArgs), _vp]),
+    "dl_xent_grad": (_i32, [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i32, _i32, _i32, _vp]),
     "dl_perron_workspace_bytes": (_sz, [_i32, _i32, _i64]),
     "dl_perron_round": (_i32, [ctypes.POINTER(DlPerronArgs), _vp, _sz, _vp]),
 }

@@ -28,6 +28,7 @@ struct TileArgs {
     int32_t regular;  // >0: every row has exactly `regular` entries (row_ptr not staged)
     int32_t mean_from_inputs;  // 1: W doubly stochastic -> tile mean taken from the staged t
     int32_t nt_store;          // 1: non-temporal stores of y (FAST path)
+    int32_t nt_load;           // 1: non-temporal loads of x, g (FAST path)
     int64_t n_params;
     int32_t n_tiles;
     int64_t col_base; // first column of tile 0
@@ -89,5 +90,39 @@ int perron_tile_cols(int dtype, int n_rows, int64_t n_params);
 hipError_t launch_perron_single(const PerronArgs &a, int dtype, int tile_cols, hipStream_t s);
 hipError_t launch_perron_step(const PerronArgs &a, int dtype, int tile_cols, const void *yin,
                               void *yout, bool prescale, hipStream_t s);
+
+enum Epi {
+    EPI_NONE = 0,
+    EPI_BIAS = 1,
+    EPI_BIAS_RELU = 2,
+    EPI_BIAS_TANH = 3,
+    EPI_BIAS_ELU = 4,
+    EPI_DRELU = 5,
+    EPI_DTANH = 6,
+    EPI_DELU = 7
+};
+
+struct BgemmArgs {
+    int32_t batch, M, N, K;
+    const float *A;
+    int64_t lda, sA;
+    int32_t ta;
+    const float *B;
+    int64_t ldb, sB;
+    int32_t tb;
+    float *C;
+    int64_t ldc, sC;
+    int32_t epi;
+    const float *bias;
+    int64_t sBias;
+    const float *H;
+    int64_t ldh, sH;
+    float *rowsum;
+    int64_t sR;
+};
+hipError_t launch_bgemm(const BgemmArgs &p, hipStream_t s);
+hipError_t launch_xent_grad(const float *Z, int64_t sZ, const int32_t *y, int64_t sY, float *dZ,
+                            int64_t sD, float *loss, int batch, int rows, int classes,
+                            hipStream_t s);
 
 }  // namespace dl

@@ -23,6 +23,12 @@ __device__ __forceinline__ float4 zero4() { return make_float4(0.f, 0.f, 0.f, 0.
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// 16-byte non-temporal load (global_load_dwordx4 ... nt): streamed once, keep it out of L2/MALL
+__device__ __forceinline__ float4 nt_load4(const float4 *p) {
+    const f32x4 x = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(p));
+    return make_float4(x.x, x.y, x.z, x.w);
+}
+
 // 16-byte non-temporal store (global_store_dwordx4 ... nt)
 __device__ __forceinline__ void nt_store4(float4 v, float4 *p) {
     f32x4 x = {v.x, v.y, v.z, v.w};
@@ -164,11 +170,20 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
             const float *xt = reinterpret_cast<const float *>(tile_base(a.x, a.xts, tile_id));
             const float *gt =
                 SGD ? reinterpret_cast<const float *>(tile_base(a.g, a.gts, tile_id)) : nullptr;
+            if (a.nt_load) {
 #pragma unroll
-            for (int k = 0; k < KV; ++k) {
-                const bool ok = s + k * SLOTS < R;
-                px[k] = *at(xt, ok ? ox + k * sx : 16u * c);
-                if (SGD) pg[k] = *at(gt, ok ? og + k * sg : 16u * c);
+                for (int k = 0; k < KV; ++k) {
+                    const bool ok = s + k * SLOTS < R;
+                    px[k] = nt_load4(at(xt, ok ? ox + k * sx : 16u * c));
+                    if (SGD) pg[k] = nt_load4(at(gt, ok ? og + k * sg : 16u * c));
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < KV; ++k) {
+                    const bool ok = s + k * SLOTS < R;
+                    px[k] = *at(xt, ok ? ox + k * sx : 16u * c);
+                    if (SGD) pg[k] = *at(gt, ok ? og + k * sg : 16u * c);
+                }
             }
         } else {
             const int64_t cc = col0 + 4 * c;
@@ -234,6 +249,20 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
         }
     };
 
+    // one pass of the FAST prefetch (used to refill px[k]/pg[k] as soon as pass k is staged)
+    auto prefetch_pass = [&](int tile_id, int k) {
+        const float *xt = reinterpret_cast<const float *>(tile_base(a.x, a.xts, tile_id));
+        const bool ok = s + k * SLOTS < R;
+        const uint32_t o1 = ok ? ox + k * sx : 16u * c;
+        px[k] = a.nt_load ? nt_load4(at(xt, o1)) : *at(xt, o1);
+        if (SGD) {
+            const float *gt = reinterpret_cast<const float *>(tile_base(a.g, a.gts, tile_id));
+            const uint32_t o2 = ok ? og + k * sg : 16u * c;
+            pg[k] = a.nt_load ? nt_load4(at(gt, o2)) : *at(gt, o2);
+        }
+    };
+    constexpr bool EARLY = FAST && !HALO;  // refill each pass right after staging it
+
     int tile_id = blockIdx.x;
     if (tile_id < a.n_tiles) prefetch(tile_id);
     for (; tile_id < a.n_tiles; tile_id += gridDim.x) {
@@ -244,11 +273,13 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
         if (MIX) {
             // stage the (stepped) tile of every source row in LDS
             float4 cst = zero4();  // column partial sums of t (doubly stochastic W only)
+            const bool more = nxt < a.n_tiles;
 #pragma unroll
             for (int k = 0; k < KV; ++k) {
                 const int r = s + k * SLOTS;
                 float4 t = px[k];
                 if (SGD && (!HALO || r < Nr)) t = local_step(t, pg[k], a.lr);
+                if (EARLY && more) prefetch_pass(nxt, k);  // in flight across the barrier
                 if (r < R) {
                     tile[r * C + c] = t;
                     if (DEV) add4(cst, t);
@@ -273,7 +304,7 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
                 mean_t.z = mean_t.z / n;
                 mean_t.w = mean_t.w / n;
             }
-            if (nxt < a.n_tiles) prefetch(nxt);  // lands while we mix from LDS
+            if (!EARLY && nxt < a.n_tiles) prefetch(nxt);  // lands while we mix from LDS
             float *yt = const_cast<float *>(
                 reinterpret_cast<const float *>(tile_base(a.y, a.yts, tile_id)));
             float4 cs = zero4();
@@ -403,7 +434,7 @@ __global__ void __launch_bounds__(1024) dev_reduce_kernel(const float *__restric
 
 // Streaming copy (HBM ceiling measurement), float4.  Each workgroup moves 256 x U float4 per
 // step with all U loads of a thread in flight before its stores; NT = non-temporal stores.
-template <int U, bool NT>
+template <int U, bool NT, bool NTL = false>
 __global__ void __launch_bounds__(256) stream_copy_kernel(const float4 *__restrict__ src,
                                                           float4 *__restrict__ dst, int64_t n4) {
     const int64_t step = (int64_t)gridDim.x * 256 * U;
@@ -412,7 +443,7 @@ __global__ void __launch_bounds__(256) stream_copy_kernel(const float4 *__restri
 #pragma unroll
         for (int j = 0; j < U; ++j) {
             const int64_t i = base + j * 256 + threadIdx.x;
-            if (i < n4) v[j] = src[i];
+            if (i < n4) v[j] = NTL ? nt_load4(src + i) : src[i];
         }
 #pragma unroll
         for (int j = 0; j < U; ++j) {
@@ -521,9 +552,9 @@ hipError_t launch_dev_reduce(const float *partial, int nparts, int n_rows, float
 hipError_t launch_stream_copy(const float *src, float *dst, int64_t n_floats, int variant,
                               hipStream_t s) {
     const int64_t n4 = n_floats / 4;
-    const int U = variant == 0 ? 1 : 8;
+    const int U = variant == 0 ? 1 : variant == 3 ? 4 : 8;
     int64_t grid = (n4 + 256 * U - 1) / (256 * U);
-    const int64_t gmax = variant == 0 ? 256 * 8 : 256 * 4;
+    const int64_t gmax = variant == 0 ? 256 * 8 : variant == 3 ? 256 * 32 : 256 * 4;
     if (grid > gmax) grid = gmax;
     if (grid < 1) grid = 1;
     auto f4s = reinterpret_cast<const float4 *>(src);
@@ -531,7 +562,8 @@ hipError_t launch_stream_copy(const float *src, float *dst, int64_t n_floats, in
     switch (variant) {
         case 0: hipLaunchKernelGGL((stream_copy_kernel<1, false>), dim3((unsigned)grid), dim3(256), 0, s, f4s, f4d, n4); break;
         case 1: hipLaunchKernelGGL((stream_copy_kernel<8, false>), dim3((unsigned)grid), dim3(256), 0, s, f4s, f4d, n4); break;
-        default: hipLaunchKernelGGL((stream_copy_kernel<8, true>), dim3((unsigned)grid), dim3(256), 0, s, f4s, f4d, n4); break;
+        case 2: hipLaunchKernelGGL((stream_copy_kernel<8, true>), dim3((unsigned)grid), dim3(256), 0, s, f4s, f4d, n4); break;
+        default: hipLaunchKernelGGL((stream_copy_kernel<4, true, true>), dim3((unsigned)grid), dim3(256), 0, s, f4s, f4d, n4); break;
     }
     return hipGetLastError();
 }

@@ -1,0 +1,109 @@
+"""Batched per-agent ANNModel gradients on the GPU (BASELINE config c3).
+
+The reference trains each agent's ``ANNModel`` (networks/ann_model.py:4-45) separately with torch
+autograd and a cross-entropy loss; consensus then mixes the flattened parameters (mixer.py:69).
+Here all agents' parameters are rows of one matrix X[N, P] (the Mixer flatten order: fc1.w,
+fc1.b, fc2.w, fc2.b, fc3.w, fc3.b, fc4.w, fc4.b), and one step runs 4 forward and 7 backward
+batched fp32-MFMA GEMMs over every agent at once (``dl_bgemm``), with bias/activation fused into
+the forward epilogues, activation derivatives fused into the backward ones, and weight/bias
+gradients written directly into each agent's row of G -- the G that the fused local step of
+``dl_mix_round`` consumes.  No per-agent Python loop, no autograd graph.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from .. import _lib
+from .ann_model import ANNModel
+
+
+class BatchedANN:
+    def __init__(self, n_agents, batch, input_dim=784, hidden_dim=150, output_dim=10,
+                 device="cuda"):
+        self.N, self.B = int(n_agents), int(batch)
+        self.din, self.dh, self.dout = int(input_dim), int(hidden_dim), int(output_dim)
+        if self.dout > 64:
+            raise ValueError("the cross-entropy head supports at most 64 classes")
+        self.device = torch.device(device)
+        self.offsets = {}
+        off = 0
+        for name, shape in ANNModel.param_shapes(self.din, self.dh, self.dout):
+            self.offsets[name] = off
+            off += int(np.prod(shape))
+        self.P = off
+        f = lambda *s: torch.empty(*s, dtype=torch.float32, device=self.device)  # noqa: E731
+        self.H1, self.H2, self.H3 = (f(self.N, self.B, self.dh) for _ in range(3))
+        self.Z4 = f(self.N, self.B, self.dout)
+        self.dZ4 = f(self.N, self.B, self.dout)
+        self.dZa, self.dZb = f(self.N, self.B, self.dh), f(self.N, self.B, self.dh)
+        self.loss = f(self.N)
+
+    # -------------------------------------------------------------- helpers
+    def _gemm(self, M, N, K, A, lda, sA, ta, B, ldb, sB, tb, C, ldc, sC, epi="none", bias=None,
+              H=None, rowsum=None, X=None):
+        lib = _lib.load()
+
+        def p(t, off=0):
+            if t is None:
+                return None
+            return ctypes.c_void_p(t.data_ptr() + 4 * off)
+        args = _lib.DlBgemmArgs(
+            self.N, M, N, K, p(*A), lda, sA, int(ta), p(*B), ldb, sB, int(tb), p(*C), ldc, sC,
+            _lib.EPI[epi], p(*bias) if bias else None, self.P if bias else 0,
+            p(H) if H is not None else None, self.dh if H is not None else 0,
+            self.B * self.dh if H is not None else 0,
+            p(*rowsum) if rowsum else None, self.P if rowsum else 0)
+        _lib.check(lib.dl_bgemm(ctypes.byref(args), _lib.stream_handle(self.device)), "dl_bgemm")
+
+    def gradients(self, X, data, labels, G):
+        """G[a] = d loss_a / d params_a for every agent.  X, G: [N, P] row-major fp32 (row stride
+        may exceed P); data: [N, B, input_dim] fp32; labels: [N, B] int32.  Returns the per-agent
+        mean cross-entropy (device tensor [N])."""
+        lib = _lib.load()
+        N, B, din, dh, dout, P = self.N, self.B, self.din, self.dh, self.dout, self.P
+        for t, shape in ((X, (N, P)), (G, (N, P))):
+            if tuple(t.shape) != shape or t.stride(1) != 1 or t.dtype != torch.float32:
+                raise ValueError(f"expected a row-major fp32 [{N}, {P}] tensor")
+        if tuple(data.shape) != (N, B, din) or not data.is_contiguous():
+            raise ValueError(f"data must be contiguous [{N}, {B}, {din}] fp32")
+        if tuple(labels.shape) != (N, B) or labels.dtype != torch.int32:
+            raise ValueError(f"labels must be int32 [{N}, {B}]")
+        sx, sg = X.stride(0), G.stride(0)
+        o = self.offsets
+        hs = B * dh
+        # ---- forward: H1 = relu(x W1^T + b1), H2 = tanh(.), H3 = elu(.), Z4 = H3 W4^T + b4
+        self._gemm(B, dh, din, (data,), din, B * din, 0, (X, o["fc1.weight"]), din, sx, 1,
+                   (self.H1,), dh, hs, "bias_relu", bias=(X, o["fc1.bias"]))
+        self._gemm(B, dh, dh, (self.H1,), dh, hs, 0, (X, o["fc2.weight"]), dh, sx, 1,
+                   (self.H2,), dh, hs, "bias_tanh", bias=(X, o["fc2.bias"]))
+        self._gemm(B, dh, dh, (self.H2,), dh, hs, 0, (X, o["fc3.weight"]), dh, sx, 1,
+                   (self.H3,), dh, hs, "bias_elu", bias=(X, o["fc3.bias"]))
+        self._gemm(B, dout, dh, (self.H3,), dh, hs, 0, (X, o["fc4.weight"]), dh, sx, 1,
+                   (self.Z4,), dout, B * dout, "bias", bias=(X, o["fc4.bias"]))
+        _lib.check(lib.dl_xent_grad(_lib.ptr(self.Z4), B * dout, _lib.ptr(labels), B,
+                                    _lib.ptr(self.dZ4), B * dout, _lib.ptr(self.loss), N, B, dout,
+                                    _lib.stream_handle(self.device)), "dl_xent_grad")
+        # ---- backward (weight grads straight into G rows, bias grads as row sums of dZ^T)
+        self._gemm(dout, dh, B, (self.dZ4,), dout, B * dout, 1, (self.H3,), dh, hs, 0,
+                   (G, o["fc4.weight"]), dh, sg, rowsum=(G, o["fc4.bias"]))
+        self._gemm(B, dh, dout, (self.dZ4,), dout, B * dout, 0, (X, o["fc4.weight"]), dh, sx, 0,
+                   (self.dZa,), dh, hs, "delu", H=self.H3)                  # dZ3
+        self._gemm(dh, dh, B, (self.dZa,), dh, hs, 1, (self.H2,), dh, hs, 0,
+                   (G, o["fc3.weight"]), dh, sg, rowsum=(G, o["fc3.bias"]))
+        self._gemm(B, dh, dh, (self.dZa,), dh, hs, 0, (X, o["fc3.weight"]), dh, sx, 0,
+                   (self.dZb,), dh, hs, "dtanh", H=self.H2)                 # dZ2
+        self._gemm(dh, dh, B, (self.dZb,), dh, hs, 1, (self.H1,), dh, hs, 0,
+                   (G, o["fc2.weight"]), dh, sg, rowsum=(G, o["fc2.bias"]))
+        self._gemm(B, dh, dh, (self.dZb,), dh, hs, 0, (X, o["fc2.weight"]), dh, sx, 0,
+                   (self.dZa,), dh, hs, "drelu", H=self.H1)                 # dZ1
+        self._gemm(dh, din, B, (self.dZa,), dh, hs, 1, (data,), din, B * din, 0,
+                   (G, o["fc1.weight"]), din, sg, rowsum=(G, o["fc1.bias"]))
+        return self.loss
+
+    def flops_per_step(self):
+        B, din, dh, dout = self.B, self.din, self.dh, self.dout
+        fwd = 2 * B * (din * dh + 2 * dh * dh + dh * dout)
+        bwd_w = fwd
+        bwd_x = 2 * B * (dout * dh + 2 * dh * dh)
+        return self.N * (fwd + bwd_w + bwd_x)

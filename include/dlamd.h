@@ -144,7 +144,8 @@ int dl_step_rows(const float *x, int64_t ldx, const float *g, int64_t ldg, float
                  dl_stream_t stream);
 
 /* dst[i] = src[i] for n_floats floats (float4 streaming copy; variant 0: one load in flight
- * per thread, 1: eight, 2: eight + non-temporal stores).  Not on the reference path: the bench
+ * per thread, 1: eight, 2: eight + non-temporal stores, 3: four + non-temporal loads and
+ * stores on a 8192-workgroup grid).  Not on the reference path: the bench
  * uses it to measure the HBM copy ceiling next to the mix kernel's achieved bandwidth. */
 int dl_stream_copy(const float *src, float *dst, int64_t n_floats, int32_t variant,
                    dl_stream_t stream);
@@ -179,6 +180,37 @@ typedef struct dl_perron_args {
 size_t dl_perron_workspace_bytes(int32_t dtype, int32_t n_rows, int64_t n_params);
 int dl_perron_round(const dl_perron_args *args, void *workspace, size_t ws_bytes,
                     dl_stream_t stream);
+
+/* ---------------------------------------------------------------- batched per-agent GEMMs
+ * BASELINE config c3: every agent trains its own ANNModel (networks/ann_model.py:4-45) on its own
+ * batch; the reference runs torch autograd per agent.  Here one launch covers all agents:
+ *   C[b] = epi( op(A[b]) . op(B[b]) )      b < batch,  op(A) is M x K,  op(B) is K x N
+ * ta: A stored [K][M] (row stride lda) instead of [M][K];  tb: B stored [N][K] instead of [K][N].
+ * epi: DL_EPI_BIAS[_RELU|_TANH|_ELU] add bias[b][n] then activate (forward);
+ *      DL_EPI_D{RELU,TANH,ELU} multiply by the activation derivative read from the layer's
+ *      OUTPUT H[b] (ldh) (backward);  rowsum (nullable) receives sum_k op(A)[b][m][k] (the
+ *      bias gradient when op(A) = dZ^T).  fp32 MFMA (16x16x4), exact fp32 products. */
+enum dl_epilogue {
+    DL_EPI_NONE = 0, DL_EPI_BIAS = 1, DL_EPI_BIAS_RELU = 2, DL_EPI_BIAS_TANH = 3,
+    DL_EPI_BIAS_ELU = 4, DL_EPI_DRELU = 5, DL_EPI_DTANH = 6, DL_EPI_DELU = 7
+};
+typedef struct dl_bgemm_args {
+    int32_t batch, M, N, K;
+    const float *A; int64_t lda, sA; int32_t ta;  /* sA: batch stride (elements) */
+    const float *B; int64_t ldb, sB; int32_t tb;
+    float *C; int64_t ldc, sC;
+    int32_t epi;
+    const float *bias; int64_t s_bias;
+    const float *H; int64_t ldh, sH;
+    float *rowsum; int64_t s_rowsum;
+} dl_bgemm_args;
+int dl_bgemm(const dl_bgemm_args *args, dl_stream_t stream);
+
+/* Cross-entropy head (torch.nn.CrossEntropyLoss, mean): dZ[b] = (softmax(Z[b]) - onehot(y[b]))
+ * / rows and loss[b] (nullable) = mean_r (logsumexp(Z[b][r]) - Z[b][r][y]).  Z, dZ: [batch]
+ * [rows][classes] with batch strides; classes <= 64. */
+int dl_xent_grad(const float *Z, int64_t sZ, const int32_t *y, int64_t sY, float *dZ, int64_t sD,
+                 float *loss, int32_t batch, int32_t rows, int32_t classes, dl_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -39,11 +39,14 @@ def main():
         G = torch.randn(1024, 1 << 20, device=dev)
         eng = engine.GossipEngine(csr, 1 << 20, device=dev, X=X)
         Gl = eng.layout_like(G)
-        for nt in ("0", "1", "0", "1"):
-            os.environ["DLAMD_NT_STORE"] = nt
-            ms = time_it(lambda: eng.round(G=Gl, lr=1e-3, deviation=True), args.reps)
-            print(json.dumps({"nt_store": nt, "ms": ms, "GBs": 12 * 1024 * (1 << 20) / ms / 1e6}),
-                  flush=True)
+        for rep in range(2):
+            for ntl in ("1",):
+                for nts in ("1",):
+                    os.environ["DLAMD_NT_STORE"] = nts
+                    os.environ["DLAMD_NT_LOAD"] = ntl
+                    ms = time_it(lambda: eng.round(G=Gl, lr=1e-3, deviation=True), args.reps)
+                    print(json.dumps({"nt_load": ntl, "nt_store": nts, "ms": ms,
+                                      "GBs": 12 * 1024 * (1 << 20) / ms / 1e6}), flush=True)
         return
     for n, P in [(1024, 1 << 20), (512, 1 << 21), (256, 1 << 22), (2048, 1 << 19)]:
         edges = random_regular_edges(4, n, seed=0)

@@ -162,10 +162,10 @@ int check_mix_args(const dl_mix_args *a) {
         return fail(DL_ERR_INVALID, "dl_mix_round: ldg < n_params");
     if (a->n_halo > 0 && (!a->halo || a->ldh < a->n_params))
         return fail(DL_ERR_INVALID, "dl_mix_round: n_halo > 0 needs halo with ldh >= n_params");
-    if (a->tile_cols < 0 || (a->tile_cols > 0 && (a->tile_cols % 4 || a->tile_cols < 16 ||
+    if (a->tile_cols < 0 || (a->tile_cols > 0 && (a->tile_cols % 4 || a->tile_cols < 4 ||
                                                    a->tile_cols > 4 * dl::kMaxChunks ||
                                                    (a->tile_cols & (a->tile_cols - 1)))))
-        return fail(DL_ERR_INVALID, "dl_mix_round: tile_cols must be 0 or a power of two in [16, %d]",
+        return fail(DL_ERR_INVALID, "dl_mix_round: tile_cols must be 0 or a power of two in [4, %d]",
                     4 * dl::kMaxChunks);
     if (a->tile_cols > 0 && a->n_halo > 0)
         return fail(DL_ERR_INVALID, "dl_mix_round: the column-tiled layout takes no halo rows");
@@ -229,7 +229,8 @@ dl::TileArgs tile_args(const dl_mix_args *a) {
               (!a->mean || aligned16(a->mean));
         t.tiled = 1;
     } else if (((R - 1) * a->ldx + 128) * 4 >= lim || ((R - 1) * a->ldy + 128) * 4 >= lim ||
-               (a->g && ((R - 1) * a->ldg + 128) * 4 >= lim)) {
+               (a->g && ((R - 1) * a->ldg + 128) * 4 >= lim) ||
+        (a->n_halo > 0 && ((int64_t)(a->n_halo - 1) * a->ldh + 128) * 4 >= lim)) {
         vec = false;
     }
     t.vec = vec ? 1 : 0;
@@ -353,6 +354,7 @@ int dl_mix_round(const dl_mix_args *args, void *workspace, size_t ws_bytes, dl_s
             t.xrs = (uint32_t)(args->ldx * 4);
             t.grs = (uint32_t)(args->ldg * 4);
             t.yrs = (uint32_t)(args->ldy * 4);
+            t.hrs = (uint32_t)(args->ldh * 4);
         }
         const int64_t n_full = t.tiled ? pl.pub.n_tiles : (t.vec ? args->n_params / T : 0);
         const int64_t n_tail = pl.pub.n_tiles - n_full;  // 0 or 1 when vec, else all tiles
@@ -504,7 +506,7 @@ int dl_deviation_tiled(const float *x, int32_t n_rows, int64_t n_params, int32_t
                        size_t ws_bytes, dl_stream_t stream) {
     g_err.clear();
     hipStream_t s = static_cast<hipStream_t>(stream);
-    if (!x || n_rows <= 0 || n_params <= 0 || tile_cols < 16 || tile_cols > 4 * dl::kMaxChunks ||
+    if (!x || n_rows <= 0 || n_params <= 0 || tile_cols < 4 || tile_cols > 4 * dl::kMaxChunks ||
         (tile_cols & (tile_cols - 1)))
         return fail(DL_ERR_INVALID, "dl_deviation_tiled: bad x/n_rows/n_params/tile_cols");
     char *ws = static_cast<char *>(workspace);

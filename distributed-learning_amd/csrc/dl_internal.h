@@ -42,6 +42,7 @@ struct TileArgs {
     int32_t tiled;
     int64_t xts, gts, yts;
     uint32_t xrs, grs, yrs;
+    uint32_t hrs;     // halo row stride in bytes (ldh*4)
     float *dev_partial;  // [gridDim.x][n_rows] per-workgroup partial ||y_a - mean||^2
     float *mean;         // [n_params] nullable
 };

@@ -156,17 +156,38 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
     float4 *scratch = reinterpret_cast<float4 *>(smem + a.scratch_off);
 
     float4 px[KV], pg[KV];
-    // per-agent ||y - mean||^2 accumulators.  When KV <= C they are spread over the C lanes of a
-    // row group (lane c keeps pass k == c): one register instead of KV.
-    constexpr bool DIST = KV <= C;
-    constexpr int ND = DIST ? 1 : KV;
+    // per-agent ||y - mean||^2 accumulators, spread over the C lanes of a row group: lane c keeps
+    // the passes k with k % C == c (slot k / C), so ceil(KV / C) registers instead of KV.
+    constexpr int ND = KV <= C ? 1 : KV / C;
     float dacc[ND];
 #pragma unroll
     for (int k = 0; k < ND; ++k) dacc[k] = 0.f;
 
     auto prefetch = [&](int tile_id) {
         const int64_t col0 = a.col_base + (int64_t)tile_id * T;
-        if (FAST && !HALO) {
+        if (FAST && HALO) {
+            // local rows from x/g (32-bit offsets), halo rows from the halo buffer (row-major,
+            // ldh); the per-lane base select keeps every pass straight-line code
+            const char *xt = tile_base(a.x, a.xts, tile_id);
+            const char *gt = SGD ? tile_base(a.g, a.gts, tile_id) : nullptr;
+            const char *ht = reinterpret_cast<const char *>(a.halo) + col0 * 4;
+#pragma unroll
+            for (int k = 0; k < KV; ++k) {
+                const int r = s + k * SLOTS;
+                const bool loc = r < Nr;
+                const bool ok = r < R;
+                const uint32_t oh = (uint32_t)(r - Nr) * a.hrs + 16u * c;
+                const char *bx = loc || !ok ? xt : ht;
+                const uint32_t o1 = loc ? ox + k * sx : ok ? oh : 16u * c;
+                const float4 *p1 = reinterpret_cast<const float4 *>(bx + o1);
+                px[k] = a.nt_load ? nt_load4(p1) : *p1;
+                if (SGD) {
+                    const float4 *p2 =
+                        reinterpret_cast<const float4 *>(gt + (loc ? og + k * sg : 16u * c));
+                    pg[k] = a.nt_load ? nt_load4(p2) : *p2;
+                }
+            }
+        } else if (FAST) {
             const float *xt = reinterpret_cast<const float *>(tile_base(a.x, a.xts, tile_id));
             const float *gt =
                 SGD ? reinterpret_cast<const float *>(tile_base(a.g, a.gts, tile_id)) : nullptr;
@@ -239,29 +260,12 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
         const float dx = y.x - mean.x, dy = y.y - mean.y;
         const float dz = y.z - mean.z, dw = y.w - mean.w;
         float v = (dx * dx + dy * dy) + (dz * dz + dw * dw);
-        if (DIST) {
 #pragma unroll
-            for (int m = 1; m < C; m <<= 1) v += __shfl_xor(v, m);  // sum over the row group
-            dacc[0] += (c == k) ? v : 0.f;
-        } else {
+        for (int m = 1; m < C; m <<= 1) v += __shfl_xor(v, m);  // sum over the row group
+        const bool mine = (k % C) == c;
 #pragma unroll
-            for (int j = 0; j < ND; ++j) dacc[j] += (j == k) ? v : 0.f;
-        }
+        for (int j = 0; j < ND; ++j) dacc[j] += (mine && j == k / C) ? v : 0.f;
     };
-
-    // one pass of the FAST prefetch (used to refill px[k]/pg[k] as soon as pass k is staged)
-    auto prefetch_pass = [&](int tile_id, int k) {
-        const float *xt = reinterpret_cast<const float *>(tile_base(a.x, a.xts, tile_id));
-        const bool ok = s + k * SLOTS < R;
-        const uint32_t o1 = ok ? ox + k * sx : 16u * c;
-        px[k] = a.nt_load ? nt_load4(at(xt, o1)) : *at(xt, o1);
-        if (SGD) {
-            const float *gt = reinterpret_cast<const float *>(tile_base(a.g, a.gts, tile_id));
-            const uint32_t o2 = ok ? og + k * sg : 16u * c;
-            pg[k] = a.nt_load ? nt_load4(at(gt, o2)) : *at(gt, o2);
-        }
-    };
-    constexpr bool EARLY = FAST && !HALO;  // refill each pass right after staging it
 
     int tile_id = blockIdx.x;
     if (tile_id < a.n_tiles) prefetch(tile_id);
@@ -273,13 +277,11 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
         if (MIX) {
             // stage the (stepped) tile of every source row in LDS
             float4 cst = zero4();  // column partial sums of t (doubly stochastic W only)
-            const bool more = nxt < a.n_tiles;
 #pragma unroll
             for (int k = 0; k < KV; ++k) {
                 const int r = s + k * SLOTS;
                 float4 t = px[k];
                 if (SGD && (!HALO || r < Nr)) t = local_step(t, pg[k], a.lr);
-                if (EARLY && more) prefetch_pass(nxt, k);  // in flight across the barrier
                 if (r < R) {
                     tile[r * C + c] = t;
                     if (DEV) add4(cst, t);
@@ -304,7 +306,7 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
                 mean_t.z = mean_t.z / n;
                 mean_t.w = mean_t.w / n;
             }
-            if (!EARLY && nxt < a.n_tiles) prefetch(nxt);  // lands while we mix from LDS
+            if (nxt < a.n_tiles) prefetch(nxt);  // lands while we mix from LDS
             float *yt = const_cast<float *>(
                 reinterpret_cast<const float *>(tile_base(a.y, a.yts, tile_id)));
             float4 cs = zero4();
@@ -360,18 +362,11 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
         __syncthreads();  // tile and scratch are rewritten by the next iteration
     }
     if (DEV) {
-        if (DIST) {
-            const int ag = s + c * SLOTS;
-            if (c < KV && ag < Nr) a.dev_partial[(int64_t)blockIdx.x * Nr + ag] = dacc[0];
-        } else {
 #pragma unroll
-            for (int k = 0; k < ND; ++k) {
-                float v = dacc[k];
-#pragma unroll
-                for (int m = 1; m < C; m <<= 1) v += __shfl_xor(v, m);
-                const int ag = s + k * SLOTS;
-                if (c == 0 && ag < Nr) a.dev_partial[(int64_t)blockIdx.x * Nr + ag] = v;
-            }
+        for (int j = 0; j < ND; ++j) {
+            const int k = j * C + c;  // the pass this lane's slot j holds
+            const int ag = s + k * SLOTS;
+            if (k < KV && ag < Nr) a.dev_partial[(int64_t)blockIdx.x * Nr + ag] = dacc[j];
         }
     }
 }
@@ -481,7 +476,7 @@ hipError_t launch_mode(const TileArgs &a, bool sgd, bool dev, bool mix, int grid
                : launch_one<C, KV, false, false, true, false, FAST>(a, grid, lds, s);
 }
 
-// FAST kernels: C in {4,8,16,32} x KV in {2,4,8}; guarded kernels: every C, KV = 8.
+// FAST kernels: every C x KV in {2,4,8}; guarded kernels: every C, KV = 8.
 template <int C>
 hipError_t launch_fast_c(const TileArgs &a, int kv, bool sgd, bool dev, bool mix, int grid,
                          int lds, hipStream_t s) {
@@ -495,15 +490,17 @@ hipError_t launch_fast_c(const TileArgs &a, int kv, bool sgd, bool dev, bool mix
 int tile_passes(int chunks, int n_src, bool fast) {
     const int slots = kTileThreads / chunks;
     const int need = (n_src + slots - 1) / slots;
-    if (!fast || chunks < 4) return kRowsPerThread;
+    if (!fast) return kRowsPerThread;
     return need <= 2 ? 2 : need <= 4 ? 4 : 8;
 }
 
 hipError_t launch_mix_tile(const TileArgs &a, int chunks, bool sgd, bool dev, bool mix, int grid,
                            int lds, bool fast, hipStream_t s) {
-    if (fast && chunks >= 4) {
+    if (fast) {
         const int kv = tile_passes(chunks, a.n_src, true);
         switch (chunks) {
+            case 1: return launch_fast_c<1>(a, kv, sgd, dev, mix, grid, lds, s);
+            case 2: return launch_fast_c<2>(a, kv, sgd, dev, mix, grid, lds, s);
             case 4: return launch_fast_c<4>(a, kv, sgd, dev, mix, grid, lds, s);
             case 8: return launch_fast_c<8>(a, kv, sgd, dev, mix, grid, lds, s);
             case 16: return launch_fast_c<16>(a, kv, sgd, dev, mix, grid, lds, s);

@@ -275,7 +275,7 @@ class GossipEngine:
         self.W = DeviceCsr(csr, self.device)
         self.n, self.P = csr.n_rows, int(n_params)
         plan = plan_shape(self.W, self.P, deviation=True)
-        tiled_ok = plan["path"] == 1 and plan["tile_cols"] >= 16 and self.W.n_src == self.n
+        tiled_ok = plan["path"] == 1 and plan["tile_cols"] >= 4 and self.W.n_src == self.n
         if layout == "auto":
             layout = "tiled" if tiled_ok else "rows"
         if layout == "tiled" and not tiled_ok:

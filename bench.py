@@ -37,6 +37,8 @@ def parse():
     p.add_argument("--cpu-cols", type=int, default=1 << 18,
                    help="columns of the bounded CPU-baseline sample (all agents)")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--dist-backend", default="nccl",
+                   help="nccl (= RCCL, default) or gloo (multi-rank rehearsal on one GPU)")
     return p.parse_args()
 
 
@@ -140,11 +142,15 @@ def main():
     if args.gpus != world and world > 1:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
     n_gpus = world
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
 
     from distributed_learning_amd import engine
 

@@ -8,7 +8,16 @@ stop test).  At N GPUs every rank owns a column stripe of 2^20 parameters for al
 per-agent deviation partials are all-reduced over RCCL every round, which is the round's real
 exchange step.  ``value`` = rounds/s in units of the 1024 x 2^20 workload, summed over ranks.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c2-mix]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c2-mix|c3|c4]
+
+Other BASELINE configs (not the headline line; run on request):
+  c3  ANNModel MLP consensus SGD, 256 agents x 164,560 params, B=64 synthetic MNIST-shaped
+      batches: batched per-agent gradients on fp32 MFMA (dl_bgemm) + the fused round.
+      N>1: independent replicas (one 256-agent system per GPU).
+  c4  64x64 periodic torus, 4096 agents x 2^18 params, best-constant weights.  N=1: the whole
+      torus on one GPU (tiled layout).  N>1: agents partitioned into 2-D torus blocks, one per
+      rank, boundary rows exchanged over RCCL send/recv every round (HaloShard), so the total
+      work is fixed (strong scaling).
 """
 import argparse
 import json
@@ -24,6 +33,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+FP32_MFMA_PEAK_TFLOPS = 157.3  # dense f32-input MFMA (MI355X_MICROARCH.md, peak FP32 matrix)
 
 
 def parse():
@@ -31,12 +41,13 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=10)
-    p.add_argument("--workload", default="c2", choices=["c2", "c2-mix"])
+    p.add_argument("--workload", default="c2", choices=["c2", "c2-mix", "c3", "c4"])
     p.add_argument("--agents", type=int, default=1024)
     p.add_argument("--params", type=int, default=1 << 20)
     p.add_argument("--cpu-cols", type=int, default=1 << 18,
                    help="columns of the bounded CPU-baseline sample (all agents)")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-graph", action="store_true", help="c3: eager launches, no hipGraph")
     p.add_argument("--dist-backend", default="nccl",
                    help="nccl (= RCCL, default) or gloo (multi-rank rehearsal on one GPU)")
     return p.parse_args()
@@ -134,6 +145,268 @@ def cpu_baseline(csr, n, P, cols, sgd, lr):
     return out
 
 
+def max_over_ranks(v, world, dev):
+    if world == 1:
+        return v
+    import torch.distributed as dist
+    t = torch.tensor([v], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def timed_loop(step, args, world, dev):
+    """W untimed warmup steps, then exactly K steps bracketed by barrier + synchronize on both
+    sides; step(i) gets the timed index (None during warmup).  Returns max-over-ranks seconds."""
+    for _ in range(args.warmup):
+        step(None)
+    torch.cuda.synchronize()
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    return max_over_ranks(time.perf_counter() - t0, world, dev)
+
+
+def event_pairs(k, n):
+    return [[torch.cuda.Event(enable_timing=True) for _ in range(n)] for _ in range(k)]
+
+
+def c3_init_rows(ann, gen):
+    """Random-init ANNModel weights for every agent in the flattened row layout: the torch
+    nn.Linear default, U(-1/sqrt(fan_in), 1/sqrt(fan_in)) for weight and bias."""
+    from distributed_learning_amd.networks.ann_model import ANNModel
+    X = torch.empty(ann.N, ann.P, device=ann.device)
+    for name, shape in ANNModel.param_shapes(ann.din, ann.dh, ann.dout):
+        layer = name.split(".")[0]
+        fan_in = {"fc1": ann.din}.get(layer, ann.dh)
+        o, sz = ann.offsets[name], int(np.prod(shape))
+        bound = 1.0 / np.sqrt(fan_in)
+        X[:, o:o + sz].uniform_(-bound, bound, generator=gen)
+    return X
+
+
+def c3_cpu_baseline(ann, csr, lr, n_agents_sample=16):
+    """The reference's CPU path for one c3 step: a per-agent torch autograd step of ANNModel
+    (networks/ann_model.py, CrossEntropyLoss) for every agent -- timed on a sample of agents and
+    scaled -- plus the numpy restatement of Mixer._mix_params_once + _get_deviation_dict on all
+    agents."""
+    from oracle import mixer_ref as M
+    from distributed_learning_amd.networks.ann_model import ANNModel
+    torch.manual_seed(0)
+    model = ANNModel(ann.din, ann.dh, ann.dout)
+    loss_fn = torch.nn.CrossEntropyLoss()
+    x = torch.randn(ann.B, ann.din)
+    y = torch.randint(0, ann.dout, (ann.B,))
+    opt = torch.optim.SGD(model.parameters(), lr=lr)
+
+    def agent_step():
+        opt.zero_grad()
+        loss_fn(model(x), y).backward()
+        opt.step()
+    agent_step()
+    t0 = time.perf_counter()
+    for _ in range(n_agents_sample):
+        agent_step()
+    t_grad = (time.perf_counter() - t0) / n_agents_sample * ann.N
+    rng = np.random.default_rng(0)
+    X = rng.standard_normal((ann.N, ann.P), dtype=np.float32)
+    t0 = time.perf_counter()
+    Y = M.mix_once(X, csr.rowptr, csr.col, csr.w)
+    M.deviation(Y)
+    t_mix = time.perf_counter() - t0
+    return 1.0 / (t_grad + t_mix), torch.get_num_threads(), t_grad, t_mix
+
+
+def run_c3(args, dev, rank, world):
+    """Config c3: MLP consensus SGD.  One step = batched per-agent gradients of ANNModel on a
+    synthetic MNIST-shaped batch (4 forward + xent + 7 backward fp32-MFMA batched GEMMs, weight
+    gradients written straight into G's rows) followed by the fused round X <- W (X - lr G) with
+    the disagreement, over a random 4-regular graph of 256 agents.  N>1: one independent
+    256-agent system per GPU (replicas)."""
+    from distributed_learning_amd import engine
+    from distributed_learning_amd.networks.batched_ann import BatchedANN
+    from distributed_learning_amd.workloads import MLPConsensusSGD
+    n, B, lr = 256, 64, 0.05
+    ann = BatchedANN(n, B, device=dev)
+    P = ann.P
+    csr, wconst = build_graph(n)
+    gen = torch.Generator(device=dev).manual_seed(rank)
+    X0 = c3_init_rows(ann, gen)
+    data = torch.randn(n, B, ann.din, device=dev, generator=gen)
+    labels = torch.randint(0, ann.dout, (n, B), device=dev, generator=gen, dtype=torch.int32)
+    eng = engine.GossipEngine(csr, P, device=dev, X=X0, layout="rows")
+    del X0
+    sgd = MLPConsensusSGD(ann, eng, data, labels, lr, deviation=True)
+    G = sgd.G
+    stream = torch.cuda.current_stream(dev)
+    # phase times: eager steps bracketed by HIP events (kernel time is the same under a graph)
+    n_ev = min(args.steps, 20)
+    evs = event_pairs(n_ev, 3)
+    for i in range(n_ev):
+        evs[i][0].record(stream)
+        ann.gradients(eng.X, data, labels, G)
+        evs[i][1].record(stream)
+        eng.round(G=G, lr=lr, deviation=True)
+        evs[i][2].record(stream)
+    torch.cuda.synchronize()
+    grad_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in evs]))
+    mix_ms = float(np.mean([b.elapsed_time(c) for _, b, c in evs]))
+    losses = [sgd.loss.mean()]
+    use_graph = not args.no_graph
+    if use_graph:
+        sgd.capture()
+
+    def step(i):
+        if use_graph:
+            sgd.replay(1)
+        else:
+            sgd.step()
+
+    elapsed = timed_loop(step, args, world, dev)
+    losses.append(sgd.loss.mean())
+    grad_ms = max_over_ranks(grad_ms, world, dev)
+    mix_ms = max_over_ranks(mix_ms, world, dev)
+    flops = ann.flops_per_step()
+    mix_bytes = 12 * n * P
+    tflops = flops / (grad_ms / 1e3) / 1e12
+    gbs = mix_bytes / (mix_ms / 1e3) / 1e9
+    if rank != 0:
+        return
+    grad_roof = {"bound": "mfma", "achieved": tflops, "peak": FP32_MFMA_PEAK_TFLOPS,
+                 "unit": "TFLOP/s", "frac": tflops / FP32_MFMA_PEAK_TFLOPS, "traffic": None,
+                 "kernel": "dl_bgemm x11 + dl_xent_grad (per-step HIP-event time)",
+                 "flops_per_launch": flops, "launch_ms": grad_ms}
+    mix_roof = {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": gbs / HBM_PEAK_GBS, "traffic": None,
+                "kernel": "mix_tile_kernel (+dev_reduce)", "bytes_per_launch": mix_bytes,
+                "launch_ms": mix_ms}
+    dominant = grad_roof if grad_ms >= mix_ms else mix_roof
+    cpu = None
+    if not args.no_cpu:
+        v, cores, tg, tm = c3_cpu_baseline(ann, csr, lr)
+        cpu = {"value": v, "unit": "steps/s", "cores": cores, "kind": "port",
+               "sample": f"torch CPU autograd step of ANNModel on 16 of {n} agents (B={B}), "
+                         f"scaled to {n}: {tg:.3f} s; numpy restatement of the mix + deviation "
+                         f"on all {n} x {P}: {tm:.3f} s",
+               "host_cores": os.cpu_count()}
+    rec = {
+        "metric": "c3 MLP consensus SGD steps/sec (256 agents x ANNModel 164,560 params)",
+        "value": world * args.steps / elapsed,
+        "unit": "steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": f"synthetic MNIST-shaped batches x ~ N(0,1) [{B}x784], labels uniform in 10 "
+                f"classes, one fixed batch per agent resident in HBM; random-init weights",
+        "config": {"workload": "c3: ANNModel consensus SGD (batched per-agent MFMA gradients + "
+                               "fused round + deviation)",
+                   "agents": n, "params": P, "batch": B, "lr": lr, "graph": "random 4-regular",
+                   "weights": f"best-constant {wconst:.6f}",
+                   "launch": "hipGraph replay per step" if use_graph else "eager",
+                   "parallelism": f"{world} independent replicas" if world > 1 else "single GPU"},
+        "roofline": dominant,
+        "phases": {"gradients": grad_roof, "round": mix_roof},
+        "cpu_baseline": cpu,
+        "mean_loss_first_last": [float(v.item()) for v in losses],
+    }
+    print(json.dumps(rec), flush=True)
+
+
+def run_c4(args, dev, rank, world):
+    """Config c4: 64x64 periodic torus, 4096 agents x 2^18 params, uniform best-constant weight
+    2/(lambda_2 + 8).  N=1: the whole torus resident in the tiled layout, one fused round
+    (local step + mix + deviation) per step.  N>1: 2-D torus blocks per rank (HaloShard), the
+    boundary rows of each column chunk exchanged with RCCL send/recv while the previous chunk is
+    mixed, deviation via an all-reduced column sum (strong scaling: total work fixed)."""
+    import math
+    from distributed_learning_amd import engine, graph, sharding
+    rows = cols = 64
+    n, P, lr = rows * cols, 1 << 18, 1e-3
+    edges = graph.torus_edges(rows, cols)
+    wconst = 2.0 / (2.0 - 2.0 * math.cos(2 * math.pi / cols) + 8.0)
+    csr = graph.from_edge_weights(edges, [wconst] * len(edges), list(range(n)))
+    gen = torch.Generator(device=dev).manual_seed(1000 + rank)
+    stream = torch.cuda.current_stream(dev)
+    evs = event_pairs(args.steps, 2)
+    halo_rows = 0
+    if world == 1:
+        X = torch.randn(n, P, device=dev, generator=gen)
+        eng = engine.GossipEngine(csr, P, device=dev, X=X)
+        G = eng.layout_like(torch.randn(n, P, device=dev, generator=gen))
+        del X
+        plan = eng.plan(deviation=True)
+
+        def step(i):
+            if i is not None:
+                evs[i][0].record(stream)
+            eng.round(G=G, lr=lr, deviation=True)
+            if i is not None:
+                evs[i][1].record(stream)
+        bytes_per_round = 12 * n * P
+    else:
+        parts = sharding.torus_block_partition(rows, cols, world)
+        rp = sharding.halo_plans(csr, parts)[rank]
+        shard = sharding.HaloShard(rp, P, dev, sharding.DistTransport(), chunk_cols=P // 8,
+                                   n_agents_total=n)
+        shard.X.normal_(generator=gen)
+        G = torch.randn(rp.n_local, P, device=dev, generator=gen)
+        halo_rows = rp.n_halo
+        plan = {"path": "halo", "n_local": rp.n_local, "n_halo": rp.n_halo,
+                "peers": sorted(rp.halo_from)}
+
+        def step(i):
+            if i is not None:
+                evs[i][0].record(stream)
+            shard.round(G=G, lr=lr)
+            shard.deviation()
+            if i is not None:
+                evs[i][1].record(stream)
+        bytes_per_round = 12 * rp.n_local * P
+    elapsed = timed_loop(step, args, world, dev)
+    launch_ms = max_over_ranks(float(np.mean([a.elapsed_time(b) for a, b in evs])), world, dev)
+    if rank != 0:
+        return
+    achieved = bytes_per_round / (launch_ms / 1e3) / 1e9
+    rec = {
+        "metric": "c4 torus consensus rounds/sec (4096 agents x 2^18 fp32 params)",
+        "value": args.steps / elapsed,
+        "unit": "rounds/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (X, G ~ N(0,1) resident in HBM)",
+        "config": {"workload": "c4: 64x64 torus, fused local step + mix + deviation",
+                   "agents": n, "params": P, "weights": f"best-constant {wconst:.6f}",
+                   "parallelism": f"2-D torus blocks x{world}, RCCL halo exchange"
+                   if world > 1 else "single GPU", "plan": plan,
+                   "halo_rows_rank0": halo_rows,
+                   "halo_bytes_per_round_rank0": halo_rows * P * 4},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "per-round HIP-event time (rank 0 local work)",
+                     "bytes_per_launch": bytes_per_round, "launch_ms": launch_ms},
+        "cpu_baseline": None,
+    }
+    print(json.dumps(rec), flush=True)
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -151,6 +424,12 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(args.dist_backend)
+
+    if args.workload in ("c3", "c4"):
+        (run_c3 if args.workload == "c3" else run_c4)(args, dev, rank, world)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     from distributed_learning_amd import engine
 

@@ -22,7 +22,8 @@ _i32, _i64, _f32, _f64, _sz = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ct
 
 class DlCsr(ctypes.Structure):
     _fields_ = [("row_ptr", _vp), ("col", _vp), ("w", _vp), ("n_rows", _i32), ("nnz", _i32),
-                ("uniform_row_nnz", _i32), ("doubly_stochastic", _i32)]
+                ("uniform_row_nnz", _i32), ("doubly_stochastic", _i32),
+                ("shared_row_weights", _i32)]
 
 
 class DlMixArgs(ctypes.Structure):
@@ -62,7 +63,8 @@ SIGNATURES = {
     "dl_last_error": (ctypes.c_char_p, []),
     "dl_mix_workspace_bytes": (_sz, [_i32, _i32, _i64]),
     "dl_mix_plan_query": (_i32, [ctypes.POINTER(DlMixArgs), ctypes.POINTER(DlMixPlan)]),
-    "dl_mix_plan_shape": (_i32, [_i32, _i32, _i64, _i32, _i32, _i32, ctypes.POINTER(DlMixPlan)]),
+    "dl_mix_plan_shape": (_i32, [_i32, _i32, _i64, _i32, _i32, _i32, _i32,
+                                 ctypes.POINTER(DlMixPlan)]),
     "dl_mix_round": (_i32, [ctypes.POINTER(DlMixArgs), _vp, _sz, _vp]),
     "dl_deviation_workspace_bytes": (_sz, [_i32, _i64]),
     "dl_deviation": (_i32, [_vp, _i64, _i32, _i64, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
@@ -79,7 +81,7 @@ SIGNATURES = {
     "dl_perron_round": (_i32, [ctypes.POINTER(DlPerronArgs), _vp, _sz, _vp]),
 }
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 _lib = None
 
 

@@ -286,7 +286,7 @@ hipError_t launch_perron_single(const PerronArgs &a, int dtype, int tile_cols, h
     const int lds = (int)(2 * (int64_t)a.n_rows * tile_cols * sz + 16);
     const void *k = dtype == 1 ? reinterpret_cast<const void *>(perron_single_kernel<double>)
                                : reinterpret_cast<const void *>(perron_single_kernel<float>);
-    hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    hipError_t e = allow_full_lds(k);
     if (e != hipSuccess) return e;
     if (dtype == 1)
         hipLaunchKernelGGL(perron_single_kernel<double>, dim3(1), dim3(1024), lds, s, a);
@@ -304,16 +304,14 @@ hipError_t launch_perron_step(const PerronArgs &a, int dtype, int tile_cols, con
     const int64_t ldout = yout == a.y ? a.ldy : a.n_params;
     if (dtype == 1) {
         auto k = perron_step_kernel<double>;
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        hipError_t e = allow_full_lds(reinterpret_cast<const void *>(k));
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(k, dim3(grid), dim3(1024), lds, s, a, tile_cols,
                            static_cast<const double *>(yin), ldin, static_cast<double *>(yout),
                            ldout, (int)do_prescale);
     } else {
         auto k = perron_step_kernel<float>;
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        hipError_t e = allow_full_lds(reinterpret_cast<const void *>(k));
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(k, dim3(grid), dim3(1024), lds, s, a, tile_cols,
                            static_cast<const float *>(yin), ldin, static_cast<float *>(yout),

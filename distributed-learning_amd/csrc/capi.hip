@@ -68,6 +68,13 @@ struct Plan {
     uint32_t csr_off, scratch_off;
 };
 
+// Workgroups per CU the tile kernel may use (LDS permitting): 2 unless DLAMD_WG_PER_CU=1
+// (a measurement knob).
+int wg_per_cu_cap() {
+    const char *v = getenv("DLAMD_WG_PER_CU");
+    return (v && v[0] == '1') ? 1 : 2;
+}
+
 int next_pow2_chunks(int64_t n_params) {
     int64_t need = (n_params + 3) / 4;
     int c = 1;
@@ -83,7 +90,8 @@ int plan_mix(const dl_mix_args *a, Plan *pl) {
     const bool want_dev = a->dev_sq || a->dev_max || a->mean;
     pl->dev = want_dev;
     const int reg = a->W.uniform_row_nnz > 0 ? 1 : 0;
-    const uint32_t csr = dl::csr_lds_bytes(a->W.n_rows, nnz, reg);
+    const int32_t n_w = (reg && a->W.shared_row_weights) ? a->W.uniform_row_nnz : nnz;
+    const uint32_t csr = dl::csr_lds_bytes(a->W.n_rows, nnz, reg, n_w);
     const int cmax = next_pow2_chunks(a->n_params);
     // DLAMD_FORCE_GATHER=1 (tests only) forces the general gather kernel
     const char *force = getenv("DLAMD_FORCE_GATHER");
@@ -99,7 +107,7 @@ int plan_mix(const dl_mix_args *a, Plan *pl) {
                                         "(%d rows); query dl_mix_plan_query on row-major args",
                         a->tile_cols, R);
         const int64_t n_tiles = (a->n_params + a->tile_cols - 1) / a->tile_cols;
-        int64_t grid = (int64_t)device_cus() * ((dl::kLdsBytes / lds) >= 2 ? 2 : 1);
+        int64_t grid = (int64_t)device_cus() * ((dl::kLdsBytes / lds) >= wg_per_cu_cap() ? wg_per_cu_cap() : 1);
         if (grid > n_tiles) grid = n_tiles;
         pl->pub.path = 1;
         pl->pub.tile_cols = a->tile_cols;
@@ -123,7 +131,7 @@ int plan_mix(const dl_mix_args *a, Plan *pl) {
             const int64_t n_tiles = (a->n_params + T - 1) / T;
             if (n_tiles > 0x7fffffff) continue;
             int bpc = (int)(dl::kLdsBytes / lds);
-            if (bpc > 2) bpc = 2;  // 1024-thread workgroups: at most 2 per CU (32 waves)
+            if (bpc > wg_per_cu_cap()) bpc = wg_per_cu_cap();  // 1024 threads: <= 2 per CU
             int64_t grid = (int64_t)device_cus() * bpc;
             if (grid > n_tiles) grid = n_tiles;
             pl->pub.path = 1;
@@ -172,6 +180,8 @@ int check_mix_args(const dl_mix_args *a) {
     if (W.uniform_row_nnz < 0 ||
         (W.uniform_row_nnz > 0 && (int64_t)W.uniform_row_nnz * W.n_rows != W.nnz))
         return fail(DL_ERR_INVALID, "dl_mix_round: uniform_row_nnz * n_rows != nnz");
+    if (W.shared_row_weights && W.uniform_row_nnz <= 0)
+        return fail(DL_ERR_INVALID, "dl_mix_round: shared_row_weights needs uniform_row_nnz > 0");
     if ((a->dev_sq || a->dev_max || a->mean) && a->n_halo > 0)
         return fail(DL_ERR_INVALID,
                     "dl_mix_round: fused deviation needs every agent local (n_halo == 0); use "
@@ -206,6 +216,8 @@ dl::TileArgs tile_args(const dl_mix_args *a) {
     t.n_src = a->W.n_rows + a->n_halo;
     t.nnz = a->W.nnz;
     t.regular = a->W.uniform_row_nnz;
+    t.n_w = (a->W.uniform_row_nnz > 0 && a->W.shared_row_weights) ? a->W.uniform_row_nnz
+                                                                   : a->W.nnz;
     t.mean_from_inputs = (a->W.doubly_stochastic && a->n_halo == 0) ? 1 : 0;
     {
         // X, G and X' are streamed exactly once per round: non-temporal loads and stores keep
@@ -306,7 +318,8 @@ int dl_mix_plan_query(const dl_mix_args *args, dl_mix_plan *plan) {
 }
 
 int dl_mix_plan_shape(int32_t n_rows, int32_t n_halo, int64_t n_params, int32_t nnz,
-                      int32_t uniform_row_nnz, int32_t deviation, dl_mix_plan *plan) {
+                      int32_t uniform_row_nnz, int32_t shared_row_weights, int32_t deviation,
+                      dl_mix_plan *plan) {
     g_err.clear();
     if (!plan || n_rows <= 0 || n_halo < 0 || n_params <= 0 || nnz < 0)
         return fail(DL_ERR_INVALID, "dl_mix_plan_shape: bad arguments");
@@ -314,6 +327,7 @@ int dl_mix_plan_shape(int32_t n_rows, int32_t n_halo, int64_t n_params, int32_t 
     a.W.n_rows = n_rows;
     a.W.nnz = nnz;
     a.W.uniform_row_nnz = uniform_row_nnz;
+    a.W.shared_row_weights = uniform_row_nnz > 0 ? shared_row_weights : 0;
     a.n_halo = n_halo;
     a.n_params = n_params;
     float dummy;

@@ -26,6 +26,7 @@ struct TileArgs {
     int32_t n_src;    // rows staged in LDS = n_rows + n_halo
     int32_t nnz;
     int32_t regular;  // >0: every row has exactly `regular` entries (row_ptr not staged)
+    int32_t n_w;      // weights staged in LDS: nnz, or `regular` when every row shares row 0's
     int32_t mean_from_inputs;  // 1: W doubly stochastic -> tile mean taken from the staged t
     int32_t nt_store;          // 1: non-temporal stores of y (FAST path)
     int32_t nt_load;           // 1: non-temporal loads of x, g (FAST path)
@@ -48,7 +49,13 @@ struct TileArgs {
 };
 
 // LDS bytes the staged CSR needs (0 if it cannot be staged: > 65535 rows/entries).
-uint32_t csr_lds_bytes(int32_t n_rows, int32_t nnz, int32_t regular);
+// Raise kernel k's dynamic-LDS limit to the whole CU (kLdsBytes), once per (kernel, device):
+// launches then make no attribute call, so they are capturable in a hipGraph and carry no
+// per-launch driver work.
+hipError_t allow_full_lds(const void *k);
+
+// n_w = weights staged (nnz, or the row degree when all rows share one weight sequence).
+uint32_t csr_lds_bytes(int32_t n_rows, int32_t nnz, int32_t regular, int32_t n_w);
 
 hipError_t launch_mix_tile(const TileArgs &a, int chunks, bool sgd, bool dev, bool mix, int grid,
                            int lds_bytes, bool fast, hipStream_t s);

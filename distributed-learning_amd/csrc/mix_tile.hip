@@ -14,6 +14,10 @@
 // the mix phase issues no vector-memory loads that would queue behind the prefetch (vmcnt is
 // in-order on CDNA).  Products and sums are separate fp32 ops in CSR order (-ffp-contract=off),
 // which reproduces the reference's left fold bit for bit.
+#include <mutex>
+#include <set>
+#include <utility>
+
 #include "dl_internal.h"
 
 namespace dl {
@@ -127,14 +131,14 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
     const int64_t P = a.n_params;
     const int nnz = a.nnz;
 
+    // staged CSR: n_w weights (all nnz, or one row's when every row shares them), u16 columns,
+    // u16 row_ptr unless the graph is regular
     float *lw = reinterpret_cast<float *>(smem + a.csr_off);
-    uint16_t *lcol = reinterpret_cast<uint16_t *>(smem + a.csr_off + 4u * (uint32_t)nnz);
+    uint16_t *lcol = reinterpret_cast<uint16_t *>(smem + a.csr_off + 4u * (uint32_t)a.n_w);
     uint16_t *lrp = lcol + nnz;
     if (MIX) {
-        for (int i = tid; i < nnz; i += NT) {
-            lw[i] = a.w[i];
-            lcol[i] = (uint16_t)a.col[i];
-        }
+        for (int i = tid; i < a.n_w; i += NT) lw[i] = a.w[i];
+        for (int i = tid; i < nnz; i += NT) lcol[i] = (uint16_t)a.col[i];
         if (!a.regular)
             for (int i = tid; i <= Nr; i += NT) lrp[i] = (uint16_t)a.rowptr[i];
     }
@@ -223,6 +227,7 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
 
     // y_a = sum_e w_e * t_{col_e} for agent ag, chunk c: left fold in CSR order from +0.0
     // (mixer.py:47); reads only LDS.
+    const bool wshared = a.n_w != nnz;  // weight of entry e is lw[e - e0]
     auto mix_row = [&](int ag) {
         int e0, e1;
         if (reg) {
@@ -232,8 +237,9 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
             e0 = lrp[ag];
             e1 = lrp[ag + 1];
         }
+        const float *wr = wshared ? lw - e0 : lw;
         float4 acc = zero4();
-        for (int e = e0; e < e1; ++e) axpy4(acc, lw[e], tile[lcol[e] * C + c]);
+        for (int e = e0; e < e1; ++e) axpy4(acc, wr[e], tile[lcol[e] * C + c]);
         return acc;
     };
 
@@ -456,8 +462,7 @@ __global__ void __launch_bounds__(256) stream_copy_kernel(const float4 *__restri
 template <int C, int KV, bool SGD, bool DEV, bool MIX, bool HALO, bool FAST>
 hipError_t launch_one(const TileArgs &a, int grid, int lds, hipStream_t s) {
     auto k = mix_tile_kernel<C, KV, SGD, DEV, MIX, HALO, FAST>;
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    hipError_t e = allow_full_lds(reinterpret_cast<const void *>(k));
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k, dim3(grid), dim3(kTileThreads), lds, s, a);
     return hipGetLastError();
@@ -519,9 +524,22 @@ hipError_t launch_mix_tile(const TileArgs &a, int chunks, bool sgd, bool dev, bo
     }
 }
 
-uint32_t csr_lds_bytes(int32_t n_rows, int32_t nnz, int32_t regular) {
+hipError_t allow_full_lds(const void *k) {
+    static std::mutex mu;
+    static std::set<std::pair<const void *, int>> done;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    std::lock_guard<std::mutex> lock(mu);
+    if (done.count({k, dev})) return hipSuccess;
+    e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+    if (e == hipSuccess) done.insert({k, dev});
+    return e;
+}
+
+uint32_t csr_lds_bytes(int32_t n_rows, int32_t nnz, int32_t regular, int32_t n_w) {
     if (nnz > 65535 || n_rows > 65535) return 0;
-    uint32_t b = 4u * (uint32_t)nnz + 2u * (uint32_t)nnz;
+    uint32_t b = 4u * (uint32_t)n_w + 2u * (uint32_t)nnz;
     if (!regular) b += 2u * (uint32_t)(n_rows + 1);
     return (b + 15u) & ~15u;
 }

@@ -31,10 +31,12 @@ class DeviceCsr:
         self.nnz = csr.nnz
         self.uniform_row_nnz = csr.uniform_row_nnz
         self.doubly_stochastic = int(csr.doubly_stochastic)
+        self.shared_row_weights = int(csr.shared_row_weights)
 
     def c_struct(self):
         return _lib.DlCsr(_lib.ptr(self.rowptr), _lib.ptr(self.col), _lib.ptr(self.w),
-                          self.n_rows, self.nnz, self.uniform_row_nnz, self.doubly_stochastic)
+                          self.n_rows, self.nnz, self.uniform_row_nnz, self.doubly_stochastic,
+                          self.shared_row_weights)
 
 
 def _ld(t):
@@ -57,7 +59,8 @@ def plan_shape(W: DeviceCsr, n_params, deviation=True):
     lib = _lib.load()
     plan = _lib.DlMixPlan()
     _lib.check(lib.dl_mix_plan_shape(W.n_rows, W.n_src - W.n_rows, int(n_params), W.nnz,
-                                     W.uniform_row_nnz, int(bool(deviation)), ctypes.byref(plan)),
+                                     W.uniform_row_nnz, W.shared_row_weights,
+                                     int(bool(deviation)), ctypes.byref(plan)),
                "dl_mix_plan_shape")
     return {f: getattr(plan, f) for f, _ in plan._fields_}
 
@@ -268,7 +271,7 @@ class GossipEngine:
     Row-major data goes in and out through ``load_rows`` / ``rows`` / ``layout_like``.
     """
 
-    def __init__(self, csr: Csr, n_params, device="cuda", X=None, layout="auto"):
+    def __init__(self, csr: Csr, n_params, device="cuda", X=None, layout="auto", tile_cols=None):
         self.device = torch.device(device)
         if self.device.type == "cuda" and self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
@@ -281,7 +284,7 @@ class GossipEngine:
         if layout == "tiled" and not tiled_ok:
             raise ValueError("this graph does not fit the LDS tile kernel; use layout='rows'")
         self.layout = layout
-        self.T = plan["tile_cols"] if layout == "tiled" else 0
+        self.T = (int(tile_cols) if tile_cols else plan["tile_cols"]) if layout == "tiled" else 0
         self.dev_sq = torch.zeros(self.n, dtype=torch.float32, device=self.device)
         self.dev_max = torch.zeros(1, dtype=torch.float32, device=self.device)
         self.ws = Workspace(self.device)
@@ -309,6 +312,12 @@ class GossipEngine:
     def rows(self):
         """The agent matrix as a row-major [N, P] tensor (a conversion in the tiled layout)."""
         return from_tiled(self.X, self.P) if self.layout == "tiled" else self.X
+
+    def reserve_workspace(self, deviation=True):
+        """Allocate the round's scratch now (so a hipGraph capture allocates nothing)."""
+        if deviation:
+            lib = _lib.load()
+            self.ws.get(lib.dl_mix_workspace_bytes(self.n, self.W.n_src - self.n, self.P))
 
     def round(self, G=None, lr=0.0, deviation=False, mean=None, halo=None):
         """G must already be in the resident layout (``layout_like``)."""

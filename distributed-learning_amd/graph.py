@@ -53,6 +53,15 @@ class Csr:
         return int(d[0]) if len(d) and d[0] > 0 and np.all(d == d[0]) else 0
 
     @property
+    def shared_row_weights(self):
+        """Regular graph whose rows all carry row 0's fp32 weight sequence (bit for bit)."""
+        d = self.uniform_row_nnz
+        if d == 0:
+            return False
+        w32 = self.w.astype(np.float32).view(np.uint32).reshape(-1, d)
+        return bool(np.all(w32 == w32[0]))
+
+    @property
     def doubly_stochastic(self):
         """Every row and column of W sums to 1 (fp32 weights, 1e-6): mean(W x) = mean(x)."""
         if self.n_src != self.n_rows or self.n_rows == 0:

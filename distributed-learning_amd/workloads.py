@@ -58,3 +58,58 @@ def accuracy(w, X, y):
     m = LogRegTitanic(X.shape[1])
     m.W = w
     return m.calc_accuracy(X, y)
+
+
+class MLPConsensusSGD:
+    """Config c3 (BASELINE.json): every agent trains its own ``ANNModel`` (networks/ann_model.py)
+    on its own batch and the agents mix after every local step -- the training loop of the
+    reference's consensus notebooks (Man_Colab.ipynb cells 12-23: local SGD step, then
+    ``Mixer.mix``), with all agents resident in HBM.
+
+    One ``step()`` = batched per-agent gradients (``BatchedANN.gradients`` -> G rows) followed by
+    the fused round X <- W (X - lr G) and the disagreement (``GossipEngine.round``).  Every call
+    is stream-ordered with no host synchronisation, so ``capture()`` can record a step as a
+    hipGraph (two graphs: the engine ping-pongs X/Y) and ``replay()`` then runs steps with one
+    graph launch each instead of ~15 kernel launches from Python."""
+
+    def __init__(self, ann, eng, data, labels, lr, deviation=True):
+        if eng.layout != "rows":
+            raise ValueError("the batched gradients read X row-major: use GossipEngine(layout='rows')")
+        if eng.n != ann.N or eng.P != ann.P:
+            raise ValueError("engine and model disagree on agents/params")
+        import torch
+        self.ann, self.eng = ann, eng
+        self.data, self.labels = data, labels
+        self.lr, self.deviation = float(lr), bool(deviation)
+        self.G = torch.empty(ann.N, ann.P, dtype=torch.float32, device=eng.device)
+        self.graphs = None
+        self._torch = torch
+
+    @property
+    def loss(self):
+        """Per-agent mean cross-entropy of the last step (device tensor [N])."""
+        return self.ann.loss
+
+    def step(self):
+        self.ann.gradients(self.eng.X, self.data, self.labels, self.G)
+        self.eng.round(G=self.G, lr=self.lr, deviation=self.deviation)
+
+    def capture(self):
+        """Record one step per ping-pong parity.  Runs nothing: the engine state afterwards is
+        what it was before."""
+        torch = self._torch
+        self.eng.reserve_workspace(self.deviation)
+        graphs = []
+        for _ in range(2):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self.step()               # records; swaps eng.X / eng.Y on the host
+            graphs.append(g)
+        self.graphs = graphs              # two swaps: eng.X is the original buffer again
+        self._parity = 0
+
+    def replay(self, steps=1):
+        for _ in range(int(steps)):
+            self.graphs[self._parity].replay()
+            self._parity ^= 1
+            self.eng.X, self.eng.Y = self.eng.Y, self.eng.X

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define DLAMD_ABI_VERSION 1
+#define DLAMD_ABI_VERSION 2
 
 typedef void *dl_stream_t; /* hipStream_t; NULL = the legacy default stream */
 
@@ -63,6 +63,12 @@ typedef struct dl_csr {
                                   reference's mixing matrices), so mean(W t) = mean(t): the fused
                                   deviation then takes the column mean from the staged inputs and
                                   needs one LDS pass instead of two.  0 = general W. */
+    int32_t shared_row_weights; /* 1 promises (with uniform_row_nnz > 0) that every row's weight
+                                   sequence equals row 0's, w[a*d + k] == w[k] bit for bit (a
+                                   uniform edge weight: best-constant or analytic FA weights on a
+                                   regular graph).  The LDS kernel then stages d weights instead
+                                   of nnz, which fits ~2x more agents per tile.  w is still the
+                                   full [nnz] array.  0 = per-entry weights. */
 } dl_csr;
 
 typedef struct dl_mix_args {
@@ -105,7 +111,8 @@ size_t dl_mix_workspace_bytes(int32_t n_rows, int32_t n_halo, int64_t n_params);
  * these sizes, with (sgd) / without a local step and with (deviation) / without the fused
  * deviation.  plan->tile_cols is the width the column-tiled layout must use. */
 int dl_mix_plan_shape(int32_t n_rows, int32_t n_halo, int64_t n_params, int32_t nnz,
-                      int32_t uniform_row_nnz, int32_t deviation, dl_mix_plan *plan);
+                      int32_t uniform_row_nnz, int32_t shared_row_weights, int32_t deviation,
+                      dl_mix_plan *plan);
 int dl_mix_plan_query(const dl_mix_args *args, dl_mix_plan *plan);
 int dl_mix_round(const dl_mix_args *args, void *workspace, size_t ws_bytes, dl_stream_t stream);
 

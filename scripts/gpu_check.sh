@@ -24,6 +24,10 @@ fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
     step bench 600 python bench.py --steps 50 --warmup 5
 fi
+if [ "$MODE" = all ] || [ "$MODE" = workloads ]; then
+    step bench_c3 600 python bench.py --workload c3 --steps 50 --warmup 5
+    step bench_c4 600 python bench.py --workload c4 --steps 20 --warmup 3
+fi
 if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
     step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python bench.py --steps 20 --warmup 3 --no-cpu
 fi

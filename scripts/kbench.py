@@ -32,6 +32,57 @@ def main():
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     print(json.dumps({"copy_ceiling_GBs": bench.copy_ceiling(dev)}), flush=True)
+    if args.cases == "tile2":
+        # repeated sweep: tile width x shared weights x workgroups per CU
+        for n, P, Ts in [(1024, 1 << 20, (8, 16, 32)), (512, 1 << 21, (16, 32)),
+                         (2048, 1 << 19, (4, 8)), (256, 1 << 22, (32, 64))]:
+            edges = random_regular_edges(4, n, seed=0)
+            csr = from_edge_weights(edges, [0.2] * len(edges), list(range(n)))
+            X = torch.randn(n, P, device=dev)
+            G = torch.randn(n, P, device=dev)
+            for T in Ts:
+                for shared in (1, 0):
+                    eng = engine.GossipEngine(csr, P, device=dev, X=X, layout="tiled",
+                                              tile_cols=T)
+                    eng.W.shared_row_weights = shared
+                    Gl = eng.layout_like(G)
+                    for wg in ("2", "1"):
+                        os.environ["DLAMD_WG_PER_CU"] = wg
+                        ms = sorted(time_it(lambda: eng.round(G=Gl, lr=1e-3, deviation=True),
+                                            args.reps) for _ in range(3))
+                        print(json.dumps({"n": n, "T": T, "shared": shared, "wg": wg,
+                                          "ms": ms[1], "GBs": 12 * n * P / ms[1] / 1e6,
+                                          "spread": [ms[0], ms[2]]}), flush=True)
+                    os.environ.pop("DLAMD_WG_PER_CU")
+                    del eng, Gl
+            del X, G
+        return
+    if args.cases == "tile":
+        # tile width x shared-weight sweep (tiled layout, SGD + deviation, the bench round)
+        for n, P, Ts in [(1024, 1 << 20, (4, 8, 16, 32)), (512, 1 << 21, (8, 16, 32, 64)),
+                         (4096, 1 << 18, (4,))]:
+            edges = random_regular_edges(4, n, seed=0)
+            csr = from_edge_weights(edges, [0.2] * len(edges), list(range(n)))
+            X = torch.randn(n, P, device=dev)
+            G = torch.randn(n, P, device=dev)
+            for T in Ts:
+                for shared in (1, 0):
+                    try:
+                        eng = engine.GossipEngine(csr, P, device=dev, X=X, layout="tiled",
+                                                  tile_cols=T)
+                        eng.W.shared_row_weights = shared
+                        Gl = eng.layout_like(G)
+                        ms = time_it(lambda: eng.round(G=Gl, lr=1e-3, deviation=True), args.reps)
+                    except ValueError as ex:
+                        print(json.dumps({"n": n, "T": T, "shared": shared, "error": str(ex)}))
+                        continue
+                    lds = engine.plan_shape(eng.W, P)  # row-major plan, for reference
+                    print(json.dumps({"n": n, "P": P, "T": T, "shared": shared, "ms": ms,
+                                      "GBs": 12 * n * P / ms / 1e6,
+                                      "auto_plan_T": lds["tile_cols"]}), flush=True)
+                    del eng, Gl
+            del X, G
+        return
     if args.cases == "nt":
         edges = random_regular_edges(4, 1024, seed=0)
         csr = from_edge_weights(edges, [0.2] * len(edges), list(range(1024)))

@@ -5,6 +5,7 @@ import os
 import re
 import subprocess
 
+import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -63,3 +64,34 @@ def test_invalid_arguments_are_reported_not_crashed():
     assert rc == _lib.DL_ERR_INVALID
     rc = lib.dl_step_rows(None, 0, None, 0, 0.0, None, -1, 0, None, 0, None)
     assert rc == _lib.DL_ERR_INVALID
+
+
+def test_shared_row_weights_flag_and_plan():
+    """A uniform-weight regular graph (the c4 torus) sets shared_row_weights; the planner then
+    stages one row's weights and the 4096-agent torus fits the LDS tile kernel; the flag without
+    a regular graph is rejected before any device call."""
+    import math
+    from distributed_learning_amd import _lib, graph
+    e = graph.torus_edges(64, 64)
+    w = 2.0 / (2.0 - 2.0 * math.cos(2 * math.pi / 64) + 8.0)
+    csr = graph.from_edge_weights(e, [w] * len(e), list(range(4096)))
+    assert csr.uniform_row_nnz == 5 and csr.shared_row_weights and csr.doubly_stochastic
+    bumpy = graph.Csr(csr.rowptr, csr.col, csr.w.copy())
+    bumpy.w[7] = np.nextafter(np.float32(bumpy.w[7]), np.float32(1))
+    assert not bumpy.shared_row_weights
+    lib = _lib.load()
+    plans = []
+    for shared in (0, 1):
+        pl = _lib.DlMixPlan()
+        _lib.check(lib.dl_mix_plan_shape(4096, 0, 1 << 18, csr.nnz, 5, shared, 1,
+                                         ctypes.byref(pl)), "plan")
+        plans.append((pl.path, pl.tile_cols, pl.lds_bytes))
+    assert plans[0][0] == 2                      # per-entry weights: gather path
+    assert plans[1][:2] == (1, 4) and plans[1][2] <= 160 * 1024
+    args = _lib.DlMixArgs()
+    args.x = args.y = 16
+    args.n_params = 8
+    args.ldx = args.ldy = 8
+    args.W = _lib.DlCsr(16, 16, 16, 4, 10, 0, 0, 1)   # shared weights on an irregular CSR
+    rc = lib.dl_mix_round(ctypes.byref(args), None, 0, None)
+    assert rc == _lib.DL_ERR_INVALID and b"shared_row_weights" in lib.dl_last_error()

@@ -69,3 +69,40 @@ def test_consensus_sgd_round_with_batched_grads(cuda):
     want = cref.mix_round(X.cpu().numpy(), csr.rowptr, csr.col, csr.w,
                           G=torch.stack(grads).cpu().numpy(), lr=0.1)
     np.testing.assert_allclose(eng.rows().cpu().numpy(), want, rtol=1e-5, atol=1e-6)
+
+
+def test_mlp_consensus_graph_replay_matches_eager(cuda):
+    """c3 steps recorded as hipGraphs (two ping-pong graphs) give the same bits as eager steps,
+    for an odd and an even number of steps."""
+    from distributed_learning_amd import engine
+    from distributed_learning_amd.graph import from_edge_weights, random_regular_edges
+    from distributed_learning_amd.networks.batched_ann import BatchedANN
+    from distributed_learning_amd.workloads import MLPConsensusSGD
+    n, b = 16, 32
+    gen = torch.Generator(device=cuda).manual_seed(5)
+    bann = BatchedANN(n, b, 64, 32, 10, device=cuda)
+    X0 = 0.1 * torch.randn(n, bann.P, device=cuda, generator=gen)
+    data = torch.randn(n, b, 64, device=cuda, generator=gen)
+    labels = torch.randint(0, 10, (n, b), device=cuda, generator=gen, dtype=torch.int32)
+    edges = random_regular_edges(4, n, seed=0)
+    csr = from_edge_weights(edges, [0.2] * len(edges), list(range(n)))
+    runs = {}
+    for mode in ("eager", "graph"):
+        eng = engine.GossipEngine(csr, bann.P, device=cuda, X=X0, layout="rows")
+        sgd = MLPConsensusSGD(bann, eng, data, labels, lr=0.1)
+        out = []
+        if mode == "graph":
+            sgd.capture()
+            assert torch.equal(eng.X, X0)          # capture ran nothing
+        for k in (3, 2):
+            if mode == "graph":
+                sgd.replay(k)
+            else:
+                for _ in range(k):
+                    sgd.step()
+            torch.cuda.synchronize()
+            out.append((eng.X.clone(), eng.dev_sq.clone(), sgd.loss.clone()))
+        runs[mode] = out
+    for (xe, de, le), (xg, dg, lg) in zip(runs["eager"], runs["graph"]):
+        assert torch.equal(xe, xg) and torch.equal(de, dg) and torch.equal(le, lg)
+    assert not torch.equal(runs["eager"][0][0], X0)

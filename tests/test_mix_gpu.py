@@ -291,3 +291,35 @@ def test_doubly_stochastic_mean_from_inputs(cuda, layout):
         check_dev(want, eng.dev_sq.cpu().numpy(), float(eng.dev_max.item()), mean.cpu().numpy())
         out[ds] = eng.dev_sq.cpu().numpy()
     np.testing.assert_allclose(out[1], out[0], rtol=1e-5)
+
+
+@pytest.mark.parametrize("layout", ["tiled", "rows"])
+def test_torus_4096_shared_weights_bit_exact(cuda, layout):
+    """The c4 graph (64x64 torus, uniform best-constant weights, 4096 agents): the shared-weight
+    LDS tile path is bit-identical to the oracle and to the per-entry-weight path (which at this
+    size is the gather kernel)."""
+    import math
+    from distributed_learning_amd.graph import from_edge_weights, torus_edges
+    E = eng_mod()
+    n, P = 4096, 1024 + 20
+    e = torus_edges(64, 64)
+    w = 2.0 / (2.0 - 2.0 * math.cos(2 * math.pi / 64) + 8.0)
+    csr = from_edge_weights(e, [w] * len(e), list(range(n)))
+    rng = np.random.default_rng(64)
+    X = rng.standard_normal((n, P), dtype=np.float32)
+    G = rng.standard_normal((n, P), dtype=np.float32)
+    want = cref.mix_round(X, csr.rowptr, csr.col, csr.w, G=G, lr=0.01)
+    eng = E.GossipEngine(csr, P, device=cuda, X=torch.from_numpy(X).to(cuda), layout=layout)
+    assert eng.plan()["path"] == 1
+    mean = torch.empty(P, device=cuda)
+    eng.round(G=eng.layout_like(torch.from_numpy(G).to(cuda)), lr=0.01, deviation=True, mean=mean)
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(eng.rows().cpu().numpy()), bits(want))
+    check_dev(want, eng.dev_sq.cpu().numpy(), float(eng.dev_max.item()), mean.cpu().numpy())
+    # the same graph with per-entry weights (no shared flag) -> gather path, same bits
+    W = E.DeviceCsr(csr, cuda)
+    W.shared_row_weights = 0
+    Y = torch.empty(n, P, device=cuda)
+    E.mix_round(W, torch.from_numpy(X).to(cuda), Y, G=torch.from_numpy(G).to(cuda), lr=0.01)
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(Y.cpu().numpy()), bits(want))

@@ -241,7 +241,9 @@ def run_c3(args, dev, rank, world):
     X0 = c3_init_rows(ann, gen)
     data = torch.randn(n, B, ann.din, device=dev, generator=gen)
     labels = torch.randint(0, ann.dout, (n, B), device=dev, generator=gen, dtype=torch.int32)
-    eng = engine.GossipEngine(csr, P, device=dev, X=X0, layout="rows")
+    P_pad = MLPConsensusSGD.padded_params(csr, P, dev)   # zero columns: no ragged tail tile
+    X0 = torch.nn.functional.pad(X0, (0, P_pad - P))
+    eng = engine.GossipEngine(csr, P_pad, device=dev, X=X0, layout="rows")
     del X0
     sgd = MLPConsensusSGD(ann, eng, data, labels, lr, deviation=True)
     G = sgd.G
@@ -251,7 +253,7 @@ def run_c3(args, dev, rank, world):
     evs = event_pairs(n_ev, 3)
     for i in range(n_ev):
         evs[i][0].record(stream)
-        ann.gradients(eng.X, data, labels, G)
+        ann.gradients(eng.X[:, :P], data, labels, G[:, :P])
         evs[i][1].record(stream)
         eng.round(G=G, lr=lr, deviation=True)
         evs[i][2].record(stream)
@@ -274,7 +276,7 @@ def run_c3(args, dev, rank, world):
     grad_ms = max_over_ranks(grad_ms, world, dev)
     mix_ms = max_over_ranks(mix_ms, world, dev)
     flops = ann.flops_per_step()
-    mix_bytes = 12 * n * P
+    mix_bytes = 12 * n * P       # algorithmic: the real columns only (padding is overhead)
     tflops = flops / (grad_ms / 1e3) / 1e12
     gbs = mix_bytes / (mix_ms / 1e3) / 1e9
     if rank != 0:
@@ -312,7 +314,8 @@ def run_c3(args, dev, rank, world):
                 f"classes, one fixed batch per agent resident in HBM; random-init weights",
         "config": {"workload": "c3: ANNModel consensus SGD (batched per-agent MFMA gradients + "
                                "fused round + deviation)",
-                   "agents": n, "params": P, "batch": B, "lr": lr, "graph": "random 4-regular",
+                   "agents": n, "params": P, "params_padded": P_pad, "batch": B, "lr": lr,
+                   "graph": "random 4-regular",
                    "weights": f"best-constant {wconst:.6f}",
                    "launch": "hipGraph replay per step" if use_graph else "eager",
                    "parallelism": f"{world} independent replicas" if world > 1 else "single GPU"},

@@ -51,11 +51,12 @@ class DlBgemmArgs(ctypes.Structure):
                 ("B", _vp), ("ldb", _i64), ("sB", _i64), ("tb", _i32),
                 ("C", _vp), ("ldc", _i64), ("sC", _i64), ("epi", _i32),
                 ("bias", _vp), ("s_bias", _i64), ("H", _vp), ("ldh", _i64), ("sH", _i64),
-                ("rowsum", _vp), ("s_rowsum", _i64)]
+                ("rowsum", _vp), ("s_rowsum", _i64),
+                ("labels", _vp), ("s_labels", _i64), ("loss", _vp)]
 
 
 EPI = {"none": 0, "bias": 1, "bias_relu": 2, "bias_tanh": 3, "bias_elu": 4, "drelu": 5,
-       "dtanh": 6, "delu": 7}
+       "dtanh": 6, "delu": 7, "bias_xent": 8}
 
 # exported symbol -> (restype, argtypes); tests check every one is exported
 SIGNATURES = {
@@ -63,7 +64,7 @@ SIGNATURES = {
     "dl_last_error": (ctypes.c_char_p, []),
     "dl_mix_workspace_bytes": (_sz, [_i32, _i32, _i64]),
     "dl_mix_plan_query": (_i32, [ctypes.POINTER(DlMixArgs), ctypes.POINTER(DlMixPlan)]),
-    "dl_mix_plan_shape": (_i32, [_i32, _i32, _i64, _i32, _i32, _i32, _i32,
+    "dl_mix_plan_shape": (_i32, [_i32, _i32, _i64, _i32, _i32, _i32, _i32, _i32,
                                  ctypes.POINTER(DlMixPlan)]),
     "dl_mix_round": (_i32, [ctypes.POINTER(DlMixArgs), _vp, _sz, _vp]),
     "dl_deviation_workspace_bytes": (_sz, [_i32, _i64]),

@@ -82,6 +82,22 @@ int next_pow2_chunks(int64_t n_params) {
     return c;
 }
 
+// Tile width (float4 chunks) for the column-tiled layout: the widest power of two whose tile
+// of all R rows is <= 64 KiB and fits LDS beside the CSR.  Measured on MI355X:
+// 64-KiB tiles stream at 5.7-5.85 TB/s for N = 256..1024, 128-KiB tiles at 5.0-5.6 TB/s
+// depending on the box.  0 = no tiled configuration fits.
+int choose_tiled_chunks(int32_t R, uint32_t csr, bool want_dev) {
+    if (csr == 0 || R > 65535) return 0;
+    for (int c = dl::kMaxChunks; c >= 1; c >>= 1) {
+        if ((int64_t)R * c > (int64_t)dl::kRowsPerThread * dl::kTileThreads) continue;
+        const int64_t tile = (int64_t)R * c * 16;
+        if (tile > 65536 && c > 1) continue;
+        const int64_t scratch = want_dev ? (int64_t)(dl::kTileThreads / 64) * c * 16 : 0;
+        if (tile + csr + scratch <= dl::kLdsBytes) return c;
+    }
+    return 0;
+}
+
 // Pick the kernel configuration for a mix round.
 int plan_mix(const dl_mix_args *a, Plan *pl) {
     std::memset(pl, 0, sizeof *pl);
@@ -107,7 +123,13 @@ int plan_mix(const dl_mix_args *a, Plan *pl) {
                                         "(%d rows); query dl_mix_plan_query on row-major args",
                         a->tile_cols, R);
         const int64_t n_tiles = (a->n_params + a->tile_cols - 1) / a->tile_cols;
-        int64_t grid = (int64_t)device_cus() * ((dl::kLdsBytes / lds) >= wg_per_cu_cap() ? wg_per_cu_cap() : 1);
+        // two 1024-thread workgroups per CU when LDS allows, except at C = 4, where the second
+        // workgroup's LDS traffic (4 rows of 64 B per 16 lanes: the most bank conflicts of any
+        // C) costs more than its extra loads in flight (measured 5.5 vs 5.8 TB/s at N = 1024)
+        int bpc = (int)(dl::kLdsBytes / lds);
+        if (bpc > wg_per_cu_cap()) bpc = wg_per_cu_cap();
+        if (c == 4) bpc = 1;
+        int64_t grid = (int64_t)device_cus() * (bpc < 1 ? 1 : bpc);
         if (grid > n_tiles) grid = n_tiles;
         pl->pub.path = 1;
         pl->pub.tile_cols = a->tile_cols;
@@ -319,9 +341,9 @@ int dl_mix_plan_query(const dl_mix_args *args, dl_mix_plan *plan) {
 
 int dl_mix_plan_shape(int32_t n_rows, int32_t n_halo, int64_t n_params, int32_t nnz,
                       int32_t uniform_row_nnz, int32_t shared_row_weights, int32_t deviation,
-                      dl_mix_plan *plan) {
+                      int32_t tile_cols, dl_mix_plan *plan) {
     g_err.clear();
-    if (!plan || n_rows <= 0 || n_halo < 0 || n_params <= 0 || nnz < 0)
+    if (!plan || n_rows <= 0 || n_halo < 0 || n_params <= 0 || nnz < 0 || tile_cols < -1)
         return fail(DL_ERR_INVALID, "dl_mix_plan_shape: bad arguments");
     dl_mix_args a{};
     a.W.n_rows = n_rows;
@@ -332,6 +354,20 @@ int dl_mix_plan_shape(int32_t n_rows, int32_t n_halo, int64_t n_params, int32_t 
     a.n_params = n_params;
     float dummy;
     if (deviation) a.dev_max = &dummy;
+    if (tile_cols == -1) {  // pick the column-tiled width (no halo rows in that layout)
+        const int reg = uniform_row_nnz > 0 ? 1 : 0;
+        const int32_t n_w = (reg && a.W.shared_row_weights) ? uniform_row_nnz : nnz;
+        const int c = n_halo == 0 ? choose_tiled_chunks(n_rows, dl::csr_lds_bytes(
+                                                                    n_rows, nnz, reg, n_w),
+                                                        deviation != 0)
+                                  : 0;
+        if (c == 0) {  // not tileable: report the row-major plan
+            tile_cols = 0;
+        } else {
+            tile_cols = 4 * c;
+        }
+    }
+    a.tile_cols = tile_cols;
     Plan pl;
     int rc = plan_mix(&a, &pl);
     if (rc) return rc;
@@ -609,13 +645,16 @@ int dl_stream_copy(const float *src, float *dst, int64_t n_floats, int32_t varia
 int dl_bgemm(const dl_bgemm_args *a, dl_stream_t stream) {
     g_err.clear();
     if (!a || a->batch <= 0 || a->M <= 0 || a->N <= 0 || a->K <= 0 || !a->A || !a->B || !a->C ||
-        a->batch > 65535 || a->epi < DL_EPI_NONE || a->epi > DL_EPI_DELU)
+        a->batch > 65535 || a->epi < DL_EPI_NONE || a->epi > DL_EPI_BIAS_XENT)
         return fail(DL_ERR_INVALID, "dl_bgemm: bad sizes/pointers/epilogue");
     if ((a->ta ? a->lda < a->M : a->lda < a->K) || (a->tb ? a->ldb < a->K : a->ldb < a->N) ||
         a->ldc < a->N)
         return fail(DL_ERR_INVALID, "dl_bgemm: leading dimension too small");
-    if (a->epi >= DL_EPI_DRELU && (!a->H || a->ldh < a->N))
+    if (a->epi >= DL_EPI_DRELU && a->epi <= DL_EPI_DELU && (!a->H || a->ldh < a->N))
         return fail(DL_ERR_INVALID, "dl_bgemm: derivative epilogue needs H with ldh >= N");
+    if (a->epi == DL_EPI_BIAS_XENT && (a->M > 64 || a->N > 64 || !a->labels))
+        return fail(DL_ERR_INVALID, "dl_bgemm: cross-entropy epilogue needs M <= 64 rows, "
+                                    "N <= 64 classes and labels");
     dl::BgemmArgs p{};
     p.batch = a->batch; p.M = a->M; p.N = a->N; p.K = a->K;
     p.A = a->A; p.lda = a->lda; p.sA = a->sA; p.ta = a->ta;
@@ -624,6 +663,7 @@ int dl_bgemm(const dl_bgemm_args *a, dl_stream_t stream) {
     p.epi = a->epi; p.bias = a->bias; p.sBias = a->s_bias;
     p.H = a->H; p.ldh = a->ldh; p.sH = a->sH;
     p.rowsum = a->rowsum; p.sR = a->s_rowsum;
+    p.labels = a->labels; p.sLab = a->s_labels; p.loss = a->loss;
     hipError_t e = dl::launch_bgemm(p, static_cast<hipStream_t>(stream));
     return e == hipSuccess ? DL_OK : hip_fail(e, "bgemm launch");
 }

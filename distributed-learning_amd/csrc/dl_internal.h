@@ -107,7 +107,8 @@ enum Epi {
     EPI_BIAS_ELU = 4,
     EPI_DRELU = 5,
     EPI_DTANH = 6,
-    EPI_DELU = 7
+    EPI_DELU = 7,
+    EPI_BIAS_XENT = 8
 };
 
 struct BgemmArgs {
@@ -127,6 +128,9 @@ struct BgemmArgs {
     int64_t ldh, sH;
     float *rowsum;
     int64_t sR;
+    const int32_t *labels;
+    int64_t sLab;
+    float *loss;
 };
 hipError_t launch_bgemm(const BgemmArgs &p, hipStream_t s);
 hipError_t launch_xent_grad(const float *Z, int64_t sZ, const int32_t *y, int64_t sY, float *dZ,

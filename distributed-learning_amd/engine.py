@@ -54,13 +54,14 @@ def _check(t, name, rows, cols, device):
         raise ValueError(f"{name} has shape {tuple(t.shape)}, expected ({rows}, {cols})")
 
 
-def plan_shape(W: DeviceCsr, n_params, deviation=True):
-    """dl_mix_plan_shape: the kernel configuration for these sizes (no tensors needed)."""
+def plan_shape(W: DeviceCsr, n_params, deviation=True, tile_cols=0):
+    """dl_mix_plan_shape: the kernel configuration for these sizes (no tensors needed).
+    tile_cols: 0 row-major, > 0 column-tiled of that width, -1 choose the tiled width."""
     lib = _lib.load()
     plan = _lib.DlMixPlan()
     _lib.check(lib.dl_mix_plan_shape(W.n_rows, W.n_src - W.n_rows, int(n_params), W.nnz,
                                      W.uniform_row_nnz, W.shared_row_weights,
-                                     int(bool(deviation)), ctypes.byref(plan)),
+                                     int(bool(deviation)), int(tile_cols), ctypes.byref(plan)),
                "dl_mix_plan_shape")
     return {f: getattr(plan, f) for f, _ in plan._fields_}
 
@@ -277,7 +278,8 @@ class GossipEngine:
             self.device = torch.device("cuda", torch.cuda.current_device())
         self.W = DeviceCsr(csr, self.device)
         self.n, self.P = csr.n_rows, int(n_params)
-        plan = plan_shape(self.W, self.P, deviation=True)
+        plan = plan_shape(self.W, self.P, deviation=True,
+                          tile_cols=int(tile_cols) if tile_cols else -1)
         tiled_ok = plan["path"] == 1 and plan["tile_cols"] >= 4 and self.W.n_src == self.n
         if layout == "auto":
             layout = "tiled" if tiled_ok else "rows"
@@ -333,6 +335,6 @@ class GossipEngine:
         return deviation(self.X, self.dev_sq, self.dev_max, mean_out=mean_out, workspace=self.ws)
 
     def plan(self, deviation=True):
-        p = plan_shape(self.W, self.P, deviation)
+        p = plan_shape(self.W, self.P, deviation, tile_cols=self.T)
         p["layout"] = self.layout
         return p

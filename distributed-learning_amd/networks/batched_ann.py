@@ -41,7 +41,7 @@ class BatchedANN:
 
     # -------------------------------------------------------------- helpers
     def _gemm(self, M, N, K, A, lda, sA, ta, B, ldb, sB, tb, C, ldc, sC, epi="none", bias=None,
-              H=None, rowsum=None, X=None):
+              H=None, rowsum=None, labels=None, loss=None):
         lib = _lib.load()
 
         def p(t, off=0):
@@ -50,10 +50,11 @@ class BatchedANN:
             return ctypes.c_void_p(t.data_ptr() + 4 * off)
         args = _lib.DlBgemmArgs(
             self.N, M, N, K, p(*A), lda, sA, int(ta), p(*B), ldb, sB, int(tb), p(*C), ldc, sC,
-            _lib.EPI[epi], p(*bias) if bias else None, self.P if bias else 0,
+            _lib.EPI[epi], p(*bias) if bias else None, bias[0].stride(0) if bias else 0,
             p(H) if H is not None else None, self.dh if H is not None else 0,
             self.B * self.dh if H is not None else 0,
-            p(*rowsum) if rowsum else None, self.P if rowsum else 0)
+            p(*rowsum) if rowsum else None, rowsum[0].stride(0) if rowsum else 0,
+            p(labels), labels.stride(0) if labels is not None else 0, p(loss))
         _lib.check(lib.dl_bgemm(ctypes.byref(args), _lib.stream_handle(self.device)), "dl_bgemm")
 
     def gradients(self, X, data, labels, G):
@@ -79,11 +80,16 @@ class BatchedANN:
                    (self.H2,), dh, hs, "bias_tanh", bias=(X, o["fc2.bias"]))
         self._gemm(B, dh, dh, (self.H2,), dh, hs, 0, (X, o["fc3.weight"]), dh, sx, 1,
                    (self.H3,), dh, hs, "bias_elu", bias=(X, o["fc3.bias"]))
-        self._gemm(B, dout, dh, (self.H3,), dh, hs, 0, (X, o["fc4.weight"]), dh, sx, 1,
-                   (self.Z4,), dout, B * dout, "bias", bias=(X, o["fc4.bias"]))
-        _lib.check(lib.dl_xent_grad(_lib.ptr(self.Z4), B * dout, _lib.ptr(labels), B,
-                                    _lib.ptr(self.dZ4), B * dout, _lib.ptr(self.loss), N, B, dout,
-                                    _lib.stream_handle(self.device)), "dl_xent_grad")
+        if B <= 64:   # logits + cross-entropy head in one launch (one tile per agent)
+            self._gemm(B, dout, dh, (self.H3,), dh, hs, 0, (X, o["fc4.weight"]), dh, sx, 1,
+                       (self.dZ4,), dout, B * dout, "bias_xent", bias=(X, o["fc4.bias"]),
+                       labels=labels, loss=self.loss)
+        else:
+            self._gemm(B, dout, dh, (self.H3,), dh, hs, 0, (X, o["fc4.weight"]), dh, sx, 1,
+                       (self.Z4,), dout, B * dout, "bias", bias=(X, o["fc4.bias"]))
+            _lib.check(lib.dl_xent_grad(_lib.ptr(self.Z4), B * dout, _lib.ptr(labels), B,
+                                        _lib.ptr(self.dZ4), B * dout, _lib.ptr(self.loss), N, B,
+                                        dout, _lib.stream_handle(self.device)), "dl_xent_grad")
         # ---- backward (weight grads straight into G rows, bias grads as row sums of dZ^T)
         self._gemm(dout, dh, B, (self.dZ4,), dout, B * dout, 1, (self.H3,), dh, hs, 0,
                    (G, o["fc4.weight"]), dh, sg, rowsum=(G, o["fc4.bias"]))

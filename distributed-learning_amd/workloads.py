@@ -75,13 +75,16 @@ class MLPConsensusSGD:
     def __init__(self, ann, eng, data, labels, lr, deviation=True):
         if eng.layout != "rows":
             raise ValueError("the batched gradients read X row-major: use GossipEngine(layout='rows')")
-        if eng.n != ann.N or eng.P != ann.P:
+        if eng.n != ann.N or eng.P < ann.P:
             raise ValueError("engine and model disagree on agents/params")
         import torch
         self.ann, self.eng = ann, eng
         self.data, self.labels = data, labels
         self.lr, self.deviation = float(lr), bool(deviation)
-        self.G = torch.empty(ann.N, ann.P, dtype=torch.float32, device=eng.device)
+        # The engine may carry zero padding columns [ann.P, eng.P) (a whole number of mix tiles:
+        # no ragged tail launch).  They stay exactly zero -- G is zero there and W 0 = 0 -- and
+        # add exact zeros to the deviation, so results are those of the unpadded round.
+        self.G = torch.zeros(ann.N, eng.P, dtype=torch.float32, device=eng.device)
         self.graphs = None
         self._torch = torch
 
@@ -90,8 +93,16 @@ class MLPConsensusSGD:
         """Per-agent mean cross-entropy of the last step (device tensor [N])."""
         return self.ann.loss
 
+    @staticmethod
+    def padded_params(csr, n_params, device):
+        """n_params rounded up to the row-major mix tile width for this graph."""
+        from .engine import DeviceCsr, plan_shape
+        T = plan_shape(DeviceCsr(csr, device), n_params, deviation=True)["tile_cols"]
+        return -(-n_params // T) * T if T else n_params
+
     def step(self):
-        self.ann.gradients(self.eng.X, self.data, self.labels, self.G)
+        P = self.ann.P
+        self.ann.gradients(self.eng.X[:, :P], self.data, self.labels, self.G[:, :P])
         self.eng.round(G=self.G, lr=self.lr, deviation=self.deviation)
 
     def capture(self):

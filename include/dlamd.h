@@ -107,12 +107,13 @@ int dl_abi_version(void);
 const char *dl_last_error(void);
 
 size_t dl_mix_workspace_bytes(int32_t n_rows, int32_t n_halo, int64_t n_params);
-/* Plan from shapes only (no pointers): what dl_mix_round would pick for a row-major round with
- * these sizes, with (sgd) / without a local step and with (deviation) / without the fused
- * deviation.  plan->tile_cols is the width the column-tiled layout must use. */
+/* Plan from shapes only (no pointers): what dl_mix_round would pick for these sizes, with
+ * (deviation) / without the fused deviation.  tile_cols: 0 = row-major operands; > 0 = operands
+ * in the column-tiled layout of that width; -1 = choose the width for a column-tiled layout
+ * (plan->tile_cols; 0 with the row-major plan if no tile of all rows fits LDS). */
 int dl_mix_plan_shape(int32_t n_rows, int32_t n_halo, int64_t n_params, int32_t nnz,
                       int32_t uniform_row_nnz, int32_t shared_row_weights, int32_t deviation,
-                      dl_mix_plan *plan);
+                      int32_t tile_cols, dl_mix_plan *plan);
 int dl_mix_plan_query(const dl_mix_args *args, dl_mix_plan *plan);
 int dl_mix_round(const dl_mix_args *args, void *workspace, size_t ws_bytes, dl_stream_t stream);
 
@@ -196,10 +197,16 @@ int dl_perron_round(const dl_perron_args *args, void *workspace, size_t ws_bytes
  * epi: DL_EPI_BIAS[_RELU|_TANH|_ELU] add bias[b][n] then activate (forward);
  *      DL_EPI_D{RELU,TANH,ELU} multiply by the activation derivative read from the layer's
  *      OUTPUT H[b] (ldh) (backward);  rowsum (nullable) receives sum_k op(A)[b][m][k] (the
- *      bias gradient when op(A) = dZ^T).  fp32 MFMA (16x16x4), exact fp32 products. */
+ *      bias gradient when op(A) = dZ^T).
+ *      DL_EPI_BIAS_XENT (M <= 64 rows = the batch, N <= 64 classes): add bias -> logits z, then
+ *      the torch.nn.CrossEntropyLoss head in the same launch: C[b] receives
+ *      dZ = (softmax(z) - onehot(labels[b])) / M and loss[b] (nullable) the mean loss; labels
+ *      must lie in [0, N).  Deterministic (fixed-order sums).
+ * fp32 MFMA (16x16x4), exact fp32 products. */
 enum dl_epilogue {
     DL_EPI_NONE = 0, DL_EPI_BIAS = 1, DL_EPI_BIAS_RELU = 2, DL_EPI_BIAS_TANH = 3,
-    DL_EPI_BIAS_ELU = 4, DL_EPI_DRELU = 5, DL_EPI_DTANH = 6, DL_EPI_DELU = 7
+    DL_EPI_BIAS_ELU = 4, DL_EPI_DRELU = 5, DL_EPI_DTANH = 6, DL_EPI_DELU = 7,
+    DL_EPI_BIAS_XENT = 8
 };
 typedef struct dl_bgemm_args {
     int32_t batch, M, N, K;
@@ -210,6 +217,8 @@ typedef struct dl_bgemm_args {
     const float *bias; int64_t s_bias;
     const float *H; int64_t ldh, sH;
     float *rowsum; int64_t s_rowsum;
+    const int32_t *labels; int64_t s_labels;   /* DL_EPI_BIAS_XENT: [batch][M] class ids */
+    float *loss;                               /* DL_EPI_BIAS_XENT: nullable [batch] */
 } dl_bgemm_args;
 int dl_bgemm(const dl_bgemm_args *args, dl_stream_t stream);
 

@@ -83,7 +83,7 @@ def test_shared_row_weights_flag_and_plan():
     plans = []
     for shared in (0, 1):
         pl = _lib.DlMixPlan()
-        _lib.check(lib.dl_mix_plan_shape(4096, 0, 1 << 18, csr.nnz, 5, shared, 1,
+        _lib.check(lib.dl_mix_plan_shape(4096, 0, 1 << 18, csr.nnz, 5, shared, 1, -1,
                                          ctypes.byref(pl)), "plan")
         plans.append((pl.path, pl.tile_cols, pl.lds_bytes))
     assert plans[0][0] == 2                      # per-entry weights: gather path
@@ -95,3 +95,20 @@ def test_shared_row_weights_flag_and_plan():
     args.W = _lib.DlCsr(16, 16, 16, 4, 10, 0, 0, 1)   # shared weights on an irregular CSR
     rc = lib.dl_mix_round(ctypes.byref(args), None, 0, None)
     assert rc == _lib.DL_ERR_INVALID and b"shared_row_weights" in lib.dl_last_error()
+
+
+@pytest.mark.parametrize("n,T", [(1024, 16), (512, 32), (256, 64), (2048, 8), (4096, 4),
+                                 (64, 128), (7, 128)])
+def test_tiled_width_choice(n, T):
+    """dl_mix_plan_shape(tile_cols=-1) picks the widest tile of <= 64 KiB for
+    degree-4 graphs with one shared weight sequence."""
+    from distributed_learning_amd import _lib
+    lib = _lib.load()
+    pl = _lib.DlMixPlan()
+    nnz = 5 * n
+    _lib.check(lib.dl_mix_plan_shape(n, 0, 1 << 20, nnz, 5, 1, 1, -1, ctypes.byref(pl)), "plan")
+    assert pl.path == 1 and pl.tile_cols == T
+    assert pl.tile_cols * n * 4 <= 65536 or pl.tile_cols == 4
+    # at C = 4 one workgroup per CU, else two when LDS allows
+    if T == 16:
+        assert pl.grid <= 256

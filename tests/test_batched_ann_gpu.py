@@ -106,3 +106,36 @@ def test_mlp_consensus_graph_replay_matches_eager(cuda):
     for (xe, de, le), (xg, dg, lg) in zip(runs["eager"], runs["graph"]):
         assert torch.equal(xe, xg) and torch.equal(de, dg) and torch.equal(le, lg)
     assert not torch.equal(runs["eager"][0][0], X0)
+
+
+def test_mlp_consensus_zero_padding_is_exact(cuda):
+    """Zero padding columns up to a whole mix tile (no ragged tail launch) leave the real
+    columns bit-identical to the unpadded round; the deviation sums the same terms (plus exact
+    zeros) grouped by a different launch split, so it agrees to fp32 rounding."""
+    from distributed_learning_amd import engine
+    from distributed_learning_amd.graph import from_edge_weights, random_regular_edges
+    from distributed_learning_amd.networks.batched_ann import BatchedANN
+    from distributed_learning_amd.workloads import MLPConsensusSGD
+    n, b = 32, 16
+    gen = torch.Generator(device=cuda).manual_seed(9)
+    bann = BatchedANN(n, b, 40, 24, 10, device=cuda)
+    P = bann.P
+    X0 = 0.2 * torch.randn(n, P, device=cuda, generator=gen)
+    data = torch.randn(n, b, 40, device=cuda, generator=gen)
+    labels = torch.randint(0, 10, (n, b), device=cuda, generator=gen, dtype=torch.int32)
+    edges = random_regular_edges(4, n, seed=2)
+    csr = from_edge_weights(edges, [0.2] * len(edges), list(range(n)))
+    P_pad = MLPConsensusSGD.padded_params(csr, P, cuda)
+    assert P_pad > P
+    res = []
+    for cols in (P, P_pad):
+        eng = engine.GossipEngine(csr, cols, device=cuda,
+                                  X=torch.nn.functional.pad(X0, (0, cols - P)), layout="rows")
+        sgd = MLPConsensusSGD(bann, eng, data, labels, lr=0.2)
+        for _ in range(3):
+            sgd.step()
+        torch.cuda.synchronize()
+        assert torch.all(eng.X[:, P:] == 0)
+        res.append((eng.X[:, :P].clone(), eng.dev_sq.clone()))
+    assert torch.equal(res[0][0], res[1][0])
+    torch.testing.assert_close(res[0][1], res[1][1], rtol=1e-5, atol=0)

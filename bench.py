@@ -67,17 +67,20 @@ def build_graph(n):
 
 
 def copy_ceiling(dev, nbytes=4 << 30, reps=10):
-    """Measured HBM ceiling: float4 streaming copy (libdlamd dl_stream_copy) of a 4 GiB buffer,
-    counting read + write bytes."""
+    """Measured HBM ceilings (libdlamd dl_stream_copy) over 4 GiB streams: float4 copies
+    (variants 0-3, read + write bytes) and the triad y = x - lr g (variants 4-5: two reads, one
+    write -- the fused round's own traffic, 12 B per element).  Returns (best copy GB/s, best
+    triad GB/s, per-variant GB/s)."""
     from distributed_learning_amd import _lib
     lib = _lib.load()
-    a = torch.zeros(nbytes // 4, dtype=torch.float32, device=dev)
-    b = torch.empty_like(a)
+    a = torch.zeros(2 * nbytes // 4, dtype=torch.float32, device=dev)
+    b = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
+    n = b.numel()
 
     best = {}
-    for variant in (0, 1, 2, 3):
+    for variant in (0, 1, 2, 3, 4, 5):
         def cp():
-            _lib.check(lib.dl_stream_copy(_lib.ptr(a), _lib.ptr(b), a.numel(), variant,
+            _lib.check(lib.dl_stream_copy(_lib.ptr(a), _lib.ptr(b), n, variant,
                                           _lib.stream_handle(dev)), "dl_stream_copy")
         cp()
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -87,9 +90,10 @@ def copy_ceiling(dev, nbytes=4 << 30, reps=10):
             cp()
         e.record()
         torch.cuda.synchronize()
-        best[variant] = 2 * nbytes / (s.elapsed_time(e) / 1e3 / reps) / 1e9
+        moved = (3 if variant >= 4 else 2) * nbytes
+        best[variant] = moved / (s.elapsed_time(e) / 1e3 / reps) / 1e9
     del a, b
-    return max(best.values()), best
+    return (max(best[v] for v in (0, 1, 2, 3)), max(best[v] for v in (4, 5)), best)
 
 
 def kernel_name(plan, sgd, dev, n_src):
@@ -101,7 +105,7 @@ def kernel_name(plan, sgd, dev, n_src):
     return f"mix_tile_kernel<{c}, {kv}, {b(sgd)}, {b(dev)}, true, false, true>"
 
 
-def traffic_from_profile(kname, path=os.path.join(ROOT, "profiles", "r01", "summary.json")):
+def traffic_from_profile(kname, path=os.path.join(ROOT, "profiles", "r02", "summary.json")):
     """HBM bytes per launch of this kernel from the committed rocprofv3 PMC summary
     (FETCH_SIZE x 2 + WRITE_SIZE, gfx950 correction), or None if it was not profiled."""
     try:
@@ -248,7 +252,10 @@ def run_c3(args, dev, rank, world):
     sgd = MLPConsensusSGD(ann, eng, data, labels, lr, deviation=True)
     G = sgd.G
     stream = torch.cuda.current_stream(dev)
-    # phase times: eager steps bracketed by HIP events (kernel time is the same under a graph)
+    # phase times: eager steps bracketed by HIP events (kernel time is the same under a graph),
+    # after warmup steps that load every kernel's code object
+    for _ in range(max(args.warmup, 2)):
+        sgd.step()
     n_ev = min(args.steps, 20)
     evs = event_pairs(n_ev, 3)
     for i in range(n_ev):
@@ -493,7 +500,7 @@ def main():
     if rank == 0:
         kname = kernel_name(plan, sgd, True, n)
         traffic, traffic_src = traffic_from_profile(kname)
-        ceiling, ceiling_variants = copy_ceiling(dev)
+        ceiling, triad, ceiling_variants = copy_ceiling(dev)
         cpu = None
         if not args.no_cpu:
             cb = cpu_baseline(csr, n, P, min(args.cpu_cols, P), sgd, lr)
@@ -532,7 +539,9 @@ def main():
                          "kernel": "mix_tile_kernel (+dev_reduce) per-round HIP-event time",
                          "bytes_per_launch": bytes_per_round, "launch_ms": launch_ms,
                          "measured_copy_ceiling_GBs": ceiling,
-                         "copy_variants_GBs": ceiling_variants},
+                         "measured_triad_ceiling_GBs": triad,
+                         "frac_of_measured_triad": achieved / triad,
+                         "stream_variants_GBs": ceiling_variants},
             "cpu_baseline": cpu,
             "final_max_deviation": dev_max,
         }

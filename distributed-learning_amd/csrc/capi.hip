@@ -634,9 +634,9 @@ int dl_stream_copy(const float *src, float *dst, int64_t n_floats, int32_t varia
                    dl_stream_t stream) {
     g_err.clear();
     if (!src || !dst || n_floats < 0 || (n_floats & 3) || !aligned16(src) || !aligned16(dst) ||
-        variant < 0 || variant > 3)
+        variant < 0 || variant > 5)
         return fail(DL_ERR_INVALID, "dl_stream_copy: needs 16-byte aligned buffers, n %% 4 == 0, "
-                                    "variant 0..3");
+                                    "variant 0..5");
     hipError_t e = dl::launch_stream_copy(src, dst, n_floats, variant,
                                           static_cast<hipStream_t>(stream));
     return e == hipSuccess ? DL_OK : hip_fail(e, "stream_copy launch");

@@ -459,6 +459,30 @@ __global__ void __launch_bounds__(256) stream_copy_kernel(const float4 *__restri
     }
 }
 
+// Streaming triad y = x - 1e-3 g (HBM ceiling of the 2-read : 1-write round traffic),
+// grid-stride, U float4 per stream per thread in flight, non-temporal loads and stores.
+template <int U>
+__global__ void stream_triad_kernel(const float4 *__restrict__ x, const float4 *__restrict__ g,
+                                    float4 *__restrict__ y, int64_t n4) {
+    const int64_t step = (int64_t)gridDim.x * blockDim.x * U;
+    for (int64_t base = (int64_t)blockIdx.x * blockDim.x * U; base < n4; base += step) {
+        float4 a[U], b[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const int64_t i = base + j * blockDim.x + threadIdx.x;
+            if (i < n4) {
+                a[j] = nt_load4(x + i);
+                b[j] = nt_load4(g + i);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const int64_t i = base + j * blockDim.x + threadIdx.x;
+            if (i < n4) nt_store4(local_step(a[j], b[j], 1e-3f), y + i);
+        }
+    }
+}
+
 template <int C, int KV, bool SGD, bool DEV, bool MIX, bool HALO, bool FAST>
 hipError_t launch_one(const TileArgs &a, int grid, int lds, hipStream_t s) {
     auto k = mix_tile_kernel<C, KV, SGD, DEV, MIX, HALO, FAST>;
@@ -567,6 +591,15 @@ hipError_t launch_dev_reduce(const float *partial, int nparts, int n_rows, float
 hipError_t launch_stream_copy(const float *src, float *dst, int64_t n_floats, int variant,
                               hipStream_t s) {
     const int64_t n4 = n_floats / 4;
+    if (variant >= 4) {
+        auto x = reinterpret_cast<const float4 *>(src);
+        auto y = reinterpret_cast<float4 *>(dst);
+        if (variant == 4)
+            hipLaunchKernelGGL(stream_triad_kernel<1>, dim3(256), dim3(512), 0, s, x, x + n4, y, n4);
+        else
+            hipLaunchKernelGGL(stream_triad_kernel<4>, dim3(1024), dim3(256), 0, s, x, x + n4, y, n4);
+        return hipGetLastError();
+    }
     const int U = variant == 0 ? 1 : variant == 3 ? 4 : 8;
     int64_t grid = (n4 + 256 * U - 1) / (256 * U);
     const int64_t gmax = variant == 0 ? 256 * 8 : variant == 3 ? 256 * 32 : 256 * 4;

@@ -153,8 +153,12 @@ int dl_step_rows(const float *x, int64_t ldx, const float *g, int64_t ldg, float
 
 /* dst[i] = src[i] for n_floats floats (float4 streaming copy; variant 0: one load in flight
  * per thread, 1: eight, 2: eight + non-temporal stores, 3: four + non-temporal loads and
- * stores on a 8192-workgroup grid).  Not on the reference path: the bench
- * uses it to measure the HBM copy ceiling next to the mix kernel's achieved bandwidth. */
+ * stores on a 8192-workgroup grid).  Variants 4 and 5 are the triad
+ * dst[i] = src[i] - 1e-3 * src[n_floats + i] (src holds 2 * n_floats floats): two read streams
+ * and one write stream, the traffic of the fused local step + mix round (12 B per element);
+ * 4: one float4 per stream in flight, 512-thread workgroups x 256; 5: four, 256 x 1024; all
+ * non-temporal.  Not on the reference path: the bench uses them to measure the HBM streaming
+ * ceilings next to the mix kernel's achieved bandwidth. */
 int dl_stream_copy(const float *src, float *dst, int64_t n_floats, int32_t variant,
                    dl_stream_t stream);
 

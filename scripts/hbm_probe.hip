@@ -61,6 +61,58 @@ __global__ void copy_chunk_k(const f32x4 *__restrict__ s, f32x4 *__restrict__ d,
     }
 }
 
+// triad y = x - lr*g: two read streams, one write stream (the traffic of the fused SGD + mix
+// round, 12 B per element), grid-stride, U float4 per stream per thread
+template <int U, bool NT>
+__global__ void triad_k(const f32x4 *__restrict__ x, const f32x4 *__restrict__ g,
+                        f32x4 *__restrict__ y, long n4, float lr) {
+    const long step = (long)gridDim.x * blockDim.x * U;
+    for (long base = (long)blockIdx.x * blockDim.x * U; base < n4; base += step) {
+        f32x4 a[U], b[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            long i = base + (long)j * blockDim.x + threadIdx.x;
+            if (i < n4) {
+                a[j] = NT ? __builtin_nontemporal_load(x + i) : x[i];
+                b[j] = NT ? __builtin_nontemporal_load(g + i) : g[i];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            long i = base + (long)j * blockDim.x + threadIdx.x;
+            if (i < n4) {
+                f32x4 v = a[j] - lr * b[j];
+                if (NT) __builtin_nontemporal_store(v, y + i);
+                else y[i] = v;
+            }
+        }
+    }
+}
+
+// contiguous chunk per workgroup, triad (each WG streams its own range, like the tile kernel)
+template <int U>
+__global__ void triad_chunk_k(const f32x4 *__restrict__ x, const f32x4 *__restrict__ g,
+                              f32x4 *__restrict__ y, long n4, float lr) {
+    const long per = (n4 + gridDim.x - 1) / gridDim.x;
+    const long b0 = (long)blockIdx.x * per, b1 = b0 + per < n4 ? b0 + per : n4;
+    for (long base = b0; base < b1; base += (long)blockDim.x * U) {
+        f32x4 a[U], b[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            long i = base + (long)j * blockDim.x + threadIdx.x;
+            if (i < b1) {
+                a[j] = __builtin_nontemporal_load(x + i);
+                b[j] = __builtin_nontemporal_load(g + i);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            long i = base + (long)j * blockDim.x + threadIdx.x;
+            if (i < b1) __builtin_nontemporal_store(a[j] - lr * b[j], y + i);
+        }
+    }
+}
+
 template <int U>
 __global__ void read_k(const f32x4 *__restrict__ s, long n4, float *out) {
     const long step = (long)gridDim.x * blockDim.x * U;
@@ -110,8 +162,36 @@ float time_ms(F f, int reps) {
     return ms / reps;
 }
 
+int triad_main(long bytes) {
+    // x, g, y of `bytes` each; traffic = 3 * bytes per launch
+    const long n4 = bytes / 16;
+    f32x4 *x, *g, *y;
+    CHECK(hipMalloc(&x, bytes));
+    CHECK(hipMalloc(&g, bytes));
+    CHECK(hipMalloc(&y, bytes));
+    CHECK(hipMemset(x, 0, bytes));
+    CHECK(hipMemset(g, 0, bytes));
+    const int reps = 10;
+    const double traffic = 3.0 * bytes;
+    for (int bs : {256, 512, 1024})
+        for (int gr : {256, 512, 1024, 2048, 4096, 8192, 16384}) {
+            auto pr = [&](const char *name, float ms) {
+                printf("{\"kernel\":\"%s\",\"block\":%d,\"grid\":%d,\"ms\":%.4f,\"GBs\":%.1f}\n",
+                       name, bs, gr, ms, traffic / ms / 1e6);
+            };
+            pr("triad_u1_nt", time_ms([&] { triad_k<1, true><<<gr, bs>>>(x, g, y, n4, 1e-3f); }, reps));
+            pr("triad_u2_nt", time_ms([&] { triad_k<2, true><<<gr, bs>>>(x, g, y, n4, 1e-3f); }, reps));
+            pr("triad_u4_nt", time_ms([&] { triad_k<4, true><<<gr, bs>>>(x, g, y, n4, 1e-3f); }, reps));
+            pr("triad_u4", time_ms([&] { triad_k<4, false><<<gr, bs>>>(x, g, y, n4, 1e-3f); }, reps));
+            pr("triad_chunk_u2", time_ms([&] { triad_chunk_k<2><<<gr, bs>>>(x, g, y, n4, 1e-3f); }, reps));
+            fflush(stdout);
+        }
+    return 0;
+}
+
 int main(int argc, char **argv) {
     const long bytes = (argc > 1 ? atol(argv[1]) : 4096L) << 20;  // MiB
+    if (argc > 2 && argv[2][0] == 't') return triad_main(bytes);
     const long n4 = bytes / 16;
     f32x4 *s, *d;
     float *o;

@@ -18,6 +18,10 @@ Other BASELINE configs (not the headline line; run on request):
       torus on one GPU (tiled layout).  N>1: agents partitioned into 2-D torus blocks, one per
       rank, boundary rows exchanged over RCCL send/recv every round (HaloShard), so the total
       work is fixed (strong scaling).
+  c5  Wide-ResNet-16-4 consensus SGD, 64 agents x 2,751,146 params, B=64 synthetic CIFAR-shaped
+      batches: per-agent PyTorch-ROCm (MIOpen) forward/backward into G's rows, dl_sgd_step
+      (SGD momentum 0.9, wd 5e-4) and the fused round, one hipGraph per step.
+      N>1: independent replicas.
 """
 import argparse
 import json
@@ -41,13 +45,15 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=10)
-    p.add_argument("--workload", default="c2", choices=["c2", "c2-mix", "c3", "c4"])
+    p.add_argument("--workload", default="c2", choices=["c2", "c2-mix", "c3", "c4", "c5"])
     p.add_argument("--agents", type=int, default=1024)
     p.add_argument("--params", type=int, default=1 << 20)
     p.add_argument("--cpu-cols", type=int, default=1 << 18,
                    help="columns of the bounded CPU-baseline sample (all agents)")
     p.add_argument("--no-cpu", action="store_true")
-    p.add_argument("--no-graph", action="store_true", help="c3: eager launches, no hipGraph")
+    p.add_argument("--no-graph", action="store_true", help="c3/c5: eager launches, no hipGraph")
+    p.add_argument("--streams", type=int, default=1, help="c5: HIP streams the agents share")
+    p.add_argument("--batch", type=int, default=64, help="c5: images per agent per step")
     p.add_argument("--dist-backend", default="nccl",
                    help="nccl (= RCCL, default) or gloo (multi-rank rehearsal on one GPU)")
     return p.parse_args()
@@ -417,6 +423,135 @@ def run_c4(args, dev, rank, world):
     print(json.dumps(rec), flush=True)
 
 
+def c5_cpu_baseline(wl, csr, n_agents_sample=2):
+    """The reference's CPU path for one c5 step: per agent a torch CPU forward/backward of
+    Wide_ResNet on its batch and optim.SGD.step -- timed on a sample of agents and scaled --
+    plus the numpy restatement of Mixer._mix_params_once + _get_deviation_dict on all agents."""
+    from oracle import mixer_ref as M
+    from distributed_learning_amd.networks.wide_resnet import Wide_ResNet
+    torch.manual_seed(0)
+    model = Wide_ResNet(*wl.arch)
+    x = torch.randn(wl.B, 3, 32, 32)
+    y = torch.randint(0, wl.arch[3], (wl.B,))
+    opt = torch.optim.SGD(model.parameters(), lr=wl.lr, momentum=wl.momentum,
+                          weight_decay=wl.wd)
+
+    def agent_step():
+        opt.zero_grad()
+        torch.nn.functional.cross_entropy(model(x), y).backward()
+        opt.step()
+    agent_step()
+    t0 = time.perf_counter()
+    for _ in range(n_agents_sample):
+        agent_step()
+    t_grad = (time.perf_counter() - t0) / n_agents_sample * wl.N
+    X = np.random.default_rng(0).standard_normal((wl.N, wl.P), dtype=np.float32)
+    t0 = time.perf_counter()
+    Y = M.mix_once(X, csr.rowptr, csr.col, csr.w)
+    M.deviation(Y)
+    t_mix = time.perf_counter() - t0
+    return 1.0 / (t_grad + t_mix), torch.get_num_threads(), t_grad, t_mix
+
+
+def run_c5(args, dev, rank, world):
+    """Config c5: WRN-16-4 consensus SGD.  One step = every agent's forward + cross-entropy +
+    backward on its own B-image batch (MIOpen fp32 convs, gradients accumulate straight into G's
+    rows), the SGD-momentum local step (dl_sgd_step) and the fused mix + deviation round over a
+    random 4-regular graph of 64 agents.  N>1: one independent 64-agent system per GPU."""
+    from distributed_learning_amd.workloads import WRNConsensusSGD
+    n, B = 64, args.batch
+    csr, wconst = build_graph(n)
+    t0 = time.perf_counter()
+    wl = WRNConsensusSGD(csr, B, device=dev, seed=1000 * rank, streams=args.streams)
+    stream = torch.cuda.current_stream(dev)
+    wl.step()                          # MIOpen finds every conv solution here
+    torch.cuda.synchronize()
+    log(f"c5: setup + first step {time.perf_counter() - t0:.1f} s")
+    for _ in range(max(args.warmup, 1)):
+        wl.step()
+    n_ev = min(args.steps, 5)
+    evs = event_pairs(n_ev, 3)
+    for i in range(n_ev):
+        evs[i][0].record(stream)
+        wl._local_grads()
+        evs[i][1].record(stream)
+        wl._round(first=False)
+        evs[i][2].record(stream)
+        wl.steps_done += 1
+    torch.cuda.synchronize()
+    grad_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in evs]))
+    mix_ms = float(np.mean([b.elapsed_time(c) for _, b, c in evs]))
+    loss0 = float(wl.loss.mean().item())
+    use_graph = not args.no_graph
+    if use_graph:
+        wl.capture()
+
+    def step(i):
+        if use_graph:
+            wl.replay(1)
+        else:
+            wl.step()
+
+    elapsed = timed_loop(step, args, world, dev)
+    loss1 = float(wl.loss.mean().item())
+    grad_ms = max_over_ranks(grad_ms, world, dev)
+    mix_ms = max_over_ranks(mix_ms, world, dev)
+    if rank != 0:
+        return
+    flops = wl.flops_per_step()
+    ms_step = elapsed / args.steps * 1e3
+    tflops = flops / (ms_step / 1e3) / 1e12
+    mix_bytes = 28 * n * wl.P    # sgd step: read x, g, buf, write buf, s; round: read s, write x
+    gbs = mix_bytes / (mix_ms / 1e3) / 1e9
+    grad_roof = {"bound": "mfma", "achieved": tflops, "peak": FP32_MFMA_PEAK_TFLOPS,
+                 "unit": "TFLOP/s", "frac": tflops / FP32_MFMA_PEAK_TFLOPS, "traffic": None,
+                 "kernel": "MIOpen fp32 convs (per-agent forward + backward), whole step time",
+                 "flops_per_launch": flops, "launch_ms": ms_step,
+                 "eager_gradient_phase_ms": grad_ms}
+    mix_roof = {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": gbs / HBM_PEAK_GBS, "traffic": None,
+                "kernel": "sgd_step_kernel + mix_tile_kernel (+dev_reduce)",
+                "bytes_per_launch": mix_bytes, "launch_ms": mix_ms}
+    cpu = None
+    if not args.no_cpu:
+        v, cores, tg, tm = c5_cpu_baseline(wl, csr)
+        cpu = {"value": v, "unit": "steps/s", "cores": cores, "kind": "port",
+               "sample": f"torch CPU forward/backward + optim.SGD step of Wide_ResNet(16, 4) on 2 "
+                         f"of {n} agents (B={B}), scaled to {n}: {tg:.2f} s; numpy restatement "
+                         f"of the mix + deviation on all {n} x {wl.P}: {tm:.3f} s",
+               "host_cores": os.cpu_count()}
+    rec = {
+        "metric": "c5 WRN-16-4 consensus SGD steps/sec (64 agents x 2,751,146 params)",
+        "value": world * args.steps / elapsed,
+        "unit": "steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": f"synthetic CIFAR-10-shaped batches x ~ N(0,1) [{B}x3x32x32], labels uniform in "
+                f"10 classes, one fixed batch per agent resident in HBM; default torch init",
+        "config": {"workload": "c5: Wide-ResNet-16-4 consensus SGD (per-agent MIOpen convs, "
+                               "SGD momentum step + fused round + deviation)",
+                   "agents": n, "params": wl.P, "batch": B, "lr": wl.lr,
+                   "momentum": wl.momentum, "weight_decay": wl.wd,
+                   "graph": "random 4-regular", "weights": f"best-constant {wconst:.6f}",
+                   "streams": args.streams,
+                   "miopen_find_mode": os.environ.get("MIOPEN_FIND_MODE", "default"),
+                   "launch": "hipGraph replay per step" if use_graph else "eager",
+                   "images_per_s": world * args.steps * n * B / elapsed,
+                   "parallelism": f"{world} independent replicas" if world > 1 else "single GPU"},
+        "roofline": grad_roof,
+        "phases": {"gradients": grad_roof, "round": mix_roof},
+        "cpu_baseline": cpu,
+        "mean_loss_first_last": [loss0, loss1],
+    }
+    print(json.dumps(rec), flush=True)
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -435,8 +570,8 @@ def main():
         else:
             dist.init_process_group(args.dist_backend)
 
-    if args.workload in ("c3", "c4"):
-        (run_c3 if args.workload == "c3" else run_c4)(args, dev, rank, world)
+    if args.workload in ("c3", "c4", "c5"):
+        {"c3": run_c3, "c4": run_c4, "c5": run_c5}[args.workload](args, dev, rank, world)
         if world > 1:
             dist.destroy_process_group()
         return

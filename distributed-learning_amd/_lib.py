@@ -55,6 +55,13 @@ class DlBgemmArgs(ctypes.Structure):
                 ("labels", _vp), ("s_labels", _i64), ("loss", _vp)]
 
 
+class DlSgdArgs(ctypes.Structure):
+    _fields_ = [("x", _vp), ("ldx", _i64), ("g", _vp), ("ldg", _i64), ("buf", _vp), ("ldb", _i64),
+                ("out", _vp), ("ldo", _i64), ("n_rows", _i32), ("n_params", _i64), ("lr", _f32),
+                ("momentum", _f32), ("dampening", _f32), ("weight_decay", _f32),
+                ("nesterov", _i32), ("first", _i32)]
+
+
 EPI = {"none": 0, "bias": 1, "bias_relu": 2, "bias_tanh": 3, "bias_elu": 4, "drelu": 5,
        "dtanh": 6, "delu": 7, "bias_xent": 8}
 
@@ -76,6 +83,7 @@ SIGNATURES = {
     "dl_max_column_std": (_i32, [_vp, _i64, _i32, _i64, _vp, _vp]),
     "dl_step_rows": (_i32, [_vp, _i64, _vp, _i64, _f32, _vp, _i32, _i64, _vp, _i64, _vp]),
     "dl_stream_copy": (_i32, [_vp, _vp, _i64, _i32, _vp]),
+    "dl_sgd_step": (_i32, [ctypes.POINTER(DlSgdArgs), _vp]),
     "dl_bgemm": (_i32, [ctypes.POINTER(DlBgemmArgs), _vp]),
     "dl_xent_grad": (_i32, [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i32, _i32, _i32, _vp]),
     "dl_perron_workspace_bytes": (_sz, [_i32, _i32, _i64]),

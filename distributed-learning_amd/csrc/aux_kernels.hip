@@ -88,6 +88,68 @@ __global__ void __launch_bounds__(256) step_rows_kernel(const float *__restrict_
     }
 }
 
+// ---------------------------------------------------------------- local optimizer step
+// torch.optim.SGD.step (single-tensor form, torch/optim/sgd.py) over a block of agent rows, in
+// the rounding of torch's fused add-with-alpha (one fma per `add(.., alpha=..)`):
+//   d = fma(wd, x, g)                                   grad.add(param, alpha=weight_decay)
+//   buf = first ? d : fma(1 - dampening, d, mu * buf)   buf.mul_(momentum).add_(grad, alpha=1-damp)
+//   d = nesterov ? fma(mu, buf, d) : buf                grad.add(buf, alpha=momentum)
+//   out = fma(-lr, d, x)                                param.add_(grad, alpha=-lr)
+// out may alias x (in-place step) or be the round's input buffer (step fused into the ping-pong).
+typedef float v4f __attribute__((ext_vector_type(4)));
+
+struct SgdParams {
+    float lr, mu, damp, wd;
+    int first, nesterov;
+};
+
+__device__ __forceinline__ float sgd_elem(float x, float g, float &b, const SgdParams &p) {
+    float d = p.wd != 0.f ? __builtin_fmaf(p.wd, x, g) : g;
+    if (p.mu != 0.f) {
+        b = p.first ? d : __builtin_fmaf(1.f - p.damp, d, p.mu * b);
+        d = p.nesterov ? __builtin_fmaf(p.mu, b, d) : b;
+    }
+    return __builtin_fmaf(-p.lr, d, x);
+}
+
+template <bool VEC>
+__global__ void __launch_bounds__(256) sgd_step_kernel(const float *x, int64_t ldx,
+                                                       const float *__restrict__ g, int64_t ldg,
+                                                       float *__restrict__ buf, int64_t ldb,
+                                                       float *out, int64_t ldo, int64_t n_params,
+                                                       SgdParams p) {
+    const int r = blockIdx.y;
+    const float *xr = x + (int64_t)r * ldx;
+    const float *gr = g + (int64_t)r * ldg;
+    float *br = buf ? buf + (int64_t)r * ldb : nullptr;
+    float *orow = out + (int64_t)r * ldo;
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    if (VEC) {
+        const int64_t n4 = n_params >> 2;
+        for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) {
+            const v4f xv = __builtin_nontemporal_load(reinterpret_cast<const v4f *>(xr) + i);
+            const v4f gv = __builtin_nontemporal_load(reinterpret_cast<const v4f *>(gr) + i);
+            v4f bv = br && !p.first ? reinterpret_cast<const v4f *>(br)[i] : v4f{0.f, 0.f, 0.f, 0.f};
+            v4f ov;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                float b = bv[k];
+                ov[k] = sgd_elem(xv[k], gv[k], b, p);
+                bv[k] = b;
+            }
+            if (br) reinterpret_cast<v4f *>(br)[i] = bv;
+            reinterpret_cast<v4f *>(orow)[i] = ov;
+        }
+    } else {
+        for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n_params; i += stride) {
+            float b = br && !p.first ? br[i] : 0.f;
+            const float o = sgd_elem(xr[i], gr[i], b, p);
+            if (br) br[i] = b;
+            orow[i] = o;
+        }
+    }
+}
+
 // ---------------------------------------------------------------- Perron / asyncio round
 // One Jacobi iteration on element i of an [R, TP] tile held in LDS (cur), neighbour sums in
 // socket order (np.sum(list, axis=0): first term, then left fold), then scale.
@@ -270,6 +332,26 @@ hipError_t launch_step_rows(const float *x, int64_t ldx, const float *g, int64_t
     if (bx > 1024) bx = 1024;
     hipLaunchKernelGGL(step_rows_kernel, dim3((unsigned)bx, n_sel), dim3(256), 0, s, x, ldx, g,
                        ldg, lr, rows, n_sel, n_params, out, ldo);
+    return hipGetLastError();
+}
+
+hipError_t launch_sgd_step(const float *x, int64_t ldx, const float *g, int64_t ldg, float *buf,
+                           int64_t ldb, float *out, int64_t ldo, int n_rows, int64_t n_params,
+                           float lr, float mu, float damp, float wd, int first, int nesterov,
+                           bool vec, hipStream_t s) {
+    const SgdParams p{lr, mu, damp, wd, first, nesterov};
+    const int64_t work = vec ? n_params >> 2 : n_params;
+    int64_t bx = (work + 255) / 256;
+    // ~16 workgroups per CU over all rows, each thread a few float4s (grid-stride)
+    int64_t cap = (8192 + n_rows - 1) / n_rows;
+    if (cap < 1) cap = 1;
+    if (bx > cap) bx = cap;
+    if (vec)
+        hipLaunchKernelGGL(sgd_step_kernel<true>, dim3((unsigned)bx, n_rows), dim3(256), 0, s, x,
+                           ldx, g, ldg, buf, ldb, out, ldo, n_params, p);
+    else
+        hipLaunchKernelGGL(sgd_step_kernel<false>, dim3((unsigned)bx, n_rows), dim3(256), 0, s, x,
+                           ldx, g, ldg, buf, ldb, out, ldo, n_params, p);
     return hipGetLastError();
 }
 

@@ -630,6 +630,34 @@ int dl_step_rows(const float *x, int64_t ldx, const float *g, int64_t ldg, float
     return e == hipSuccess ? DL_OK : hip_fail(e, "step_rows launch");
 }
 
+int dl_sgd_step(const dl_sgd_args *a, dl_stream_t stream) {
+    g_err.clear();
+    if (!a) return fail(DL_ERR_INVALID, "dl_sgd_step: null args");
+    if (a->n_rows == 0 || a->n_params == 0) return DL_OK;
+    if (!a->x || !a->g || !a->out || a->n_rows < 0 || a->n_rows > 65535 || a->n_params < 0 ||
+        a->ldx < a->n_params || a->ldg < a->n_params || a->ldo < a->n_params)
+        return fail(DL_ERR_INVALID, "dl_sgd_step: bad arguments (n_rows %d, n_params %lld)",
+                    a->n_rows, (long long)a->n_params);
+    if (a->momentum != 0.f && (!a->buf || a->ldb < a->n_params))
+        return fail(DL_ERR_INVALID, "dl_sgd_step: momentum needs a buffer [n_rows, ldb >= n_params]");
+    if (a->nesterov && (a->momentum <= 0.f || a->dampening != 0.f))
+        return fail(DL_ERR_INVALID, "dl_sgd_step: Nesterov momentum requires a momentum and zero "
+                                    "dampening");
+    const size_t rb = (size_t)a->n_params * sizeof(float);
+    if (a->out != a->x && overlaps(a->out, ((size_t)a->n_rows - 1) * a->ldo * 4 + rb, a->x,
+                                   ((size_t)a->n_rows - 1) * a->ldx * 4 + rb))
+        return fail(DL_ERR_INVALID, "dl_sgd_step: out must be x itself or not overlap it");
+    float *buf = a->momentum != 0.f ? a->buf : nullptr;
+    const bool vec = aligned16(a->x) && aligned16(a->g) && aligned16(a->out) &&
+                     (!buf || aligned16(buf)) && (a->n_params & 3) == 0 && (a->ldx & 3) == 0 &&
+                     (a->ldg & 3) == 0 && (a->ldo & 3) == 0 && (!buf || (a->ldb & 3) == 0);
+    hipError_t e = dl::launch_sgd_step(a->x, a->ldx, a->g, a->ldg, buf, a->ldb, a->out, a->ldo,
+                                       a->n_rows, a->n_params, a->lr, a->momentum, a->dampening,
+                                       a->weight_decay, a->first ? 1 : 0, a->nesterov ? 1 : 0,
+                                       vec, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? DL_OK : hip_fail(e, "sgd_step launch");
+}
+
 int dl_stream_copy(const float *src, float *dst, int64_t n_floats, int32_t variant,
                    dl_stream_t stream) {
     g_err.clear();

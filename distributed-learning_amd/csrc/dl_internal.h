@@ -76,6 +76,10 @@ hipError_t launch_max_column_std(const float *x, int64_t ldx, int n_rows, int64_
 hipError_t launch_step_rows(const float *x, int64_t ldx, const float *g, int64_t ldg, float lr,
                             const int32_t *rows, int n_sel, int64_t n_params, float *out,
                             int64_t ldo, hipStream_t s);
+hipError_t launch_sgd_step(const float *x, int64_t ldx, const float *g, int64_t ldg, float *buf,
+                           int64_t ldb, float *out, int64_t ldo, int n_rows, int64_t n_params,
+                           float lr, float mu, float damp, float wd, int first, int nesterov,
+                           bool vec, hipStream_t s);
 
 struct PerronArgs {
     void *y;

@@ -124,3 +124,194 @@ class MLPConsensusSGD:
             self.graphs[self._parity].replay()
             self._parity ^= 1
             self.eng.X, self.eng.Y = self.eng.Y, self.eng.X
+
+
+def _sgd_args(X, G, M, out, lr, momentum, dampening, weight_decay, nesterov, first):
+    from . import _lib
+    return _lib.DlSgdArgs(_lib.ptr(X), X.stride(0), _lib.ptr(G), G.stride(0), _lib.ptr(M),
+                          M.stride(0) if M is not None else 0, _lib.ptr(out), out.stride(0),
+                          X.shape[0], X.shape[1], float(lr), float(momentum), float(dampening),
+                          float(weight_decay), int(bool(nesterov)), int(bool(first)))
+
+
+def sgd_step(X, G, M=None, out=None, lr=0.1, momentum=0.0, dampening=0.0, weight_decay=0.0,
+             nesterov=False, first=False):
+    """``dl_sgd_step``: torch.optim.SGD.step over agent rows (X, G, M, out: [N, P] row-major
+    device tensors; out defaults to X, i.e. in place).  Stream-ordered, no host sync."""
+    import ctypes
+
+    from . import _lib
+    out = X if out is None else out
+    for name, t in (("X", X), ("G", G), ("M", M), ("out", out)):
+        if t is None:
+            continue
+        if t.dtype.itemsize != 4 or not t.is_floating_point() or t.dim() != 2 or \
+                t.stride(1) != 1 or tuple(t.shape) != tuple(X.shape) or t.device != X.device:
+            raise ValueError(f"{name} must be a row-major float32 [N, P] tensor like X")
+    if momentum != 0.0 and M is None:
+        raise ValueError("momentum needs a buffer M")
+    args = _sgd_args(X, G, M, out, lr, momentum, dampening, weight_decay, nesterov, first)
+    _lib.check(_lib.load().dl_sgd_step(ctypes.byref(args), _lib.stream_handle(X.device)),
+               "dl_sgd_step")
+    return out
+
+
+def wrn_flops_per_image(depth=16, widen=4, num_classes=10, hw=32):
+    """Forward FLOPs of one image through Wide_ResNet (convs + linear, 2 per MAC), and the FLOPs of
+    forward + backward (input and weight gradients; the first conv needs no input gradient)."""
+    n = (depth - 4) // 6
+    st = [16, 16 * widen, 32 * widen, 64 * widen]
+    convs = [(3, st[0], 3, hw)]               # (cin, cout, k, output hw)
+    cin, h = st[0], hw
+    for i, s in enumerate([1, 2, 2]):
+        for j in range(n):
+            stride = s if j == 0 else 1
+            cout = st[i + 1]
+            ho = h // stride
+            convs.append((cin, cout, 3, h))           # conv1 (stride 1)
+            convs.append((cout, cout, 3, ho))         # conv2 (strided)
+            if stride != 1 or cin != cout:
+                convs.append((cin, cout, 1, ho))      # 1x1 shortcut
+            cin, h = cout, ho
+    fwd = [2 * ci * co * k * k * o * o for ci, co, k, o in convs] + [2 * st[3] * num_classes]
+    total = sum(fwd)
+    return total, total + 2 * total - fwd[0]
+
+
+class WRNConsensusSGD:
+    """Config c5 (BASELINE.json): every agent trains its own Wide-ResNet (WRN-16-4,
+    networks/wide_resnet.py) with the optimizer of Man_Colab.ipynb cell 19 (SGD, momentum 0.9,
+    weight decay 5e-4, lr 0.02) on its own CIFAR-shaped batch, and the agents mix after every
+    local step (the ``MasterNode`` loop the notebook drives, cells 21-23: local step, then
+    ``Mixer.mix``, mixer.py:18-49).
+
+    Layout: all agents' parameters are the rows of one row-major X[N, P] in HBM -- the Mixer's
+    flatten order (mixer.py:68-69) -- and every agent's ``nn.Module`` parameters are views of its
+    row; their ``.grad`` are views of G's rows, so backward accumulates straight into G.  One
+    ``step()``:
+      1. G = 0; per agent: forward, cross-entropy, backward (PyTorch-ROCm convs, MIOpen), agents
+         spread round-robin over ``streams`` HIP streams;
+      2. ``dl_sgd_step``: torch.optim.SGD's update (momentum buffers M), written to the scratch
+         S instead of in place;
+      3. ``dl_mix_round``: X <- W S with the fused disagreement -- the parameters land back in
+         X, so the module views never move and no copy or re-binding is needed.
+    Every call is stream-ordered: ``capture()`` records a step as one hipGraph."""
+
+    def __init__(self, csr, batch, depth=16, widen=4, dropout=0.0, num_classes=10, lr=0.02,
+                 momentum=0.9, weight_decay=5e-4, device="cuda", X0=None, seed=0, streams=1,
+                 deviation=True, data=None, labels=None):
+        import torch
+
+        from .engine import DeviceCsr, Workspace, plan_shape
+        from .networks.wide_resnet import Wide_ResNet
+        self._torch = torch
+        self.device = torch.device(device)
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        self.N, self.B = csr.n_rows, int(batch)
+        self.lr, self.momentum, self.wd = float(lr), float(momentum), float(weight_decay)
+        self.deviation = bool(deviation)
+        self.arch = (int(depth), int(widen), float(dropout), int(num_classes))
+        self.models = []
+        with torch.random.fork_rng(devices=[]):     # default torch init, agent a seeded seed + a
+            for a in range(self.N):
+                torch.manual_seed(seed + a)
+                self.models.append(Wide_ResNet(*self.arch).to(self.device))
+        shapes = [p.shape for p in self.models[0].parameters()]
+        self.P = sum(int(np.prod(s)) for s in shapes)
+        self.W = DeviceCsr(csr, self.device)
+        T = plan_shape(self.W, self.P, deviation=True)["tile_cols"] or 1
+        self.ld = -(-self.P // max(T, 16)) * max(T, 16)   # zero padding: no ragged tail launch
+        f = lambda: torch.zeros(self.N, self.ld, dtype=torch.float32, device=self.device)  # noqa
+        self.X, self.S, self.G = f(), f(), f()
+        self.M = f() if self.momentum != 0.0 else None
+        with torch.no_grad():
+            for a, m in enumerate(self.models):
+                if X0 is None:
+                    self.X[a, :self.P] = torch.cat([p.detach().reshape(-1) for p in m.parameters()])
+                else:
+                    self.X[a, :self.P] = torch.as_tensor(X0[a], dtype=torch.float32)
+                off = 0
+                for p in m.parameters():
+                    n = p.numel()
+                    p.set_(self.X[a, off:off + n].view_as(p))
+                    p.grad = self.G[a, off:off + n].view_as(p)
+                    off += n
+        self.dev_sq = torch.zeros(self.N, dtype=torch.float32, device=self.device)
+        self.dev_max = torch.zeros(1, dtype=torch.float32, device=self.device)
+        self.loss = torch.zeros(self.N, dtype=torch.float32, device=self.device)
+        self.ws = Workspace(self.device)
+        if data is None:
+            g = torch.Generator(device=self.device).manual_seed(seed)
+            data = torch.randn(self.N, self.B, 3, 32, 32, device=self.device, generator=g)
+            labels = torch.randint(0, num_classes, (self.N, self.B), device=self.device,
+                                   generator=g)
+        self.data, self.labels = data, labels
+        self.n_streams = max(1, int(streams))
+        self.streams = [torch.cuda.Stream(self.device) for _ in range(self.n_streams)] \
+            if self.n_streams > 1 else []
+        self.steps_done = 0
+        self.graph = None
+
+    def params(self):
+        """Row-major [N, P] view of every agent's flattened parameters (Mixer order)."""
+        return self.X[:, :self.P]
+
+    def flops_per_step(self):
+        return wrn_flops_per_image(self.arch[0], self.arch[1], self.arch[3])[1] * self.N * self.B
+
+    def _local_grads(self):
+        torch = self._torch
+        F = torch.nn.functional
+        self.G.zero_()
+        main = torch.cuda.current_stream(self.device)
+        for s in self.streams:
+            s.wait_stream(main)
+        for a, m in enumerate(self.models):
+            ctx = torch.cuda.stream(self.streams[a % self.n_streams]) if self.streams else \
+                _nullctx()
+            with ctx:
+                loss = F.cross_entropy(m(self.data[a]), self.labels[a])
+                loss.backward()
+                self.loss[a:a + 1].copy_(loss.detach().reshape(1))
+        for s in self.streams:
+            main.wait_stream(s)
+
+    def _round(self, first):
+        from .engine import mix_round
+        sgd_step(self.X, self.G, self.M, out=self.S, lr=self.lr, momentum=self.momentum,
+                 weight_decay=self.wd, first=first)
+        mix_round(self.W, self.S, self.X, dev_sq=self.dev_sq if self.deviation else None,
+                  dev_max=self.dev_max if self.deviation else None, workspace=self.ws)
+
+    def step(self):
+        self._local_grads()
+        self._round(first=self.steps_done == 0)
+        self.steps_done += 1
+
+    def capture(self):
+        """Record one step (after at least one eager step: the momentum buffers exist and every
+        MIOpen solution is found) as a hipGraph.  Runs nothing."""
+        torch = self._torch
+        if self.steps_done == 0:
+            raise RuntimeError("run one eager step before capture()")
+        from . import _lib
+        self.ws.get(_lib.load().dl_mix_workspace_bytes(self.N, 0, self.ld))
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._local_grads()
+            self._round(first=False)
+        self.graph = g
+
+    def replay(self, steps=1):
+        for _ in range(int(steps)):
+            self.graph.replay()
+            self.steps_done += 1
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False

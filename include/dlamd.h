@@ -151,6 +151,28 @@ int dl_step_rows(const float *x, int64_t ldx, const float *g, int64_t ldg, float
                  const int32_t *rows, int32_t n_sel, int64_t n_params, float *out, int64_t ldo,
                  dl_stream_t stream);
 
+/* Local optimizer step of config c5 (Man_Colab.ipynb cell 19: optimizer = optim.SGD,
+ * {'momentum': 0.9, 'weight_decay': 5e-4}, lr 0.02), i.e. torch.optim.SGD.step (torch/optim/sgd.py,
+ * single-tensor form) applied to every agent row at once, with torch's rounding (one fma per
+ * add-with-alpha):
+ *   d = g + wd*x;  buf = first ? d : mu*buf + (1-dampening)*d;  d = nesterov ? d + mu*buf : buf;
+ *   out = x - lr*d
+ * out may be x itself (in place, as optimizer.step) or a separate buffer, e.g. the input of the
+ * following dl_mix_round (the parameters stay put and the round writes them back).  buf
+ * (momentum buffer) is read unless `first` and always written when momentum != 0. */
+typedef struct dl_sgd_args {
+    const float *x; int64_t ldx;    /* [n_rows, ldx] parameters */
+    const float *g; int64_t ldg;    /* [n_rows, ldg] gradients */
+    float *buf; int64_t ldb;        /* [n_rows, ldb] momentum buffers (nullable if momentum == 0) */
+    float *out; int64_t ldo;        /* [n_rows, ldo] stepped parameters (== x or disjoint) */
+    int32_t n_rows;
+    int64_t n_params;
+    float lr, momentum, dampening, weight_decay;
+    int32_t nesterov;
+    int32_t first;                  /* 1: buf = d (torch's first step: clone of the gradient) */
+} dl_sgd_args;
+int dl_sgd_step(const dl_sgd_args *args, dl_stream_t stream);
+
 /* dst[i] = src[i] for n_floats floats (float4 streaming copy; variant 0: one load in flight
  * per thread, 1: eight, 2: eight + non-temporal stores, 3: four + non-temporal loads and
  * stores on a 8192-workgroup grid).  Variants 4 and 5 are the triad

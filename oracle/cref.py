@@ -28,6 +28,9 @@ def lib():
         L.ref_column_mean.restype = None
         L.ref_deviation_sq.argtypes = [P, i64, i32, i64, P, P]
         L.ref_deviation_sq.restype = None
+        L.ref_sgd_step.argtypes = [P, i64, P, i64, P, i64, P, i64, i32, i64, f32, f32, f32, f32,
+                                   i32, i32]
+        L.ref_sgd_step.restype = None
         _lib = L
     return _lib
 
@@ -67,3 +70,19 @@ def deviation_sq(X, mean=None):
     d = np.empty(X.shape[0], np.float64)
     lib().ref_deviation_sq(_p(X), X.shape[1], X.shape[0], X.shape[1], _p(mean), _p(d))
     return d
+
+
+def sgd_step(X, G, buf=None, lr=0.1, momentum=0.0, dampening=0.0, weight_decay=0.0,
+             nesterov=False, first=False):
+    """C restatement of torch.optim.SGD.step over agent rows.  Returns the stepped X; ``buf`` is
+    updated in place (a new zero buffer when None and momentum != 0)."""
+    X = np.ascontiguousarray(X, np.float32)
+    G = np.ascontiguousarray(G, np.float32)
+    n, p = X.shape
+    if momentum != 0.0 and buf is None:
+        buf = np.zeros_like(X)
+    out = np.empty_like(X)
+    lib().ref_sgd_step(_p(X), p, _p(G), p, _p(buf), p, _p(out), p, n, p, float(lr),
+                       float(momentum), float(dampening), float(weight_decay), int(nesterov),
+                       int(first))
+    return out

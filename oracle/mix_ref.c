@@ -69,3 +69,30 @@ void ref_deviation_sq(const float *x, int64_t ldx, int32_t n_rows, int64_t n_par
         dev_sq[a] = s;
     }
 }
+
+/* torch.optim.SGD.step (torch/optim/sgd.py, single-tensor form) on an [n_rows, n_params] block,
+ * restated with explicit fmaf for each of torch's add-with-alpha (ATen's add kernels compute
+ * a + alpha*b as one fused multiply-add) -- the local step of config c5 (Man_Colab.ipynb cell 19).
+ *   d = g + wd*x;  buf = first ? d : mu*buf + (1-damp)*d;  d = nesterov ? d + mu*buf : buf;
+ *   out = x - lr*d      (buf may be NULL when mu == 0; out may alias x) */
+void ref_sgd_step(const float *x, int64_t ldx, const float *g, int64_t ldg, float *buf,
+                  int64_t ldb, float *out, int64_t ldo, int32_t n_rows, int64_t n_params,
+                  float lr, float mu, float damp, float wd, int32_t nesterov, int32_t first) {
+    for (int32_t r = 0; r < n_rows; ++r)
+        for (int64_t p = 0; p < n_params; ++p) {
+            const float xv = x[r * ldx + p];
+            float d = g[r * ldg + p];
+            if (wd != 0.0f) d = fmaf(wd, xv, d);
+            if (mu != 0.0f) {
+                float *b = buf + r * ldb + p;
+                if (first) {
+                    *b = d;
+                } else {
+                    const float m = mu * *b;
+                    *b = fmaf(1.0f - damp, d, m);
+                }
+                d = nesterov ? fmaf(mu, *b, d) : *b;
+            }
+            out[r * ldo + p] = fmaf(-lr, d, xv);
+        }
+}

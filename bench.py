@@ -52,7 +52,7 @@ def parse():
                    help="columns of the bounded CPU-baseline sample (all agents)")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-graph", action="store_true", help="c3/c5: eager launches, no hipGraph")
-    p.add_argument("--streams", type=int, default=1, help="c5: HIP streams the agents share")
+    p.add_argument("--streams", type=int, default=8, help="c5: HIP streams the agents share")
     p.add_argument("--batch", type=int, default=64, help="c5: images per agent per step")
     p.add_argument("--dist-backend", default="nccl",
                    help="nccl (= RCCL, default) or gloo (multi-rank rehearsal on one GPU)")

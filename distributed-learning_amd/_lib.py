@@ -62,6 +62,12 @@ class DlSgdArgs(ctypes.Structure):
                 ("nesterov", _i32), ("first", _i32)]
 
 
+class DlMlpArgs(ctypes.Structure):
+    _fields_ = [("n_agents", _i32), ("batch", _i32), ("input_dim", _i32), ("hidden_dim", _i32),
+                ("output_dim", _i32), ("X", _vp), ("ldx", _i64), ("data", _vp), ("s_data", _i64),
+                ("labels", _vp), ("s_labels", _i64), ("G", _vp), ("ldg", _i64), ("loss", _vp)]
+
+
 EPI = {"none": 0, "bias": 1, "bias_relu": 2, "bias_tanh": 3, "bias_elu": 4, "drelu": 5,
        "dtanh": 6, "delu": 7, "bias_xent": 8}
 
@@ -84,6 +90,7 @@ SIGNATURES = {
     "dl_step_rows": (_i32, [_vp, _i64, _vp, _i64, _f32, _vp, _i32, _i64, _vp, _i64, _vp]),
     "dl_stream_copy": (_i32, [_vp, _vp, _i64, _i32, _vp]),
     "dl_sgd_step": (_i32, [ctypes.POINTER(DlSgdArgs), _vp]),
+    "dl_mlp_grad": (_i32, [ctypes.POINTER(DlMlpArgs), _vp]),
     "dl_bgemm": (_i32, [ctypes.POINTER(DlBgemmArgs), _vp]),
     "dl_xent_grad": (_i32, [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i32, _i32, _i32, _vp]),
     "dl_perron_workspace_bytes": (_sz, [_i32, _i32, _i64]),

@@ -1,0 +1,475 @@
+// Fused per-agent ANNModel gradients (BASELINE config c3) on fp32 MFMA, one workgroup per agent.
+//
+// The reference trains every agent's ANNModel (networks/ann_model.py:4-45: 784 -> 150 ReLU ->
+// 150 Tanh -> 150 ELU -> 10, torch.nn.CrossEntropyLoss) with its own autograd pass.  The layered
+// path (bgemm.hip) runs that as 11 batched GEMM launches; each is a small GEMM (64 batch rows)
+// whose per-slice global->LDS latency, not the matrix cores, sets its time.  Here one 512-thread
+// workgroup runs an agent's whole forward + cross-entropy + backward:
+//   * the three 64 x 150 activations stay in LDS for the whole pass (3 x 39 KiB), and the
+//     backward overwrites each in place with its dZ once its weight gradient is done;
+//   * only the agent's parameter row of X, its input batch (read twice) and its gradient row of
+//     G touch HBM: ~1.7 MB per agent, every byte once;
+//   * weights stream through one LDS staging area (global loads for slice s+1 in registers while
+//     the MFMAs consume slice s);
+//   * weight gradients go from the MFMA accumulators straight into the agent's row of G (the
+//     Mixer flatten order, mixer.py:69), bias gradients are fixed-order column sums, and the
+//     per-agent loss is summed in a fixed order (deterministic, hipGraph-replay stable).
+// LDS strides are chosen per access so the MFMA fragment reads are bank-conflict free:
+//   [row][k] images read by 16 rows x 4 k   -> stride = 4 (mod 8)  floats  (36, 156)
+//   [k][col] images read by 16 cols x 4 k   -> stride = 16 (mod 32) floats (80, 176)
+// f32 MFMA (16x16x4) products are exact fp32 fma chains; summation order differs from
+// autograd's BLAS, so parity is a tolerance (tests/test_batched_ann_gpu.py).
+#include "dl_internal.h"
+
+namespace dl {
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int NTHR = 512;     // 8 waves, 2 per SIMD
+constexpr int MB = 64;        // batch rows per agent
+constexpr int LDH = 156;      // activation row stride: dh <= 152 columns + zero pad
+constexpr int BK = 32;        // K slice of the staged GEMMs
+constexpr int LDS1 = 36;      // [row][BK] slices
+constexpr int LDT = 176;      // [k][col] slices (cols <= 160)
+constexpr int LDX2 = 80;      // dW1: x chunk [64][64 (+16)]
+constexpr int LDZ = 17;       // logits / dZ4 [64][16 (+1)]
+constexpr int LDW4 = 156;     // W4 image [16][dh] for the logits
+
+constexpr int H_FLOATS = MB * LDH;                        // one activation buffer
+constexpr int STAGE_FLOATS = MB * LDS1 + 160 * LDS1;      // largest staging use (layer 1)
+constexpr int Z_FLOATS = MB * LDZ;
+constexpr int LDS_FLOATS = 3 * H_FLOATS + STAGE_FLOATS + Z_FLOATS + 16;
+static_assert(160 * LDS1 + MB * LDS1 >= 32 * LDT, "staging area holds a [32][176] slice");
+static_assert(160 * LDS1 + MB * LDS1 >= MB * LDX2, "staging area holds a dW1 x chunk");
+static_assert(160 * LDS1 + MB * LDS1 >= 16 * LDW4, "staging area holds W4");
+static_assert(LDS_FLOATS * 4 <= kLdsBytes, "fits one CU's LDS");
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ int round4(int v) { return (v + 3) & ~3; }
+
+// ---------------------------------------------------------------- staging (global -> LDS)
+// rows x BK slice of a row-major [rows][ld] matrix, columns [k0, k0 + BK), zero outside
+// [0, n_rows) x [0, K), into S[r * LDS1 + c].  Register-prefetched: load() then store().
+template <int ROWS>
+struct RowSlice {
+    static constexpr int PER = (ROWS * BK + NTHR - 1) / NTHR;
+    float v[PER];
+    __device__ __forceinline__ void load(const float *W, int64_t ld, int n_rows, int K, int k0) {
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int e = threadIdx.x + i * NTHR;
+            const int r = e / BK, c = e % BK;
+            v[i] = (e < ROWS * BK && r < n_rows && k0 + c < K) ? W[(int64_t)r * ld + k0 + c] : 0.f;
+        }
+    }
+    __device__ __forceinline__ void store(float *S) const {
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int e = threadIdx.x + i * NTHR;
+            if (e < ROWS * BK) S[(e / BK) * LDS1 + e % BK] = v[i];
+        }
+    }
+};
+
+// float4 form for 16-byte aligned rows (layer 1: x and W1 with din % 4 == 0)
+template <int ROWS>
+struct RowSlice4 {
+    static constexpr int Q = BK / 4;
+    static constexpr int PER = (ROWS * Q + NTHR - 1) / NTHR;
+    f32x4 v[PER];
+    __device__ __forceinline__ void load(const float *W, int64_t ld, int n_rows, int K, int k0) {
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int e = threadIdx.x + i * NTHR;
+            const int r = e / Q, c = 4 * (e % Q);
+            v[i] = (e < ROWS * Q && r < n_rows && k0 + c < K)
+                       ? *reinterpret_cast<const f32x4 *>(W + (int64_t)r * ld + k0 + c)
+                       : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+    }
+    __device__ __forceinline__ void store(float *S) const {
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int e = threadIdx.x + i * NTHR;
+            if (e < ROWS * Q) *reinterpret_cast<f32x4 *>(S + (e / Q) * LDS1 + 4 * (e % Q)) = v[i];
+        }
+    }
+};
+
+// BK rows [k0, k0 + BK) of a row-major [K][ld] matrix, columns [0, n_cols), zero outside, into
+// S[kl * LDT + n] (cols < 160)
+struct ColSlice {
+    static constexpr int PER = BK * 160 / NTHR;  // 10
+    float v[PER];
+    __device__ __forceinline__ void load(const float *W, int64_t ld, int n_cols, int K, int k0) {
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int e = threadIdx.x + i * NTHR;
+            const int kl = e / 160, n = e % 160;
+            v[i] = (n < n_cols && k0 + kl < K) ? W[(int64_t)(k0 + kl) * ld + n] : 0.f;
+        }
+    }
+    __device__ __forceinline__ void store(float *S) const {
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int e = threadIdx.x + i * NTHR;
+            S[(e / 160) * LDT + e % 160] = v[i];
+        }
+    }
+};
+
+__device__ __forceinline__ float act_fwd(int layer, float z) {
+    if (layer == 0) return z > 0.f ? z : 0.f;   // ReLU
+    if (layer == 1) return tanhf(z);            // Tanh
+    return z > 0.f ? z : expm1f(z);             // ELU(alpha = 1)
+}
+// derivative through the layer's OUTPUT h (what the forward kept)
+__device__ __forceinline__ float act_grad(int layer, float h) {
+    if (layer == 0) return h > 0.f ? 1.f : 0.f;
+    if (layer == 1) return 1.f - h * h;
+    return h > 0.f ? 1.f : h + 1.f;
+}
+
+// ------------------------------------------------------------- [64 x 160] output GEMM tiles
+// wave w owns M-tile (w & 3) and the five N-tiles 5 * (w >> 2) + t.  acc = sum_k A(m,k) B(n,k)
+// with A(m, k) = Alds[m * lda + k] and B(n, k) = Blds[n * LDS1 + k] (staged [n][k] slice) or
+// Blds[k * LDT + n] (staged [k][n] slice).
+template <bool B_KMAJOR>
+__device__ __forceinline__ void mma_rows64(f32x4 (&acc)[5], const float *A, int lda,
+                                           const float *Bs, int kn) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int m = (wave & 3) * 16 + (lane & 15);
+    const int n0 = (wave >> 2) * 80 + (lane & 15);
+    for (int kk = 0; kk < kn; kk += 4) {
+        const int k = kk + (lane >> 4);
+        const float a = A[m * lda + k];
+#pragma unroll
+        for (int t = 0; t < 5; ++t) {
+            const int n = n0 + 16 * t;
+            const float b = B_KMAJOR ? Bs[k * LDT + n] : Bs[n * LDS1 + k];
+            acc[t] = mfma4(a, b, acc[t]);
+        }
+    }
+}
+
+__device__ __forceinline__ void zero(f32x4 (&acc)[5]) {
+#pragma unroll
+    for (int t = 0; t < 5; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+}
+
+// C/D fragment -> (row, col) of the [64 x 160] output: row = 16 (w & 3) + 4 (lane >> 4) + r,
+// col = 80 (w >> 2) + 16 t + (lane & 15)
+template <typename F>
+__device__ __forceinline__ void epi_rows64(const f32x4 (&acc)[5], F f) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int t = 0; t < 5; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            f((wave & 3) * 16 + 4 * (lane >> 4) + r, (wave >> 2) * 80 + 16 * t + (lane & 15),
+              acc[t][r]);
+}
+
+// Forward layer on an LDS-resident input: H = act(Hin W^T + b), K = N = dh, W staged by slices.
+__device__ void forward_hidden(const float *W, const float *bias, int dh, const float *Hin,
+                               float *Hout, float *stage, int layer) {
+    f32x4 acc[5];
+    zero(acc);
+    RowSlice<160> ws;
+    const int ns = (dh + BK - 1) / BK;
+    ws.load(W, dh, dh, dh, 0);
+    for (int s = 0; s < ns; ++s) {
+        ws.store(stage);
+        __syncthreads();
+        if (s + 1 < ns) ws.load(W, dh, dh, dh, (s + 1) * BK);
+        const int k0 = s * BK;
+        mma_rows64<false>(acc, Hin + k0, LDH, stage, round4(min(BK, dh - k0)));
+        __syncthreads();
+    }
+    epi_rows64(acc, [&](int m, int n, float v) {
+        if (n < dh) Hout[m * LDH + n] = act_fwd(layer, v + bias[n]);
+    });
+}
+
+// Backward through a hidden layer: Hio <- (dZ W) * act'(Hio)  (in place), K = dk rows of W.
+__device__ void backward_dz(const float *W, int dk, int dh, const float *dZ, int ldz, float *Hio,
+                            float *stage, int layer) {
+    f32x4 acc[5];
+    zero(acc);
+    ColSlice ws;
+    const int ns = (dk + BK - 1) / BK;
+    ws.load(W, dh, dh, dk, 0);
+    for (int s = 0; s < ns; ++s) {
+        ws.store(stage);
+        __syncthreads();
+        if (s + 1 < ns) ws.load(W, dh, dh, dk, (s + 1) * BK);
+        const int k0 = s * BK;
+        mma_rows64<true>(acc, dZ + k0, ldz, stage, round4(min(BK, dk - k0)));
+        __syncthreads();
+    }
+    epi_rows64(acc, [&](int m, int n, float v) {
+        if (n < dh) Hio[m * LDH + n] = v * act_grad(layer, Hio[m * LDH + n]);
+    });
+}
+
+// Weight gradient of a hidden layer: dW[i][j] = sum_b dZ[b][i] Hin[b][j] (both LDS-resident,
+// [64][LDH]), i, j < dh, straight into G; bias gradient db[i] = sum_b dZ[b][i] in order.
+// 100 tiles (10 x 10 of 16 x 16) over 8 waves, 13 consecutive tiles per wave.
+__device__ void weight_grad_hidden(const float *dZ, const float *Hin, int dh, float *gW,
+                                   float *gb) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    constexpr int TPW = 13;
+    f32x4 acc[TPW];
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int t0 = wave * TPW;
+    for (int kk = 0; kk < MB; kk += 4) {
+        const int b = kk + (lane >> 4);
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) {
+            const int tile = t0 + t;
+            if (tile < 100) {
+                const float a = dZ[b * LDH + (tile / 10) * 16 + (lane & 15)];
+                const float bb = Hin[b * LDH + (tile % 10) * 16 + (lane & 15)];
+                acc[t] = mfma4(a, bb, acc[t]);
+            }
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+        const int tile = t0 + t;
+        if (tile >= 100) continue;
+        const int j = (tile % 10) * 16 + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = (tile / 10) * 16 + 4 * (lane >> 4) + r;
+            if (i < dh && j < dh) gW[(int64_t)i * dh + j] = acc[t][r];
+        }
+    }
+    if (threadIdx.x < dh) {
+        float s = 0.f;
+        for (int b = 0; b < MB; ++b) s += dZ[b * LDH + threadIdx.x];
+        gb[threadIdx.x] = s;
+    }
+}
+
+struct MlpArgs {
+    const float *X;
+    int64_t ldx;
+    const float *data;
+    int64_t s_data;
+    const int32_t *labels;
+    int64_t s_lab;
+    float *G;
+    int64_t ldg;
+    float *loss;
+    int32_t din, dh, dout;
+};
+
+__global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    float *H1 = lds, *H2 = lds + H_FLOATS, *H3 = lds + 2 * H_FLOATS;
+    float *stage = lds + 3 * H_FLOATS;
+    float *Zs = stage + STAGE_FLOATS;
+    float *lpart = Zs + Z_FLOATS;
+    const int a = blockIdx.x;
+    const int din = p.din, dh = p.dh, dout = p.dout;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const float *Xa = p.X + (int64_t)a * p.ldx;
+    float *Ga = p.G + (int64_t)a * p.ldg;
+    const float *x = p.data + (int64_t)a * p.s_data;
+    // parameter offsets in the Mixer flatten order (fc1.w, fc1.b, fc2.w, fc2.b, ...)
+    const int64_t o_w1 = 0, o_b1 = (int64_t)dh * din, o_w2 = o_b1 + dh, o_b2 = o_w2 + dh * dh,
+                  o_w3 = o_b2 + dh, o_b3 = o_w3 + dh * dh, o_w4 = o_b3 + dh,
+                  o_b4 = o_w4 + dout * dh;
+
+    // zero the activation pads (columns dh..LDH) and the logits image: K tails read them
+    for (int e = tid; e < 3 * MB * (LDH - dh); e += NTHR) {
+        const int buf = e / (MB * (LDH - dh)), r = e % (MB * (LDH - dh));
+        lds[buf * H_FLOATS + (r / (LDH - dh)) * LDH + dh + r % (LDH - dh)] = 0.f;
+    }
+    for (int e = tid; e < Z_FLOATS; e += NTHR) Zs[e] = 0.f;
+
+    // ---- layer 1: H1 = relu(x W1^T + b1), K = din from HBM, x and W1 slices register-prefetched
+    {
+        f32x4 acc[5];
+        zero(acc);
+        float *xs = stage, *ws = stage + MB * LDS1;
+        RowSlice4<MB> xr;
+        RowSlice4<160> wr;
+        const int ns = (din + BK - 1) / BK;
+        xr.load(x, din, MB, din, 0);
+        wr.load(Xa + o_w1, din, dh, din, 0);
+        for (int s = 0; s < ns; ++s) {
+            xr.store(xs);
+            wr.store(ws);
+            __syncthreads();
+            if (s + 1 < ns) {
+                xr.load(x, din, MB, din, (s + 1) * BK);
+                wr.load(Xa + o_w1, din, dh, din, (s + 1) * BK);
+            }
+            mma_rows64<false>(acc, xs, LDS1, ws, round4(min(BK, din - s * BK)));
+            __syncthreads();
+        }
+        const float *b1 = Xa + o_b1;
+        epi_rows64(acc, [&](int m, int n, float v) {
+            if (n < dh) H1[m * LDH + n] = act_fwd(0, v + b1[n]);
+        });
+    }
+    __syncthreads();
+    forward_hidden(Xa + o_w2, Xa + o_b2, dh, H1, H2, stage, 1);
+    __syncthreads();
+    forward_hidden(Xa + o_w3, Xa + o_b3, dh, H2, H3, stage, 2);
+    // ---- logits Z = H3 W4^T + b4 (waves 0-3, one 16 x 16 tile each), W4 image [16][LDW4]
+    for (int e = tid; e < 16 * LDW4; e += NTHR) {
+        const int n = e / LDW4, k = e % LDW4;
+        stage[e] = (n < dout && k < dh) ? Xa[o_w4 + (int64_t)n * dh + k] : 0.f;
+    }
+    __syncthreads();
+    if (wave < 4) {
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        const int m = wave * 16 + (lane & 15);
+        for (int kk = 0; kk < round4(dh); kk += 4) {
+            const int k = kk + (lane >> 4);
+            acc = mfma4(H3[m * LDH + k], stage[(lane & 15) * LDW4 + k], acc);
+        }
+        const int n = lane & 15;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            if (n < dout) Zs[(wave * 16 + 4 * (lane >> 4) + r) * LDZ + n] = acc[r] + Xa[o_b4 + n];
+    }
+    __syncthreads();
+    // ---- cross-entropy head (torch.nn.CrossEntropyLoss, mean): dZ4 = (softmax - onehot) / 64
+    {
+        float lsum = 0.f;
+        for (int m = wave; m < MB; m += 8) {
+            const float v = lane < dout ? Zs[m * LDZ + lane] : 0.f;
+            float mx = lane < dout ? v : -INFINITY;
+            for (int s = 32; s >= 1; s >>= 1) mx = fmaxf(mx, __shfl_xor(mx, s));
+            const float e = lane < dout ? expf(v - mx) : 0.f;
+            float sum = e;
+            for (int s = 32; s >= 1; s >>= 1) sum += __shfl_xor(sum, s);
+            const int label = p.labels[(int64_t)a * p.s_lab + m];
+            const float zl = __shfl(v, label);
+            if (lane < dout) Zs[m * LDZ + lane] = (e / sum - (lane == label ? 1.f : 0.f)) / (float)MB;
+            lsum += (logf(sum) + mx - zl) / (float)MB;
+        }
+        if (lane == 0) lpart[wave] = lsum;
+    }
+    __syncthreads();
+    if (tid == 0 && p.loss)
+        p.loss[a] = ((lpart[0] + lpart[1]) + (lpart[2] + lpart[3])) +
+                    ((lpart[4] + lpart[5]) + (lpart[6] + lpart[7]));
+    // ---- dW4 = dZ4^T H3 [dout x dh] (one M-tile, N-tiles w and w + 8), db4
+    {
+        for (int nt = wave; nt < 10; nt += 8) {
+            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+            for (int kk = 0; kk < MB; kk += 4) {
+                const int b = kk + (lane >> 4);
+                acc = mfma4(Zs[b * LDZ + (lane & 15)], H3[b * LDH + nt * 16 + (lane & 15)], acc);
+            }
+            const int j = nt * 16 + (lane & 15);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = 4 * (lane >> 4) + r;
+                if (i < dout && j < dh) Ga[o_w4 + (int64_t)i * dh + j] = acc[r];
+            }
+        }
+        if (tid < dout) {
+            float s = 0.f;
+            for (int b = 0; b < MB; ++b) s += Zs[b * LDZ + tid];
+            Ga[o_b4 + tid] = s;
+        }
+    }
+    __syncthreads();
+    // ---- dZ3 = (dZ4 W4) * elu'(H3) in place, K = dout
+    backward_dz(Xa + o_w4, dout, dh, Zs, LDZ, H3, stage, 2);
+    __syncthreads();
+    weight_grad_hidden(H3, H2, dh, Ga + o_w3, Ga + o_b3);
+    __syncthreads();
+    backward_dz(Xa + o_w3, dh, dh, H3, LDH, H2, stage, 1);     // dZ2 into H2
+    __syncthreads();
+    weight_grad_hidden(H2, H1, dh, Ga + o_w2, Ga + o_b2);
+    __syncthreads();
+    backward_dz(Xa + o_w2, dh, dh, H2, LDH, H1, stage, 0);     // dZ1 into H1
+    __syncthreads();
+    // ---- dW1 = dZ1^T x [dh x din] by 64-column chunks of x; db1
+    {
+        float *xs = stage;
+        constexpr int PER = MB * 16 / NTHR;   // float4s of a [64][64] chunk per thread
+        f32x4 xv[PER];
+        auto load = [&](int c0) {
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                const int e = tid + i * NTHR;
+                const int b = e / 16, c = 4 * (e % 16);
+                xv[i] = c0 + c < din ? *reinterpret_cast<const f32x4 *>(x + (int64_t)b * din + c0 + c)
+                                     : f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+        };
+        const int nc = (din + 63) / 64;
+        load(0);
+        for (int ci = 0; ci < nc; ++ci) {
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                const int e = tid + i * NTHR;
+                *reinterpret_cast<f32x4 *>(xs + (e / 16) * LDX2 + 4 * (e % 16)) = xv[i];
+            }
+            __syncthreads();
+            const int c0 = ci * 64;
+            if (ci + 1 < nc) load(c0 + 64);
+            // wave w: N-tile (w & 3) of the chunk, M-tiles 5 (w >> 2) + t
+            f32x4 acc[5];
+            zero(acc);
+            const int nl = (wave & 3) * 16 + (lane & 15);
+            if (c0 + (wave & 3) * 16 < din) {
+                for (int kk = 0; kk < MB; kk += 4) {
+                    const int b = kk + (lane >> 4);
+                    const float bv = xs[b * LDX2 + nl];
+#pragma unroll
+                    for (int t = 0; t < 5; ++t)
+                        acc[t] = mfma4(H1[b * LDH + ((wave >> 2) * 5 + t) * 16 + (lane & 15)], bv,
+                                       acc[t]);
+                }
+#pragma unroll
+                for (int t = 0; t < 5; ++t)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int i = ((wave >> 2) * 5 + t) * 16 + 4 * (lane >> 4) + r;
+                        if (i < dh && c0 + nl < din)
+                            Ga[o_w1 + (int64_t)i * din + c0 + nl] = acc[t][r];
+                    }
+            }
+            __syncthreads();
+        }
+        if (tid < dh) {
+            float s = 0.f;
+            for (int b = 0; b < MB; ++b) s += H1[b * LDH + tid];
+            Ga[o_b1 + tid] = s;
+        }
+    }
+}
+
+}  // namespace
+
+int mlp_fused_supported(int batch, int din, int dh, int dout) {
+    return batch == MB && din > 0 && din % 4 == 0 && dh > 0 && dh <= 152 && dout > 0 &&
+           dout <= 16;
+}
+
+hipError_t launch_mlp_fused(const float *X, int64_t ldx, const float *data, int64_t s_data,
+                            const int32_t *labels, int64_t s_lab, float *G, int64_t ldg,
+                            float *loss, int n_agents, int din, int dh, int dout, hipStream_t s) {
+    hipError_t e = allow_full_lds(reinterpret_cast<const void *>(mlp_fused_kernel));
+    if (e != hipSuccess) return e;
+    MlpArgs p{X, ldx, data, s_data, labels, s_lab, G, ldg, loss, din, dh, dout};
+    hipLaunchKernelGGL(mlp_fused_kernel, dim3((unsigned)n_agents), dim3(NTHR),
+                       LDS_FLOATS * sizeof(float), s, p);
+    return hipGetLastError();
+}
+
+}  // namespace dl

@@ -18,9 +18,18 @@ from .. import _lib
 from .ann_model import ANNModel
 
 
+def fused_supported(batch, input_dim, hidden_dim, output_dim):
+    """Shapes the one-launch kernel (dl_mlp_grad, csrc/mlp_fused.hip) covers."""
+    return batch == 64 and input_dim % 4 == 0 and 0 < hidden_dim <= 152 and 0 < output_dim <= 16
+
+
 class BatchedANN:
+    """path: "fused" (one dl_mlp_grad launch per step: every agent's forward + loss + backward in
+    one workgroup, activations in LDS), "layers" (11 dl_bgemm launches) or "auto" (fused when the
+    shapes allow it)."""
+
     def __init__(self, n_agents, batch, input_dim=784, hidden_dim=150, output_dim=10,
-                 device="cuda"):
+                 device="cuda", path="auto"):
         self.N, self.B = int(n_agents), int(batch)
         self.din, self.dh, self.dout = int(input_dim), int(hidden_dim), int(output_dim)
         if self.dout > 64:
@@ -38,6 +47,12 @@ class BatchedANN:
         self.dZ4 = f(self.N, self.B, self.dout)
         self.dZa, self.dZb = f(self.N, self.B, self.dh), f(self.N, self.B, self.dh)
         self.loss = f(self.N)
+        ok = fused_supported(self.B, self.din, self.dh, self.dout)
+        if path not in ("auto", "fused", "layers"):
+            raise ValueError(f"unknown path {path!r}")
+        if path == "fused" and not ok:
+            raise ValueError("these shapes are not covered by the fused kernel")
+        self.path = "fused" if (path == "auto" and ok) else ("layers" if path == "auto" else path)
 
     # -------------------------------------------------------------- helpers
     def _gemm(self, M, N, K, A, lda, sA, ta, B, ldb, sB, tb, C, ldc, sC, epi="none", bias=None,
@@ -70,6 +85,18 @@ class BatchedANN:
             raise ValueError(f"data must be contiguous [{N}, {B}, {din}] fp32")
         if tuple(labels.shape) != (N, B) or labels.dtype != torch.int32:
             raise ValueError(f"labels must be int32 [{N}, {B}]")
+        aligned = all(t.data_ptr() % 16 == 0 for t in (X, G, data)) and \
+            X.stride(0) % 4 == 0 and G.stride(0) % 4 == 0
+        if self.path == "fused" and not aligned:
+            raise ValueError("the fused kernel needs 16-byte aligned X, G, data with row strides "
+                             "% 4 == 0 (pad the parameter rows)")
+        if self.path == "fused":
+            args = _lib.DlMlpArgs(N, B, din, dh, dout, _lib.ptr(X), X.stride(0), _lib.ptr(data),
+                                  B * din, _lib.ptr(labels), labels.stride(0), _lib.ptr(G),
+                                  G.stride(0), _lib.ptr(self.loss))
+            _lib.check(lib.dl_mlp_grad(ctypes.byref(args), _lib.stream_handle(self.device)),
+                       "dl_mlp_grad")
+            return self.loss
         sx, sg = X.stride(0), G.stride(0)
         o = self.offsets
         hs = B * dh

@@ -254,6 +254,28 @@ int dl_bgemm(const dl_bgemm_args *args, dl_stream_t stream);
 int dl_xent_grad(const float *Z, int64_t sZ, const int32_t *y, int64_t sY, float *dZ, int64_t sD,
                  float *loss, int32_t batch, int32_t rows, int32_t classes, dl_stream_t stream);
 
+/* Whole-model per-agent gradients of ANNModel (networks/ann_model.py:4-45) in ONE launch: every
+ * agent's forward (Linear-ReLU-Linear-Tanh-Linear-ELU-Linear), torch.nn.CrossEntropyLoss (mean)
+ * and backward, one workgroup per agent with its activations resident in LDS.  Replaces the
+ * 11-launch dl_bgemm sequence for the shapes it supports (batch == 64, input_dim % 4 == 0,
+ * hidden_dim <= 152, output_dim <= 16); other shapes return DL_ERR_UNSUPPORTED and the caller
+ * uses dl_bgemm.
+ *   X [n_agents, ldx]: parameter rows in the Mixer flatten order (mixer.py:68-69: fc1.weight,
+ *     fc1.bias, fc2.weight, fc2.bias, fc3.weight, fc3.bias, fc4.weight, fc4.bias);
+ *   data [n_agents][batch][input_dim] (agent stride s_data), labels [n_agents][batch] int32 in
+ *     [0, output_dim);  G [n_agents, ldg]: receives d loss_a / d params_a (same order; columns
+ *     beyond the parameter count untouched);  loss nullable [n_agents]: mean cross-entropy.
+ * X, data and G 16-byte aligned, ldx, ldg and s_data multiples of 4, G disjoint from X. */
+typedef struct dl_mlp_args {
+    int32_t n_agents, batch, input_dim, hidden_dim, output_dim;
+    const float *X; int64_t ldx;
+    const float *data; int64_t s_data;
+    const int32_t *labels; int64_t s_labels;
+    float *G; int64_t ldg;
+    float *loss;
+} dl_mlp_args;
+int dl_mlp_grad(const dl_mlp_args *args, dl_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

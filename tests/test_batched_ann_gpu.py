@@ -11,20 +11,30 @@ def _flat_grads(m):
     return torch.cat([p.grad.reshape(-1) for p in m.parameters()])
 
 
-@pytest.mark.parametrize("n,b,dims", [(4, 64, (784, 150, 10)), (7, 33, (50, 40, 7)),
-                                      (3, 5, (20, 15, 3))])
-def test_gradients_match_autograd(cuda, n, b, dims):
+@pytest.mark.parametrize("n,b,dims,path", [(4, 64, (784, 150, 10), "layers"),
+                                           (4, 64, (784, 150, 10), "fused"),
+                                           (5, 64, (52, 40, 7), "fused"),
+                                           (3, 64, (16, 152, 16), "fused"),
+                                           (7, 33, (50, 40, 7), "auto"),
+                                           (3, 5, (20, 15, 3), "auto")])
+def test_gradients_match_autograd(cuda, n, b, dims, path):
     from distributed_learning_amd.networks import ANNModel
     from distributed_learning_amd.networks.batched_ann import BatchedANN
     din, dh, dout = dims
     torch.manual_seed(0)
     models = [ANNModel(din, dh, dout).to(cuda) for _ in range(n)]
-    X = torch.stack([torch.cat([p.data.reshape(-1) for p in m.parameters()]) for m in models])
+    X0 = torch.stack([torch.cat([p.data.reshape(-1) for p in m.parameters()]) for m in models])
+    P = X0.shape[1]
+    ld = -(-P // 64) * 64          # padded rows: 16-byte aligned, as the engine keeps them
+    X = torch.zeros(n, ld, device=cuda)[:, :P]
+    X.copy_(X0)
     data = torch.randn(n, b, din, device=cuda)
     labels = torch.randint(0, dout, (n, b), device=cuda, dtype=torch.int32)
-    bann = BatchedANN(n, b, din, dh, dout, device=cuda)
+    bann = BatchedANN(n, b, din, dh, dout, device=cuda, path=path)
+    assert bann.path == (path if path != "auto" else "layers")
     assert bann.P == X.shape[1]
-    G = torch.full_like(X, float("nan"))
+    Gbuf = torch.full((n, ld), float("nan"), device=cuda)
+    G = Gbuf[:, :P]
     loss = bann.gradients(X, data, labels, G).clone()
     torch.cuda.synchronize()
     for a, m in enumerate(models):
@@ -37,6 +47,7 @@ def test_gradients_match_autograd(cuda, n, b, dims):
         np.testing.assert_allclose(G[a].cpu().numpy(), ref.cpu().numpy(), rtol=1e-4,
                                    atol=1e-5 * scale)
         assert loss[a].item() == pytest.approx(ref_loss.item(), rel=1e-5)
+    assert torch.isnan(Gbuf[:, P:]).all()       # nothing written past the parameter columns
 
 
 def test_consensus_sgd_round_with_batched_grads(cuda):

@@ -9,14 +9,15 @@
 //     backward overwrites each in place with its dZ once its weight gradient is done;
 //   * only the agent's parameter row of X, its input batch (read twice) and its gradient row of
 //     G touch HBM: ~1.7 MB per agent, every byte once;
-//   * weights stream through one LDS staging area (global loads for slice s+1 in registers while
-//     the MFMAs consume slice s);
+//   * weights stream through one LDS staging area, two slices ahead in registers while the
+//     MFMAs consume the current one (pipeline2);
 //   * weight gradients go from the MFMA accumulators straight into the agent's row of G (the
 //     Mixer flatten order, mixer.py:69), bias gradients are fixed-order column sums, and the
 //     per-agent loss is summed in a fixed order (deterministic, hipGraph-replay stable).
 // LDS strides are chosen per access so the MFMA fragment reads are bank-conflict free:
 //   [row][k] images read by 16 rows x 4 k   -> stride = 4 (mod 8)  floats  (36, 156)
-//   [k][col] images read by 16 cols x 4 k   -> stride = 16 (mod 32) floats (80, 176)
+//   [k][col] images read by 16 cols x 4 k   -> stride = 16 (mod 32) floats (176)
+//   [k][col] images read by 32 cols x 2 k (32x32x2) -> stride = 32 (mod 64) floats (288)
 // f32 MFMA (16x16x4) products are exact fp32 fma chains; summation order differs from
 // autograd's BLAS, so parity is a tolerance (tests/test_batched_ann_gpu.py).
 #include "dl_internal.h"
@@ -26,13 +27,16 @@ namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+#ifndef MLP_PROBE_MODE
+#define MLP_PROBE_MODE 0   // scripts/mlp_probe builds 1 and 2 to time the phases' parts
+#endif
+
 constexpr int NTHR = 512;     // 8 waves, 2 per SIMD
 constexpr int MB = 64;        // batch rows per agent
 constexpr int LDH = 156;      // activation row stride: dh <= 152 columns + zero pad
 constexpr int BK = 32;        // K slice of the staged GEMMs
 constexpr int LDS1 = 36;      // [row][BK] slices
 constexpr int LDT = 176;      // [k][col] slices (cols <= 160)
-constexpr int LDX2 = 80;      // dW1: x chunk [64][64 (+16)]
 constexpr int LDZ = 17;       // logits / dZ4 [64][16 (+1)]
 constexpr int LDW4 = 156;     // W4 image [16][dh] for the logits
 
@@ -41,7 +45,6 @@ constexpr int STAGE_FLOATS = MB * LDS1 + 160 * LDS1;      // largest staging use
 constexpr int Z_FLOATS = MB * LDZ;
 constexpr int LDS_FLOATS = 3 * H_FLOATS + STAGE_FLOATS + Z_FLOATS + 16;
 static_assert(160 * LDS1 + MB * LDS1 >= 32 * LDT, "staging area holds a [32][176] slice");
-static_assert(160 * LDS1 + MB * LDS1 >= MB * LDX2, "staging area holds a dW1 x chunk");
 static_assert(160 * LDS1 + MB * LDS1 >= 16 * LDW4, "staging area holds W4");
 static_assert(LDS_FLOATS * 4 <= kLdsBytes, "fits one CU's LDS");
 
@@ -49,7 +52,61 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+__device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
 __device__ __forceinline__ int round4(int v) { return (v + 3) & ~3; }
+
+// Two slices in flight: while the MFMAs consume slice s from LDS, the global loads of slices
+// s + 1 and s + 2 are outstanding in two register sets (HBM latency under full load is longer
+// than one slice of MFMAs).  load(set, s) issues slice s, store(set) writes it to LDS,
+// compute(s) runs on the LDS image.  Plain loads stay in flight across the barriers.
+template <typename Set, typename Load, typename Store, typename Compute>
+__device__ __forceinline__ void pipeline2(int ns, Load load, Store store, Compute compute) {
+    Set A, B;
+    load(A, 0);
+    if (ns > 1) load(B, 1);
+    for (int s = 0; s < ns; s += 2) {
+        store(A);
+        __syncthreads();
+        if (s + 2 < ns) load(A, s + 2);
+        compute(s);
+        __syncthreads();
+        if (s + 1 < ns) {
+            store(B);
+            __syncthreads();
+            if (s + 3 < ns) load(B, s + 3);
+            compute(s + 1);
+            __syncthreads();
+        }
+    }
+}
+
+// Same, with two LDS images: slice s + 1 is written into the other image while the MFMAs read
+// slice s, so each slice costs one barrier and the LDS writes overlap the matrix work.  The
+// register set of slice s + 1 was issued two compute phases before it is stored.
+template <typename Set, typename Load, typename Store, typename Compute>
+__device__ __forceinline__ void pipeline_db(int ns, Load load, Store store, Compute compute) {
+    Set A, B;
+    load(A, 0);
+    if (ns > 1) load(B, 1);
+    store(A, 0);
+    __syncthreads();
+    for (int s = 0; s < ns; s += 2) {
+        if (s + 2 < ns) load(A, s + 2);
+        compute(s, 0);
+        if (s + 1 < ns) store(B, 1);
+        __syncthreads();
+        if (s + 1 < ns) {
+            if (s + 3 < ns) load(B, s + 3);
+            compute(s + 1, 1);
+            if (s + 2 < ns) store(A, 0);
+            __syncthreads();
+        }
+    }
+}
 
 // ---------------------------------------------------------------- staging (global -> LDS)
 // rows x BK slice of a row-major [rows][ld] matrix, columns [k0, k0 + BK), zero outside
@@ -140,19 +197,30 @@ __device__ __forceinline__ float act_grad(int layer, float h) {
 // Blds[k * LDT + n] (staged [k][n] slice).
 template <bool B_KMAJOR>
 __device__ __forceinline__ void mma_rows64(f32x4 (&acc)[5], const float *A, int lda,
-                                           const float *Bs, int kn) {
+                                           const float *Bs) {
+    // a whole BK slice, software-pipelined: the fragments of k-step s + 1 are read while the
+    // five MFMAs of step s issue, so LDS latency hides behind the matrix core instead of
+    // alternating with it (the barriers around a slice put all waves in the same phase).  K tails
+    // need no guard: staged slices are zero beyond K and LDS holds only finite values.
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int m = (wave & 3) * 16 + (lane & 15);
     const int n0 = (wave >> 2) * 80 + (lane & 15);
-    for (int kk = 0; kk < kn; kk += 4) {
-        const int k = kk + (lane >> 4);
-        const float a = A[m * lda + k];
+    float a[2], b[2][5];
+    auto read = [&](int s, int buf) {
+        const int k = 4 * s + (lane >> 4);
+        a[buf] = A[m * lda + k];
 #pragma unroll
         for (int t = 0; t < 5; ++t) {
             const int n = n0 + 16 * t;
-            const float b = B_KMAJOR ? Bs[k * LDT + n] : Bs[n * LDS1 + k];
-            acc[t] = mfma4(a, b, acc[t]);
+            b[buf][t] = B_KMAJOR ? Bs[k * LDT + n] : Bs[n * LDS1 + k];
         }
+    };
+    read(0, 0);
+#pragma unroll
+    for (int s = 0; s < BK / 4; ++s) {
+        if (s + 1 < BK / 4) read(s + 1, (s + 1) & 1);
+#pragma unroll
+        for (int t = 0; t < 5; ++t) acc[t] = mfma4(a[s & 1], b[s & 1][t], acc[t]);
     }
 }
 
@@ -175,42 +243,36 @@ __device__ __forceinline__ void epi_rows64(const f32x4 (&acc)[5], F f) {
 }
 
 // Forward layer on an LDS-resident input: H = act(Hin W^T + b), K = N = dh, W staged by slices.
-__device__ void forward_hidden(const float *W, const float *bias, int dh, const float *Hin,
+__device__ __forceinline__ void forward_hidden(const float *W, const float *bias, int dh, const float *Hin,
                                float *Hout, float *stage, int layer) {
     f32x4 acc[5];
     zero(acc);
-    RowSlice<160> ws;
-    const int ns = (dh + BK - 1) / BK;
-    ws.load(W, dh, dh, dh, 0);
-    for (int s = 0; s < ns; ++s) {
-        ws.store(stage);
-        __syncthreads();
-        if (s + 1 < ns) ws.load(W, dh, dh, dh, (s + 1) * BK);
-        const int k0 = s * BK;
-        mma_rows64<false>(acc, Hin + k0, LDH, stage, round4(min(BK, dh - k0)));
-        __syncthreads();
-    }
+    pipeline2<RowSlice<160>>(
+        (dh + BK - 1) / BK,
+        [&](RowSlice<160> &w, int s) { w.load(W, dh, dh, dh, s * BK); },
+        [&](const RowSlice<160> &w) { w.store(stage); },
+        [&](int s) {
+            const int k0 = s * BK;
+            mma_rows64<false>(acc, Hin + k0, LDH, stage);
+        });
     epi_rows64(acc, [&](int m, int n, float v) {
         if (n < dh) Hout[m * LDH + n] = act_fwd(layer, v + bias[n]);
     });
 }
 
 // Backward through a hidden layer: Hio <- (dZ W) * act'(Hio)  (in place), K = dk rows of W.
-__device__ void backward_dz(const float *W, int dk, int dh, const float *dZ, int ldz, float *Hio,
+__device__ __forceinline__ void backward_dz(const float *W, int dk, int dh, const float *dZ, int ldz, float *Hio,
                             float *stage, int layer) {
     f32x4 acc[5];
     zero(acc);
-    ColSlice ws;
-    const int ns = (dk + BK - 1) / BK;
-    ws.load(W, dh, dh, dk, 0);
-    for (int s = 0; s < ns; ++s) {
-        ws.store(stage);
-        __syncthreads();
-        if (s + 1 < ns) ws.load(W, dh, dh, dk, (s + 1) * BK);
-        const int k0 = s * BK;
-        mma_rows64<true>(acc, dZ + k0, ldz, stage, round4(min(BK, dk - k0)));
-        __syncthreads();
-    }
+    pipeline2<ColSlice>(
+        (dk + BK - 1) / BK,
+        [&](ColSlice &w, int s) { w.load(W, dh, dh, dk, s * BK); },
+        [&](const ColSlice &w) { w.store(stage); },
+        [&](int s) {
+            const int k0 = s * BK;
+            mma_rows64<true>(acc, dZ + k0, ldz, stage);
+        });
     epi_rows64(acc, [&](int m, int n, float v) {
         if (n < dh) Hio[m * LDH + n] = v * act_grad(layer, Hio[m * LDH + n]);
     });
@@ -218,36 +280,31 @@ __device__ void backward_dz(const float *W, int dk, int dh, const float *dZ, int
 
 // Weight gradient of a hidden layer: dW[i][j] = sum_b dZ[b][i] Hin[b][j] (both LDS-resident,
 // [64][LDH]), i, j < dh, straight into G; bias gradient db[i] = sum_b dZ[b][i] in order.
-// 100 tiles (10 x 10 of 16 x 16) over 8 waves, 13 consecutive tiles per wave.
-__device__ void weight_grad_hidden(const float *dZ, const float *Hin, int dh, float *gW,
+// 25 tiles of 32 x 32 (v_mfma_f32_32x32x2_f32: half the operand reads of 16x16x4 per flop),
+// wave w computes tiles w, w + 8, w + 16 (, 24) one after the other, so each tile's stores
+// overlap the next tile's MFMAs (one accumulator: the 32x32x2 issue interval equals its
+// dependent latency).  C/D: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5): every
+// store instruction writes two 128-B runs.
+__device__ __forceinline__ void weight_grad_hidden(const float *dZ, const float *Hin, int dh, float *gW,
                                    float *gb) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    constexpr int TPW = 13;
-    f32x4 acc[TPW];
+    for (int t = wave; t < 25; t += 8) {    // one tile at a time: stores overlap the next tile
+        f32x16 acc;
 #pragma unroll
-    for (int t = 0; t < TPW; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int t0 = wave * TPW;
-    for (int kk = 0; kk < MB; kk += 4) {
-        const int b = kk + (lane >> 4);
-#pragma unroll
-        for (int t = 0; t < TPW; ++t) {
-            const int tile = t0 + t;
-            if (tile < 100) {
-                const float a = dZ[b * LDH + (tile / 10) * 16 + (lane & 15)];
-                const float bb = Hin[b * LDH + (tile % 10) * 16 + (lane & 15)];
-                acc[t] = mfma4(a, bb, acc[t]);
-            }
+        for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+        const int ia = (t / 5) * 32 + (lane & 31), jb = (t % 5) * 32 + (lane & 31);
+#pragma unroll 8
+        for (int ks = 0; ks < MB / 2; ++ks) {
+            const int b = 2 * ks + (lane >> 5);
+            acc = mfma32(dZ[b * LDH + ia], Hin[b * LDH + jb], acc);
         }
-    }
+        if (jb < dh) {
+            float *g = gW + (int64_t)((t / 5) * 32 + 4 * (lane >> 5)) * dh + jb;
 #pragma unroll
-    for (int t = 0; t < TPW; ++t) {
-        const int tile = t0 + t;
-        if (tile >= 100) continue;
-        const int j = (tile % 10) * 16 + (lane & 15);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int i = (tile / 10) * 16 + 4 * (lane >> 4) + r;
-            if (i < dh && j < dh) gW[(int64_t)i * dh + j] = acc[t][r];
+            for (int r = 0; r < 16; ++r) {
+                const int i = (r & 3) + 8 * (r >> 2);
+                if ((t / 5) * 32 + 4 * (lane >> 5) + i < dh) g[i * dh] = acc[r];
+            }
         }
     }
     if (threadIdx.x < dh) {
@@ -268,7 +325,11 @@ struct MlpArgs {
     int64_t ldg;
     float *loss;
     int32_t din, dh, dout;
+    uint64_t *stamps;   // nullable: per-phase wall clocks of every workgroup (scripts/mlp_probe)
 };
+
+#define STAMP(i) \
+    if (p.stamps && threadIdx.x == 0) p.stamps[(int64_t)blockIdx.x * 16 + (i)] = wall_clock64()
 
 __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -283,47 +344,63 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
     float *Ga = p.G + (int64_t)a * p.ldg;
     const float *x = p.data + (int64_t)a * p.s_data;
     // parameter offsets in the Mixer flatten order (fc1.w, fc1.b, fc2.w, fc2.b, ...)
+    STAMP(0);
+    if (p.stamps && threadIdx.x == 0) p.stamps[(int64_t)blockIdx.x * 16 + 14] = __builtin_amdgcn_s_memtime();
     const int64_t o_w1 = 0, o_b1 = (int64_t)dh * din, o_w2 = o_b1 + dh, o_b2 = o_w2 + dh * dh,
                   o_w3 = o_b2 + dh, o_b3 = o_w3 + dh * dh, o_w4 = o_b3 + dh,
                   o_b4 = o_w4 + dout * dh;
 
-    // zero the activation pads (columns dh..LDH) and the logits image: K tails read them
-    for (int e = tid; e < 3 * MB * (LDH - dh); e += NTHR) {
-        const int buf = e / (MB * (LDH - dh)), r = e % (MB * (LDH - dh));
-        lds[buf * H_FLOATS + (r / (LDH - dh)) * LDH + dh + r % (LDH - dh)] = 0.f;
-    }
-    for (int e = tid; e < Z_FLOATS; e += NTHR) Zs[e] = 0.f;
+    // zero all of LDS: K tails and padded tiles then read only finite values (zeros where
+    // they meet a zero-filled staged operand), and the activation pads start at zero
+    for (int e = tid; e < LDS_FLOATS / 4; e += NTHR)
+        reinterpret_cast<f32x4 *>(lds)[e] = f32x4{0.f, 0.f, 0.f, 0.f};
+    __syncthreads();
 
-    // ---- layer 1: H1 = relu(x W1^T + b1), K = din from HBM, x and W1 slices register-prefetched
+    // ---- layer 1: H1 = relu(x W1^T + b1), K = din from HBM: x and W1 slices double-buffered in
+    // LDS (the H2/H3 space, free until layer 2), the next two register-prefetched
     {
         f32x4 acc[5];
         zero(acc);
-        float *xs = stage, *ws = stage + MB * LDS1;
-        RowSlice4<MB> xr;
-        RowSlice4<160> wr;
-        const int ns = (din + BK - 1) / BK;
-        xr.load(x, din, MB, din, 0);
-        wr.load(Xa + o_w1, din, dh, din, 0);
-        for (int s = 0; s < ns; ++s) {
-            xr.store(xs);
-            wr.store(ws);
-            __syncthreads();
-            if (s + 1 < ns) {
-                xr.load(x, din, MB, din, (s + 1) * BK);
-                wr.load(Xa + o_w1, din, dh, din, (s + 1) * BK);
-            }
-            mma_rows64<false>(acc, xs, LDS1, ws, round4(min(BK, din - s * BK)));
-            __syncthreads();
-        }
+        constexpr int IMG = MB * LDS1 + 160 * LDS1;   // one [x | W1] slice image
+        static_assert(2 * IMG <= 2 * H_FLOATS, "two slice images fit the H2/H3 space");
+        struct L1 {
+            RowSlice4<MB> x;
+            RowSlice4<160> w;
+        };
+        pipeline_db<L1>(
+            (din + BK - 1) / BK,
+            [&](L1 &v, int s) {
+#if MLP_PROBE_MODE == 2   // measurement only: every slice re-reads slice 0 (L2-resident)
+                s = 0;
+#endif
+#if MLP_PROBE_MODE != 3   // measurement only: 3 = no staging at all
+                v.x.load(x, din, MB, din, s * BK);
+                v.w.load(Xa + o_w1, din, dh, din, s * BK);
+#endif
+            },
+            [&](const L1 &v, int buf) {
+#if MLP_PROBE_MODE != 3
+                v.x.store(H2 + buf * IMG);
+                v.w.store(H2 + buf * IMG + MB * LDS1);
+#endif
+            },
+            [&](int s, int buf) {
+#if MLP_PROBE_MODE != 1   // measurement only: 1 = no MFMAs
+                mma_rows64<false>(acc, H2 + buf * IMG, LDS1, H2 + buf * IMG + MB * LDS1);
+#endif
+            });
         const float *b1 = Xa + o_b1;
         epi_rows64(acc, [&](int m, int n, float v) {
             if (n < dh) H1[m * LDH + n] = act_fwd(0, v + b1[n]);
         });
     }
     __syncthreads();
+    STAMP(1);
     forward_hidden(Xa + o_w2, Xa + o_b2, dh, H1, H2, stage, 1);
     __syncthreads();
+    STAMP(2);
     forward_hidden(Xa + o_w3, Xa + o_b3, dh, H2, H3, stage, 2);
+    STAMP(3);
     // ---- logits Z = H3 W4^T + b4 (waves 0-3, one 16 x 16 tile each), W4 image [16][LDW4]
     for (int e = tid; e < 16 * LDW4; e += NTHR) {
         const int n = e / LDW4, k = e % LDW4;
@@ -364,6 +441,7 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
     if (tid == 0 && p.loss)
         p.loss[a] = ((lpart[0] + lpart[1]) + (lpart[2] + lpart[3])) +
                     ((lpart[4] + lpart[5]) + (lpart[6] + lpart[7]));
+    STAMP(4);
     // ---- dW4 = dZ4^T H3 [dout x dh] (one M-tile, N-tiles w and w + 8), db4
     {
         for (int nt = wave; nt < 10; nt += 8) {
@@ -389,60 +467,76 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
     // ---- dZ3 = (dZ4 W4) * elu'(H3) in place, K = dout
     backward_dz(Xa + o_w4, dout, dh, Zs, LDZ, H3, stage, 2);
     __syncthreads();
+    STAMP(5);
     weight_grad_hidden(H3, H2, dh, Ga + o_w3, Ga + o_b3);
     __syncthreads();
+    STAMP(6);
     backward_dz(Xa + o_w3, dh, dh, H3, LDH, H2, stage, 1);     // dZ2 into H2
     __syncthreads();
+    STAMP(7);
     weight_grad_hidden(H2, H1, dh, Ga + o_w2, Ga + o_b2);
     __syncthreads();
+    STAMP(8);
     backward_dz(Xa + o_w2, dh, dh, H2, LDH, H1, stage, 0);     // dZ1 into H1
     __syncthreads();
-    // ---- dW1 = dZ1^T x [dh x din] by 64-column chunks of x; db1
+    STAMP(9);
+    // ---- dW1 = dZ1^T x [dh x din] by 256-column chunks of x, staged in the H2/H3 space (free
+    // now: dZ2 and dZ3 are consumed); wave w owns the chunk's 32-column N-tile w and all five
+    // 32-row M-tiles (v_mfma_f32_32x32x2_f32); the next chunk is loaded during the MFMAs.  db1.
     {
-        float *xs = stage;
-        constexpr int PER = MB * 16 / NTHR;   // float4s of a [64][64] chunk per thread
+        constexpr int CW = 256, LDC = 288;   // chunk width, row stride (= 32 mod 64)
+        static_assert(MB * LDC <= 2 * H_FLOATS, "x chunk fits the H2/H3 space");
+        float *xs = H2;
+        constexpr int PER = MB * CW / 4 / NTHR;   // 8 float4 per thread
         f32x4 xv[PER];
         auto load = [&](int c0) {
 #pragma unroll
             for (int i = 0; i < PER; ++i) {
                 const int e = tid + i * NTHR;
-                const int b = e / 16, c = 4 * (e % 16);
+                const int b = e / (CW / 4), c = 4 * (e % (CW / 4));
                 xv[i] = c0 + c < din ? *reinterpret_cast<const f32x4 *>(x + (int64_t)b * din + c0 + c)
                                      : f32x4{0.f, 0.f, 0.f, 0.f};
             }
         };
-        const int nc = (din + 63) / 64;
+        const int nc = (din + CW - 1) / CW;
         load(0);
         for (int ci = 0; ci < nc; ++ci) {
 #pragma unroll
             for (int i = 0; i < PER; ++i) {
                 const int e = tid + i * NTHR;
-                *reinterpret_cast<f32x4 *>(xs + (e / 16) * LDX2 + 4 * (e % 16)) = xv[i];
+                *reinterpret_cast<f32x4 *>(xs + (e / (CW / 4)) * LDC + 4 * (e % (CW / 4))) = xv[i];
             }
             __syncthreads();
-            const int c0 = ci * 64;
-            if (ci + 1 < nc) load(c0 + 64);
-            // wave w: N-tile (w & 3) of the chunk, M-tiles 5 (w >> 2) + t
-            f32x4 acc[5];
-            zero(acc);
-            const int nl = (wave & 3) * 16 + (lane & 15);
-            if (c0 + (wave & 3) * 16 < din) {
-                for (int kk = 0; kk < MB; kk += 4) {
-                    const int b = kk + (lane >> 4);
-                    const float bv = xs[b * LDX2 + nl];
+            const int c0 = ci * CW;
+            if (ci + 1 < nc) load(c0 + CW);
+            // (N-tile, M-tile) items of this chunk round-robin over the waves, one 32 x 32 tile at a
+            // time: its 16 stores go out while the wave's next tile runs on the matrix core (the
+            // G writes of dW1 are a quarter of the kernel's HBM traffic)
+            const int ntc = min(CW / 32, (din - c0 + 31) / 32);
+            int ld = din;
+            asm volatile("" : "+s"(ld));   // keep the store offsets in the loop (no hoisting)
+            for (int it = wave; it < 5 * ntc; it += 8) {
+                const int nt = it % ntc, t = it / ntc;
+                const int nl = 32 * nt + (lane & 31);
+                f32x16 acc;
 #pragma unroll
-                    for (int t = 0; t < 5; ++t)
-                        acc[t] = mfma4(H1[b * LDH + ((wave >> 2) * 5 + t) * 16 + (lane & 15)], bv,
-                                       acc[t]);
+                for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#if MLP_PROBE_MODE != 5   // measurement only: 5 = no dW1 MFMAs
+#pragma unroll 8
+                for (int ks = 0; ks < MB / 2; ++ks) {
+                    const int b = 2 * ks + (lane >> 5);
+                    acc = mfma32(H1[b * LDH + 32 * t + (lane & 31)], xs[b * LDC + nl], acc);
                 }
+#endif
+                const int j = c0 + nl;
+                if (j < din && MLP_PROBE_MODE != 4) {   // measurement only: 4 = no dW1 stores
+                    float *g = Ga + o_w1 + (32 * t + 4 * (lane >> 5)) * ld + j;
 #pragma unroll
-                for (int t = 0; t < 5; ++t)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int i = ((wave >> 2) * 5 + t) * 16 + 4 * (lane >> 4) + r;
-                        if (i < dh && c0 + nl < din)
-                            Ga[o_w1 + (int64_t)i * din + c0 + nl] = acc[t][r];
+                    for (int r = 0; r < 16; ++r) {
+                        const int i = (r & 3) + 8 * (r >> 2);
+                        if (32 * t + 4 * (lane >> 5) + i < dh) g[i * ld] = acc[r];
                     }
+                }
             }
             __syncthreads();
         }
@@ -452,6 +546,8 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
             Ga[o_b1 + tid] = s;
         }
     }
+    STAMP(10);
+    if (p.stamps && threadIdx.x == 0) p.stamps[(int64_t)blockIdx.x * 16 + 15] = __builtin_amdgcn_s_memtime();
 }
 
 }  // namespace
@@ -466,7 +562,7 @@ hipError_t launch_mlp_fused(const float *X, int64_t ldx, const float *data, int6
                             float *loss, int n_agents, int din, int dh, int dout, hipStream_t s) {
     hipError_t e = allow_full_lds(reinterpret_cast<const void *>(mlp_fused_kernel));
     if (e != hipSuccess) return e;
-    MlpArgs p{X, ldx, data, s_data, labels, s_lab, G, ldg, loss, din, dh, dout};
+    MlpArgs p{X, ldx, data, s_data, labels, s_lab, G, ldg, loss, din, dh, dout, nullptr};
     hipLaunchKernelGGL(mlp_fused_kernel, dim3((unsigned)n_agents), dim3(NTHR),
                        LDS_FLOATS * sizeof(float), s, p);
     return hipGetLastError();

@@ -53,6 +53,9 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-graph", action="store_true", help="c3/c5: eager launches, no hipGraph")
     p.add_argument("--streams", type=int, default=8, help="c5: HIP streams the agents share")
+    p.add_argument("--c3-layout", default="rows", choices=["rows", "tiled"],
+                   help="c3: resident layout of X and G (tiled: the fused gradient kernel "
+                        "addresses the round's column tiles; measured equal overall)")
     p.add_argument("--batch", type=int, default=64, help="c5: images per agent per step")
     p.add_argument("--dist-backend", default="nccl",
                    help="nccl (= RCCL, default) or gloo (multi-rank rehearsal on one GPU)")
@@ -251,9 +254,13 @@ def run_c3(args, dev, rank, world):
     X0 = c3_init_rows(ann, gen)
     data = torch.randn(n, B, ann.din, device=dev, generator=gen)
     labels = torch.randint(0, ann.dout, (n, B), device=dev, generator=gen, dtype=torch.int32)
-    P_pad = MLPConsensusSGD.padded_params(csr, P, dev)   # zero columns: no ragged tail tile
-    X0 = torch.nn.functional.pad(X0, (0, P_pad - P))
-    eng = engine.GossipEngine(csr, P_pad, device=dev, X=X0, layout="rows")
+    if ann.path == "fused" and args.c3_layout == "tiled":   # X, G column-tiled
+        P_pad = P
+        eng = engine.GossipEngine(csr, P, device=dev, X=X0, layout="tiled")
+    else:
+        P_pad = MLPConsensusSGD.padded_params(csr, P, dev)   # zero columns: no ragged tail
+        X0 = torch.nn.functional.pad(X0, (0, P_pad - P))
+        eng = engine.GossipEngine(csr, P_pad, device=dev, X=X0, layout="rows")
     del X0
     sgd = MLPConsensusSGD(ann, eng, data, labels, lr, deviation=True)
     G = sgd.G
@@ -266,7 +273,10 @@ def run_c3(args, dev, rank, world):
     evs = event_pairs(n_ev, 3)
     for i in range(n_ev):
         evs[i][0].record(stream)
-        ann.gradients(eng.X[:, :P], data, labels, G[:, :P])
+        if eng.layout == "tiled":
+            ann.gradients(eng.X, data, labels, G)
+        else:
+            ann.gradients(eng.X[:, :P], data, labels, G[:, :P])
         evs[i][1].record(stream)
         eng.round(G=G, lr=lr, deviation=True)
         evs[i][2].record(stream)
@@ -296,7 +306,8 @@ def run_c3(args, dev, rank, world):
         return
     grad_roof = {"bound": "mfma", "achieved": tflops, "peak": FP32_MFMA_PEAK_TFLOPS,
                  "unit": "TFLOP/s", "frac": tflops / FP32_MFMA_PEAK_TFLOPS, "traffic": None,
-                 "kernel": "dl_bgemm x11 + dl_xent_grad (per-step HIP-event time)",
+                 "kernel": ("mlp_fused_kernel" if ann.path == "fused" else
+                            "dl_bgemm x11 + dl_xent_grad") + " (per-step HIP-event time)",
                  "flops_per_launch": flops, "launch_ms": grad_ms}
     mix_roof = {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": gbs / HBM_PEAK_GBS, "traffic": None,
@@ -328,6 +339,7 @@ def run_c3(args, dev, rank, world):
         "config": {"workload": "c3: ANNModel consensus SGD (batched per-agent MFMA gradients + "
                                "fused round + deviation)",
                    "agents": n, "params": P, "params_padded": P_pad, "batch": B, "lr": lr,
+                   "layout": eng.layout, "gradient_path": ann.path,
                    "graph": "random 4-regular",
                    "weights": f"best-constant {wconst:.6f}",
                    "launch": "hipGraph replay per step" if use_graph else "eager",

@@ -65,7 +65,8 @@ class DlSgdArgs(ctypes.Structure):
 class DlMlpArgs(ctypes.Structure):
     _fields_ = [("n_agents", _i32), ("batch", _i32), ("input_dim", _i32), ("hidden_dim", _i32),
                 ("output_dim", _i32), ("X", _vp), ("ldx", _i64), ("data", _vp), ("s_data", _i64),
-                ("labels", _vp), ("s_labels", _i64), ("G", _vp), ("ldg", _i64), ("loss", _vp)]
+                ("labels", _vp), ("s_labels", _i64), ("G", _vp), ("ldg", _i64), ("loss", _vp),
+                ("tile_cols", _i32)]
 
 
 EPI = {"none": 0, "bias": 1, "bias_relu": 2, "bias_tanh": 3, "bias_elu": 4, "drelu": 5,

@@ -669,21 +669,26 @@ int dl_mlp_grad(const dl_mlp_args *a, dl_stream_t stream) {
                     a->output_dim);
     const int64_t din = a->input_dim, dh = a->hidden_dim, dout = a->output_dim;
     const int64_t P = dh * din + dh + 2 * (dh * dh + dh) + dout * dh + dout;
+    const int32_t T = a->tile_cols;
+    if (T < 0 || (T > 0 && (T < 4 || (T & (T - 1)) || (int64_t)T * a->n_agents > 0x7fffffff)))
+        return fail(DL_ERR_INVALID, "dl_mlp_grad: tile_cols must be 0 or a power of two >= 4");
     if (a->n_agents < 0 || a->n_agents > 65535 || !a->X || !a->data || !a->labels || !a->G ||
-        a->ldx < P || a->ldg < P || a->s_data < (int64_t)a->batch * din || a->s_labels < a->batch)
+        (T == 0 && (a->ldx < P || a->ldg < P)) || a->s_data < (int64_t)a->batch * din ||
+        a->s_labels < a->batch)
         return fail(DL_ERR_INVALID, "dl_mlp_grad: bad arguments (agents %d, params %lld, ldx %lld, "
                                     "ldg %lld)", a->n_agents, (long long)P, (long long)a->ldx,
                     (long long)a->ldg);
-    if (!aligned16(a->X) || !aligned16(a->data) || !aligned16(a->G) || (a->ldx & 3) ||
-        (a->ldg & 3) || (a->s_data & 3))
+    if (!aligned16(a->X) || !aligned16(a->data) || !aligned16(a->G) ||
+        (T == 0 && ((a->ldx & 3) || (a->ldg & 3))) || (a->s_data & 3))
         return fail(DL_ERR_INVALID, "dl_mlp_grad: X, data, G must be 16-byte aligned with row "
                                     "strides % 4 == 0");
-    const size_t xb = ((size_t)a->n_agents - 1) * a->ldx * 4 + P * 4;
-    const size_t gb = ((size_t)a->n_agents - 1) * a->ldg * 4 + P * 4;
+    const size_t tb = T ? (size_t)((P + T - 1) / T) * T * a->n_agents * 4 : 0;
+    const size_t xb = T ? tb : ((size_t)a->n_agents - 1) * a->ldx * 4 + P * 4;
+    const size_t gb = T ? tb : ((size_t)a->n_agents - 1) * a->ldg * 4 + P * 4;
     if (overlaps(a->X, xb, a->G, gb)) return fail(DL_ERR_INVALID, "dl_mlp_grad: G overlaps X");
     hipError_t e = dl::launch_mlp_fused(a->X, a->ldx, a->data, a->s_data, a->labels, a->s_labels,
                                         a->G, a->ldg, a->loss, a->n_agents, a->input_dim,
-                                        a->hidden_dim, a->output_dim,
+                                        a->hidden_dim, a->output_dim, T,
                                         static_cast<hipStream_t>(stream));
     return e == hipSuccess ? DL_OK : hip_fail(e, "mlp_fused launch");
 }

@@ -144,6 +144,7 @@ hipError_t launch_xent_grad(const float *Z, int64_t sZ, const int32_t *y, int64_
 int mlp_fused_supported(int batch, int din, int dh, int dout);
 hipError_t launch_mlp_fused(const float *X, int64_t ldx, const float *data, int64_t s_data,
                             const int32_t *labels, int64_t s_lab, float *G, int64_t ldg,
-                            float *loss, int n_agents, int din, int dh, int dout, hipStream_t s);
+                            float *loss, int n_agents, int din, int dh, int dout, int tile_cols,
+                            hipStream_t s);
 
 }  // namespace dl

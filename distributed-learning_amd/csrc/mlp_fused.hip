@@ -108,6 +108,41 @@ __device__ __forceinline__ void pipeline_db(int ns, Load load, Store store, Comp
     }
 }
 
+// ---------------------------------------------------------------- parameter addressing
+// One agent's row of X or G: parameter p -> element address, row-major (base + p) or in the
+// engine's column-tiled layout [ceil(P/T)][n_agents][T] (tile p >> sh, lane p & (T - 1)), so the
+// same kernel reads the tiled X the c3 round streams at copy speed.
+template <bool TILED>
+struct PRow {
+    float *base;        // row-major: X + a * ld;  tiled: X + a * T
+    int64_t tstride;    // tiled: n_agents * T
+    int sh;             // tiled: log2 T
+    __device__ __forceinline__ float *at(int64_t p) const {
+        if constexpr (TILED) return base + (p >> sh) * tstride + (p & ((int64_t(1) << sh) - 1));
+        return base + p;
+    }
+};
+
+// [rows][ld] matrix inside a parameter row (a weight or bias, Mixer order offsets)
+template <bool TILED>
+struct ParMat {
+    PRow<TILED> row;
+    int64_t off;
+    int ld;
+    __device__ __forceinline__ float *at(int r, int c) const {
+        return row.at(off + (int64_t)r * ld + c);
+    }
+};
+
+// plain row-major matrix (the agent's input batch)
+struct PlainMat {
+    const float *p;
+    int64_t ld;
+    __device__ __forceinline__ const float *at(int r, int c) const {
+        return p + (int64_t)r * ld + c;
+    }
+};
+
 // ---------------------------------------------------------------- staging (global -> LDS)
 // rows x BK slice of a row-major [rows][ld] matrix, columns [k0, k0 + BK), zero outside
 // [0, n_rows) x [0, K), into S[r * LDS1 + c].  Register-prefetched: load() then store().
@@ -115,12 +150,13 @@ template <int ROWS>
 struct RowSlice {
     static constexpr int PER = (ROWS * BK + NTHR - 1) / NTHR;
     float v[PER];
-    __device__ __forceinline__ void load(const float *W, int64_t ld, int n_rows, int K, int k0) {
+    template <typename M>
+    __device__ __forceinline__ void load(const M &W, int n_rows, int K, int k0) {
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
             const int e = threadIdx.x + i * NTHR;
             const int r = e / BK, c = e % BK;
-            v[i] = (e < ROWS * BK && r < n_rows && k0 + c < K) ? W[(int64_t)r * ld + k0 + c] : 0.f;
+            v[i] = (e < ROWS * BK && r < n_rows && k0 + c < K) ? *W.at(r, k0 + c) : 0.f;
         }
     }
     __device__ __forceinline__ void store(float *S) const {
@@ -138,13 +174,14 @@ struct RowSlice4 {
     static constexpr int Q = BK / 4;
     static constexpr int PER = (ROWS * Q + NTHR - 1) / NTHR;
     f32x4 v[PER];
-    __device__ __forceinline__ void load(const float *W, int64_t ld, int n_rows, int K, int k0) {
+    template <typename M>   // 4 consecutive parameters never straddle a tile (T % 4 == 0)
+    __device__ __forceinline__ void load(const M &W, int n_rows, int K, int k0) {
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
             const int e = threadIdx.x + i * NTHR;
             const int r = e / Q, c = 4 * (e % Q);
             v[i] = (e < ROWS * Q && r < n_rows && k0 + c < K)
-                       ? *reinterpret_cast<const f32x4 *>(W + (int64_t)r * ld + k0 + c)
+                       ? *reinterpret_cast<const f32x4 *>(W.at(r, k0 + c))
                        : f32x4{0.f, 0.f, 0.f, 0.f};
         }
     }
@@ -162,12 +199,13 @@ struct RowSlice4 {
 struct ColSlice {
     static constexpr int PER = BK * 160 / NTHR;  // 10
     float v[PER];
-    __device__ __forceinline__ void load(const float *W, int64_t ld, int n_cols, int K, int k0) {
+    template <typename M>
+    __device__ __forceinline__ void load(const M &W, int n_cols, int K, int k0) {
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
             const int e = threadIdx.x + i * NTHR;
             const int kl = e / 160, n = e % 160;
-            v[i] = (n < n_cols && k0 + kl < K) ? W[(int64_t)(k0 + kl) * ld + n] : 0.f;
+            v[i] = (n < n_cols && k0 + kl < K) ? *W.at(k0 + kl, n) : 0.f;
         }
     }
     __device__ __forceinline__ void store(float *S) const {
@@ -243,31 +281,33 @@ __device__ __forceinline__ void epi_rows64(const f32x4 (&acc)[5], F f) {
 }
 
 // Forward layer on an LDS-resident input: H = act(Hin W^T + b), K = N = dh, W staged by slices.
-__device__ __forceinline__ void forward_hidden(const float *W, const float *bias, int dh, const float *Hin,
-                               float *Hout, float *stage, int layer) {
+template <typename M>
+__device__ __forceinline__ void forward_hidden(const M &W, const M &bias, int dh, const float *Hin,
+                                               float *Hout, float *stage, int layer) {
     f32x4 acc[5];
     zero(acc);
     pipeline2<RowSlice<160>>(
         (dh + BK - 1) / BK,
-        [&](RowSlice<160> &w, int s) { w.load(W, dh, dh, dh, s * BK); },
+        [&](RowSlice<160> &w, int s) { w.load(W, dh, dh, s * BK); },
         [&](const RowSlice<160> &w) { w.store(stage); },
         [&](int s) {
             const int k0 = s * BK;
             mma_rows64<false>(acc, Hin + k0, LDH, stage);
         });
     epi_rows64(acc, [&](int m, int n, float v) {
-        if (n < dh) Hout[m * LDH + n] = act_fwd(layer, v + bias[n]);
+        if (n < dh) Hout[m * LDH + n] = act_fwd(layer, v + *bias.at(0, n));
     });
 }
 
 // Backward through a hidden layer: Hio <- (dZ W) * act'(Hio)  (in place), K = dk rows of W.
-__device__ __forceinline__ void backward_dz(const float *W, int dk, int dh, const float *dZ, int ldz, float *Hio,
-                            float *stage, int layer) {
+template <typename M>
+__device__ __forceinline__ void backward_dz(const M &W, int dk, int dh, const float *dZ, int ldz,
+                                            float *Hio, float *stage, int layer) {
     f32x4 acc[5];
     zero(acc);
     pipeline2<ColSlice>(
         (dk + BK - 1) / BK,
-        [&](ColSlice &w, int s) { w.load(W, dh, dh, dk, s * BK); },
+        [&](ColSlice &w, int s) { w.load(W, dh, dk, s * BK); },
         [&](const ColSlice &w) { w.store(stage); },
         [&](int s) {
             const int k0 = s * BK;
@@ -285,8 +325,9 @@ __device__ __forceinline__ void backward_dz(const float *W, int dk, int dh, cons
 // overlap the next tile's MFMAs (one accumulator: the 32x32x2 issue interval equals its
 // dependent latency).  C/D: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5): every
 // store instruction writes two 128-B runs.
-__device__ __forceinline__ void weight_grad_hidden(const float *dZ, const float *Hin, int dh, float *gW,
-                                   float *gb) {
+template <typename M>
+__device__ __forceinline__ void weight_grad_hidden(const float *dZ, const float *Hin, int dh,
+                                                   const M &gW, const M &gb) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (int t = wave; t < 25; t += 8) {    // one tile at a time: stores overlap the next tile
         f32x16 acc;
@@ -299,18 +340,18 @@ __device__ __forceinline__ void weight_grad_hidden(const float *dZ, const float 
             acc = mfma32(dZ[b * LDH + ia], Hin[b * LDH + jb], acc);
         }
         if (jb < dh) {
-            float *g = gW + (int64_t)((t / 5) * 32 + 4 * (lane >> 5)) * dh + jb;
+            const int i0 = (t / 5) * 32 + 4 * (lane >> 5);
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int i = (r & 3) + 8 * (r >> 2);
-                if ((t / 5) * 32 + 4 * (lane >> 5) + i < dh) g[i * dh] = acc[r];
+                const int i = i0 + (r & 3) + 8 * (r >> 2);
+                if (i < dh) *gW.at(i, jb) = acc[r];
             }
         }
     }
     if (threadIdx.x < dh) {
         float s = 0.f;
         for (int b = 0; b < MB; ++b) s += dZ[b * LDH + threadIdx.x];
-        gb[threadIdx.x] = s;
+        *gb.at(0, threadIdx.x) = s;
     }
 }
 
@@ -325,12 +366,15 @@ struct MlpArgs {
     int64_t ldg;
     float *loss;
     int32_t din, dh, dout;
+    int32_t tsh;        // column-tiled X and G: log2 of the tile width (0 = row-major)
+    int64_t tstride;    // column-tiled: n_agents * T floats per tile
     uint64_t *stamps;   // nullable: per-phase wall clocks of every workgroup (scripts/mlp_probe)
 };
 
 #define STAMP(i) \
     if (p.stamps && threadIdx.x == 0) p.stamps[(int64_t)blockIdx.x * 16 + (i)] = wall_clock64()
 
+template <bool TILED>
 __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     float *H1 = lds, *H2 = lds + H_FLOATS, *H3 = lds + 2 * H_FLOATS;
@@ -340,8 +384,14 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
     const int a = blockIdx.x;
     const int din = p.din, dh = p.dh, dout = p.dout;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const float *Xa = p.X + (int64_t)a * p.ldx;
-    float *Ga = p.G + (int64_t)a * p.ldg;
+    PRow<TILED> Xr, Gr;
+    if constexpr (TILED) {
+        Xr = {const_cast<float *>(p.X) + ((int64_t)a << p.tsh), p.tstride, p.tsh};
+        Gr = {p.G + ((int64_t)a << p.tsh), p.tstride, p.tsh};
+    } else {
+        Xr = {const_cast<float *>(p.X) + (int64_t)a * p.ldx, 0, 0};
+        Gr = {p.G + (int64_t)a * p.ldg, 0, 0};
+    }
     const float *x = p.data + (int64_t)a * p.s_data;
     // parameter offsets in the Mixer flatten order (fc1.w, fc1.b, fc2.w, fc2.b, ...)
     STAMP(0);
@@ -349,6 +399,8 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
     const int64_t o_w1 = 0, o_b1 = (int64_t)dh * din, o_w2 = o_b1 + dh, o_b2 = o_w2 + dh * dh,
                   o_w3 = o_b2 + dh, o_b3 = o_w3 + dh * dh, o_w4 = o_b3 + dh,
                   o_b4 = o_w4 + dout * dh;
+    using PM = ParMat<TILED>;
+    auto mat = [&](const PRow<TILED> &r, int64_t off, int ld) { return PM{r, off, ld}; };
 
     // zero all of LDS: K tails and padded tiles then read only finite values (zeros where
     // they meet a zero-filled staged operand), and the activation pads start at zero
@@ -374,8 +426,8 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
                 s = 0;
 #endif
 #if MLP_PROBE_MODE != 3   // measurement only: 3 = no staging at all
-                v.x.load(x, din, MB, din, s * BK);
-                v.w.load(Xa + o_w1, din, dh, din, s * BK);
+                v.x.load(PlainMat{x, din}, MB, din, s * BK);
+                v.w.load(mat(Xr, o_w1, din), dh, din, s * BK);
 #endif
             },
             [&](const L1 &v, int buf) {
@@ -389,22 +441,21 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
                 mma_rows64<false>(acc, H2 + buf * IMG, LDS1, H2 + buf * IMG + MB * LDS1);
 #endif
             });
-        const float *b1 = Xa + o_b1;
         epi_rows64(acc, [&](int m, int n, float v) {
-            if (n < dh) H1[m * LDH + n] = act_fwd(0, v + b1[n]);
+            if (n < dh) H1[m * LDH + n] = act_fwd(0, v + *Xr.at(o_b1 + n));
         });
     }
     __syncthreads();
     STAMP(1);
-    forward_hidden(Xa + o_w2, Xa + o_b2, dh, H1, H2, stage, 1);
+    forward_hidden(mat(Xr, o_w2, dh), mat(Xr, o_b2, 0), dh, H1, H2, stage, 1);
     __syncthreads();
     STAMP(2);
-    forward_hidden(Xa + o_w3, Xa + o_b3, dh, H2, H3, stage, 2);
+    forward_hidden(mat(Xr, o_w3, dh), mat(Xr, o_b3, 0), dh, H2, H3, stage, 2);
     STAMP(3);
     // ---- logits Z = H3 W4^T + b4 (waves 0-3, one 16 x 16 tile each), W4 image [16][LDW4]
     for (int e = tid; e < 16 * LDW4; e += NTHR) {
         const int n = e / LDW4, k = e % LDW4;
-        stage[e] = (n < dout && k < dh) ? Xa[o_w4 + (int64_t)n * dh + k] : 0.f;
+        stage[e] = (n < dout && k < dh) ? *Xr.at(o_w4 + (int64_t)n * dh + k) : 0.f;
     }
     __syncthreads();
     if (wave < 4) {
@@ -417,7 +468,7 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
         const int n = lane & 15;
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-            if (n < dout) Zs[(wave * 16 + 4 * (lane >> 4) + r) * LDZ + n] = acc[r] + Xa[o_b4 + n];
+            if (n < dout) Zs[(wave * 16 + 4 * (lane >> 4) + r) * LDZ + n] = acc[r] + *Xr.at(o_b4 + n);
     }
     __syncthreads();
     // ---- cross-entropy head (torch.nn.CrossEntropyLoss, mean): dZ4 = (softmax - onehot) / 64
@@ -454,30 +505,30 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int i = 4 * (lane >> 4) + r;
-                if (i < dout && j < dh) Ga[o_w4 + (int64_t)i * dh + j] = acc[r];
+                if (i < dout && j < dh) *Gr.at(o_w4 + (int64_t)i * dh + j) = acc[r];
             }
         }
         if (tid < dout) {
             float s = 0.f;
             for (int b = 0; b < MB; ++b) s += Zs[b * LDZ + tid];
-            Ga[o_b4 + tid] = s;
+            *Gr.at(o_b4 + tid) = s;
         }
     }
     __syncthreads();
     // ---- dZ3 = (dZ4 W4) * elu'(H3) in place, K = dout
-    backward_dz(Xa + o_w4, dout, dh, Zs, LDZ, H3, stage, 2);
+    backward_dz(mat(Xr, o_w4, dh), dout, dh, Zs, LDZ, H3, stage, 2);
     __syncthreads();
     STAMP(5);
-    weight_grad_hidden(H3, H2, dh, Ga + o_w3, Ga + o_b3);
+    weight_grad_hidden(H3, H2, dh, mat(Gr, o_w3, dh), mat(Gr, o_b3, 0));
     __syncthreads();
     STAMP(6);
-    backward_dz(Xa + o_w3, dh, dh, H3, LDH, H2, stage, 1);     // dZ2 into H2
+    backward_dz(mat(Xr, o_w3, dh), dh, dh, H3, LDH, H2, stage, 1);     // dZ2 into H2
     __syncthreads();
     STAMP(7);
-    weight_grad_hidden(H2, H1, dh, Ga + o_w2, Ga + o_b2);
+    weight_grad_hidden(H2, H1, dh, mat(Gr, o_w2, dh), mat(Gr, o_b2, 0));
     __syncthreads();
     STAMP(8);
-    backward_dz(Xa + o_w2, dh, dh, H2, LDH, H1, stage, 0);     // dZ1 into H1
+    backward_dz(mat(Xr, o_w2, dh), dh, dh, H2, LDH, H1, stage, 0);     // dZ1 into H1
     __syncthreads();
     STAMP(9);
     // ---- dW1 = dZ1^T x [dh x din] by 256-column chunks of x, staged in the H2/H3 space (free
@@ -513,8 +564,6 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
             // time: its 16 stores go out while the wave's next tile runs on the matrix core (the
             // G writes of dW1 are a quarter of the kernel's HBM traffic)
             const int ntc = min(CW / 32, (din - c0 + 31) / 32);
-            int ld = din;
-            asm volatile("" : "+s"(ld));   // keep the store offsets in the loop (no hoisting)
             for (int it = wave; it < 5 * ntc; it += 8) {
                 const int nt = it % ntc, t = it / ntc;
                 const int nl = 32 * nt + (lane & 31);
@@ -530,11 +579,11 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
 #endif
                 const int j = c0 + nl;
                 if (j < din && MLP_PROBE_MODE != 4) {   // measurement only: 4 = no dW1 stores
-                    float *g = Ga + o_w1 + (32 * t + 4 * (lane >> 5)) * ld + j;
+                    const int i0 = 32 * t + 4 * (lane >> 5);
 #pragma unroll
                     for (int r = 0; r < 16; ++r) {
-                        const int i = (r & 3) + 8 * (r >> 2);
-                        if (32 * t + 4 * (lane >> 5) + i < dh) g[i * ld] = acc[r];
+                        const int i = i0 + (r & 3) + 8 * (r >> 2);
+                        if (i < dh) *Gr.at(o_w1 + (int64_t)i * din + j) = acc[r];
                     }
                 }
             }
@@ -543,7 +592,7 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
         if (tid < dh) {
             float s = 0.f;
             for (int b = 0; b < MB; ++b) s += H1[b * LDH + tid];
-            Ga[o_b1 + tid] = s;
+            *Gr.at(o_b1 + tid) = s;
         }
     }
     STAMP(10);
@@ -559,12 +608,22 @@ int mlp_fused_supported(int batch, int din, int dh, int dout) {
 
 hipError_t launch_mlp_fused(const float *X, int64_t ldx, const float *data, int64_t s_data,
                             const int32_t *labels, int64_t s_lab, float *G, int64_t ldg,
-                            float *loss, int n_agents, int din, int dh, int dout, hipStream_t s) {
-    hipError_t e = allow_full_lds(reinterpret_cast<const void *>(mlp_fused_kernel));
+                            float *loss, int n_agents, int din, int dh, int dout, int tile_cols,
+                            hipStream_t s) {
+    int tsh = 0;
+    while (tile_cols > 0 && (1 << tsh) < tile_cols) ++tsh;
+    MlpArgs p{X, ldx, data, s_data, labels, s_lab, G, ldg, loss, din, dh, dout, tsh,
+              (int64_t)n_agents * tile_cols, nullptr};
+    const void *k = tile_cols > 0 ? reinterpret_cast<const void *>(mlp_fused_kernel<true>)
+                                  : reinterpret_cast<const void *>(mlp_fused_kernel<false>);
+    hipError_t e = allow_full_lds(k);
     if (e != hipSuccess) return e;
-    MlpArgs p{X, ldx, data, s_data, labels, s_lab, G, ldg, loss, din, dh, dout, nullptr};
-    hipLaunchKernelGGL(mlp_fused_kernel, dim3((unsigned)n_agents), dim3(NTHR),
-                       LDS_FLOATS * sizeof(float), s, p);
+    if (tile_cols > 0)
+        hipLaunchKernelGGL(mlp_fused_kernel<true>, dim3((unsigned)n_agents), dim3(NTHR),
+                           LDS_FLOATS * sizeof(float), s, p);
+    else
+        hipLaunchKernelGGL(mlp_fused_kernel<false>, dim3((unsigned)n_agents), dim3(NTHR),
+                           LDS_FLOATS * sizeof(float), s, p);
     return hipGetLastError();
 }
 

@@ -74,17 +74,33 @@ class BatchedANN:
 
     def gradients(self, X, data, labels, G):
         """G[a] = d loss_a / d params_a for every agent.  X, G: [N, P] row-major fp32 (row stride
-        may exceed P); data: [N, B, input_dim] fp32; labels: [N, B] int32.  Returns the per-agent
-        mean cross-entropy (device tensor [N])."""
+        may exceed P), or -- fused path only -- the engine's column-tiled [tiles, N, T] tensors
+        (tiles * T >= P); data: [N, B, input_dim] fp32; labels: [N, B] int32.  Returns the
+        per-agent mean cross-entropy (device tensor [N])."""
         lib = _lib.load()
         N, B, din, dh, dout, P = self.N, self.B, self.din, self.dh, self.dout, self.P
-        for t, shape in ((X, (N, P)), (G, (N, P))):
-            if tuple(t.shape) != shape or t.stride(1) != 1 or t.dtype != torch.float32:
-                raise ValueError(f"expected a row-major fp32 [{N}, {P}] tensor")
         if tuple(data.shape) != (N, B, din) or not data.is_contiguous():
             raise ValueError(f"data must be contiguous [{N}, {B}, {din}] fp32")
         if tuple(labels.shape) != (N, B) or labels.dtype != torch.int32:
             raise ValueError(f"labels must be int32 [{N}, {B}]")
+        if X.dim() == 3:
+            if self.path != "fused":
+                raise ValueError("the column-tiled layout needs the fused kernel")
+            tiles, n, T = X.shape
+            if n != N or tiles * T < P or tuple(G.shape) != tuple(X.shape) or \
+                    not X.is_contiguous() or not G.is_contiguous() or \
+                    X.dtype != torch.float32 or G.dtype != torch.float32:
+                raise ValueError(f"expected contiguous fp32 [tiles, {N}, T] tensors covering {P} "
+                                 "columns")
+            args = _lib.DlMlpArgs(N, B, din, dh, dout, _lib.ptr(X), 0, _lib.ptr(data), B * din,
+                                  _lib.ptr(labels), labels.stride(0), _lib.ptr(G), 0,
+                                  _lib.ptr(self.loss), T)
+            _lib.check(lib.dl_mlp_grad(ctypes.byref(args), _lib.stream_handle(self.device)),
+                       "dl_mlp_grad")
+            return self.loss
+        for t, shape in ((X, (N, P)), (G, (N, P))):
+            if tuple(t.shape) != shape or t.stride(1) != 1 or t.dtype != torch.float32:
+                raise ValueError(f"expected a row-major fp32 [{N}, {P}] tensor")
         aligned = all(t.data_ptr() % 16 == 0 for t in (X, G, data)) and \
             X.stride(0) % 4 == 0 and G.stride(0) % 4 == 0
         if self.path == "fused" and not aligned:
@@ -93,7 +109,7 @@ class BatchedANN:
         if self.path == "fused":
             args = _lib.DlMlpArgs(N, B, din, dh, dout, _lib.ptr(X), X.stride(0), _lib.ptr(data),
                                   B * din, _lib.ptr(labels), labels.stride(0), _lib.ptr(G),
-                                  G.stride(0), _lib.ptr(self.loss))
+                                  G.stride(0), _lib.ptr(self.loss), 0)
             _lib.check(lib.dl_mlp_grad(ctypes.byref(args), _lib.stream_handle(self.device)),
                        "dl_mlp_grad")
             return self.loss

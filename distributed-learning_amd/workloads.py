@@ -73,18 +73,20 @@ class MLPConsensusSGD:
     graph launch each instead of ~15 kernel launches from Python."""
 
     def __init__(self, ann, eng, data, labels, lr, deviation=True):
-        if eng.layout != "rows":
-            raise ValueError("the batched gradients read X row-major: use GossipEngine(layout='rows')")
+        if eng.layout == "tiled" and ann.path != "fused":
+            raise ValueError("the layered gradients read X row-major: use GossipEngine("
+                             "layout='rows') or the fused kernel")
         if eng.n != ann.N or eng.P < ann.P:
             raise ValueError("engine and model disagree on agents/params")
         import torch
         self.ann, self.eng = ann, eng
         self.data, self.labels = data, labels
         self.lr, self.deviation = float(lr), bool(deviation)
-        # The engine may carry zero padding columns [ann.P, eng.P) (a whole number of mix tiles:
-        # no ragged tail launch).  They stay exactly zero -- G is zero there and W 0 = 0 -- and
-        # add exact zeros to the deviation, so results are those of the unpadded round.
-        self.G = torch.zeros(ann.N, eng.P, dtype=torch.float32, device=eng.device)
+        # Row-major engines may carry zero padding columns [ann.P, eng.P) (a whole number of mix
+        # tiles: no ragged tail launch); the tiled layout zero-pads its last tile itself.  Padding
+        # stays exactly zero -- G is zero there and W 0 = 0 -- and adds exact zeros to the
+        # deviation, so results are those of the unpadded round.
+        self.G = torch.zeros_like(eng.X)
         self.graphs = None
         self._torch = torch
 
@@ -102,7 +104,10 @@ class MLPConsensusSGD:
 
     def step(self):
         P = self.ann.P
-        self.ann.gradients(self.eng.X[:, :P], self.data, self.labels, self.G[:, :P])
+        if self.eng.layout == "tiled":     # the fused kernel addresses the tiles directly
+            self.ann.gradients(self.eng.X, self.data, self.labels, self.G)
+        else:
+            self.ann.gradients(self.eng.X[:, :P], self.data, self.labels, self.G[:, :P])
         self.eng.round(G=self.G, lr=self.lr, deviation=self.deviation)
 
     def capture(self):

@@ -265,6 +265,9 @@ int dl_xent_grad(const float *Z, int64_t sZ, const int32_t *y, int64_t sY, float
  *   data [n_agents][batch][input_dim] (agent stride s_data), labels [n_agents][batch] int32 in
  *     [0, output_dim);  G [n_agents, ldg]: receives d loss_a / d params_a (same order; columns
  *     beyond the parameter count untouched);  loss nullable [n_agents]: mean cross-entropy.
+ *   tile_cols T > 0: X and G are instead in the column-tiled layout of dl_mix_args
+ *     ([ceil(P/T)][n_agents][T], T a power of two >= 4; ldx, ldg ignored), the resident layout
+ *     the fused round streams fastest.
  * X, data and G 16-byte aligned, ldx, ldg and s_data multiples of 4, G disjoint from X. */
 typedef struct dl_mlp_args {
     int32_t n_agents, batch, input_dim, hidden_dim, output_dim;
@@ -273,6 +276,7 @@ typedef struct dl_mlp_args {
     const int32_t *labels; int64_t s_labels;
     float *G; int64_t ldg;
     float *loss;
+    int32_t tile_cols;   /* 0 = row-major X, G;  T > 0 = column-tiled (see above) */
 } dl_mlp_args;
 int dl_mlp_grad(const dl_mlp_args *args, dl_stream_t stream);
 

@@ -46,8 +46,8 @@ int main() {
     CHECK(hipMemcpy(X, hx.data(), hx.size() * 4, hipMemcpyHostToDevice));
     CHECK(hipMemcpy(D, hd.data(), hd.size() * 4, hipMemcpyHostToDevice));
     CHECK(hipMemcpy(Y, hl.data(), hl.size() * 4, hipMemcpyHostToDevice));
-    CHECK(dl::allow_full_lds(reinterpret_cast<const void *>(dl::mlp_fused_kernel)));
-    dl::MlpArgs p{X, ld, D, (long)B * din, Y, B, G, ld, L, din, dh, dout, st};
+    CHECK(dl::allow_full_lds(reinterpret_cast<const void *>(dl::mlp_fused_kernel<false>)));
+    dl::MlpArgs p{X, ld, D, (long)B * din, Y, B, G, ld, L, din, dh, dout, 0, 0, st};
     int rate_khz = 0;
     CHECK(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, 0));
     const char *names[] = {"layer1 fwd", "fwd2", "fwd3", "logits+xent", "dW4+db4+dZ3", "dW3",
@@ -57,7 +57,7 @@ int main() {
     CHECK(hipEventCreate(&e1));
     for (int rep = 0; rep < 6; ++rep) {
         CHECK(hipEventRecord(e0));
-        hipLaunchKernelGGL(dl::mlp_fused_kernel, dim3(N), dim3(dl::NTHR),
+        hipLaunchKernelGGL(dl::mlp_fused_kernel<false>, dim3(N), dim3(dl::NTHR),
                            dl::LDS_FLOATS * sizeof(float), 0, p);
         CHECK(hipEventRecord(e1));
         CHECK(hipDeviceSynchronize());

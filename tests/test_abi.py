@@ -38,7 +38,10 @@ def test_struct_layout_matches_c(tmp_path):
                     'int main(void){printf("%zu %zu %zu %zu %zu %zu %zu\\n",'
                     'sizeof(dl_csr), sizeof(dl_mix_args), offsetof(dl_mix_args, W),'
                     'offsetof(dl_mix_args, lr), offsetof(dl_mix_args, mean),'
-                    'sizeof(dl_mix_plan), sizeof(dl_perron_args));return 0;}\n')
+                    'sizeof(dl_mix_plan), sizeof(dl_perron_args));'
+                    'printf("%zu %zu %zu %zu %zu\\n", sizeof(dl_sgd_args), offsetof(dl_sgd_args, lr),'
+                    'sizeof(dl_mlp_args), offsetof(dl_mlp_args, tile_cols), sizeof(dl_bgemm_args));'
+                    'return 0;}\n')
     exe = tmp_path / "layout"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(prog), "-o", str(exe)],
                    check=True)
@@ -46,7 +49,9 @@ def test_struct_layout_matches_c(tmp_path):
                                         check=True).stdout.split()]
     py = [ctypes.sizeof(_lib.DlCsr), ctypes.sizeof(_lib.DlMixArgs), _lib.DlMixArgs.W.offset,
           _lib.DlMixArgs.lr.offset, _lib.DlMixArgs.mean.offset, ctypes.sizeof(_lib.DlMixPlan),
-          ctypes.sizeof(_lib.DlPerronArgs)]
+          ctypes.sizeof(_lib.DlPerronArgs), ctypes.sizeof(_lib.DlSgdArgs),
+          _lib.DlSgdArgs.lr.offset, ctypes.sizeof(_lib.DlMlpArgs), _lib.DlMlpArgs.tile_cols.offset,
+          ctypes.sizeof(_lib.DlBgemmArgs)]
     assert c == py
 
 

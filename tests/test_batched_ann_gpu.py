@@ -150,3 +150,37 @@ def test_mlp_consensus_zero_padding_is_exact(cuda):
         res.append((eng.X[:, :P].clone(), eng.dev_sq.clone()))
     assert torch.equal(res[0][0], res[1][0])
     torch.testing.assert_close(res[0][1], res[1][1], rtol=1e-5, atol=0)
+
+
+def test_mlp_consensus_tiled_layout_matches_rows(cuda):
+    """c3 with X and G in the engine's column-tiled layout (the fused kernel addresses the tiles,
+    the round streams whole HBM blocks) gives the same parameters, bit for bit, as the
+    row-major layout; the deviation agrees to fp32 rounding (different reduction split)."""
+    from distributed_learning_amd import engine
+    from distributed_learning_amd.graph import from_edge_weights, random_regular_edges
+    from distributed_learning_amd.networks.batched_ann import BatchedANN
+    from distributed_learning_amd.workloads import MLPConsensusSGD
+    n, b = 48, 64
+    gen = torch.Generator(device=cuda).manual_seed(11)
+    bann = BatchedANN(n, b, 100, 60, 10, device=cuda)
+    assert bann.path == "fused"
+    P = bann.P
+    X0 = 0.1 * torch.randn(n, P, device=cuda, generator=gen)
+    data = torch.randn(n, b, 100, device=cuda, generator=gen)
+    labels = torch.randint(0, 10, (n, b), device=cuda, generator=gen, dtype=torch.int32)
+    edges = random_regular_edges(4, n, seed=4)
+    csr = from_edge_weights(edges, [0.2] * len(edges), list(range(n)))
+    res = {}
+    for layout in ("rows", "tiled"):
+        cols = P if layout == "tiled" else MLPConsensusSGD.padded_params(csr, P, cuda)
+        X = X0 if layout == "tiled" else torch.nn.functional.pad(X0, (0, cols - P))
+        eng = engine.GossipEngine(csr, cols, device=cuda, X=X, layout=layout)
+        assert eng.layout == layout
+        sgd = MLPConsensusSGD(bann, eng, data, labels, lr=0.1)
+        for _ in range(3):
+            sgd.step()
+        torch.cuda.synchronize()
+        res[layout] = (eng.rows()[:, :P].clone(), eng.dev_sq.clone(), sgd.loss.clone())
+    assert torch.equal(res["rows"][0], res["tiled"][0])
+    assert torch.equal(res["rows"][2], res["tiled"][2])
+    torch.testing.assert_close(res["rows"][1], res["tiled"][1], rtol=1e-5, atol=0)

@@ -683,6 +683,8 @@ int dl_mlp_grad(const dl_mlp_args *a, dl_stream_t stream) {
         return fail(DL_ERR_INVALID, "dl_mlp_grad: X, data, G must be 16-byte aligned with row "
                                     "strides % 4 == 0");
     const size_t tb = T ? (size_t)((P + T - 1) / T) * T * a->n_agents * 4 : 0;
+    if (T && tb / 4 > 0x7fffffff)   // the kernel addresses an agent's tiled row with 32-bit offsets
+        return fail(DL_ERR_UNSUPPORTED, "dl_mlp_grad: tiled X too large for 32-bit offsets");
     const size_t xb = T ? tb : ((size_t)a->n_agents - 1) * a->ldx * 4 + P * 4;
     const size_t gb = T ? tb : ((size_t)a->n_agents - 1) * a->ldg * 4 + P * 4;
     if (overlaps(a->X, xb, a->G, gb)) return fail(DL_ERR_INVALID, "dl_mlp_grad: G overlaps X");

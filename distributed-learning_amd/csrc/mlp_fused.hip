@@ -112,13 +112,14 @@ __device__ __forceinline__ void pipeline_db(int ns, Load load, Store store, Comp
 // One agent's row of X or G: parameter p -> element address, row-major (base + p) or in the
 // engine's column-tiled layout [ceil(P/T)][n_agents][T] (tile p >> sh, lane p & (T - 1)), so the
 // same kernel reads the tiled X the c3 round streams at copy speed.
+// Offsets are 32-bit (the ABI checks that every offset from an agent's base fits).
 template <bool TILED>
 struct PRow {
     float *base;        // row-major: X + a * ld;  tiled: X + a * T
-    int64_t tstride;    // tiled: n_agents * T
+    int tstride;        // tiled: n_agents * T
     int sh;             // tiled: log2 T
-    __device__ __forceinline__ float *at(int64_t p) const {
-        if constexpr (TILED) return base + (p >> sh) * tstride + (p & ((int64_t(1) << sh) - 1));
+    __device__ __forceinline__ float *at(int p) const {
+        if constexpr (TILED) return base + ((p >> sh) * tstride + (p & ((1 << sh) - 1)));
         return base + p;
     }
 };
@@ -127,12 +128,24 @@ struct PRow {
 template <bool TILED>
 struct ParMat {
     PRow<TILED> row;
-    int64_t off;
+    int off;
     int ld;
-    __device__ __forceinline__ float *at(int r, int c) const {
-        return row.at(off + (int64_t)r * ld + c);
-    }
+    __device__ __forceinline__ float *at(int r, int c) const { return row.at(off + r * ld + c); }
 };
+
+// Store a finished 32 x 32 MFMA tile: register r holds row i0 + (r & 3) + 8 (r >> 2) of this
+// lane's column j (C/D map); every store instruction writes two 128-B runs.  (Issuing these
+// stores interleaved with the next tile's MFMA chain measured slower: dW1 53 -> 64 us.)
+template <typename M>
+__device__ __forceinline__ void store_tile(const f32x16 &v, int i0, int j, const M &m, int rows,
+                                           int cols) {
+    if (j >= cols) return;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int i = i0 + (r & 3) + 8 * (r >> 2);
+        if (i < rows) *m.at(i, j) = v[r];
+    }
+}
 
 // plain row-major matrix (the agent's input batch)
 struct PlainMat {
@@ -329,7 +342,7 @@ template <typename M>
 __device__ __forceinline__ void weight_grad_hidden(const float *dZ, const float *Hin, int dh,
                                                    const M &gW, const M &gb) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    for (int t = wave; t < 25; t += 8) {    // one tile at a time: stores overlap the next tile
+    for (int t = wave; t < 25; t += 8) {    // one tile at a time (one accumulator)
         f32x16 acc;
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[r] = 0.f;
@@ -339,14 +352,7 @@ __device__ __forceinline__ void weight_grad_hidden(const float *dZ, const float 
             const int b = 2 * ks + (lane >> 5);
             acc = mfma32(dZ[b * LDH + ia], Hin[b * LDH + jb], acc);
         }
-        if (jb < dh) {
-            const int i0 = (t / 5) * 32 + 4 * (lane >> 5);
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int i = i0 + (r & 3) + 8 * (r >> 2);
-                if (i < dh) *gW.at(i, jb) = acc[r];
-            }
-        }
+        store_tile(acc, (t / 5) * 32 + 4 * (lane >> 5), jb, gW, dh, dh);
     }
     if (threadIdx.x < dh) {
         float s = 0.f;
@@ -386,8 +392,8 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     PRow<TILED> Xr, Gr;
     if constexpr (TILED) {
-        Xr = {const_cast<float *>(p.X) + ((int64_t)a << p.tsh), p.tstride, p.tsh};
-        Gr = {p.G + ((int64_t)a << p.tsh), p.tstride, p.tsh};
+        Xr = {const_cast<float *>(p.X) + ((int64_t)a << p.tsh), (int)p.tstride, p.tsh};
+        Gr = {p.G + ((int64_t)a << p.tsh), (int)p.tstride, p.tsh};
     } else {
         Xr = {const_cast<float *>(p.X) + (int64_t)a * p.ldx, 0, 0};
         Gr = {p.G + (int64_t)a * p.ldg, 0, 0};
@@ -396,11 +402,10 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
     // parameter offsets in the Mixer flatten order (fc1.w, fc1.b, fc2.w, fc2.b, ...)
     STAMP(0);
     if (p.stamps && threadIdx.x == 0) p.stamps[(int64_t)blockIdx.x * 16 + 14] = __builtin_amdgcn_s_memtime();
-    const int64_t o_w1 = 0, o_b1 = (int64_t)dh * din, o_w2 = o_b1 + dh, o_b2 = o_w2 + dh * dh,
-                  o_w3 = o_b2 + dh, o_b3 = o_w3 + dh * dh, o_w4 = o_b3 + dh,
-                  o_b4 = o_w4 + dout * dh;
+    const int o_w1 = 0, o_b1 = dh * din, o_w2 = o_b1 + dh, o_b2 = o_w2 + dh * dh,
+              o_w3 = o_b2 + dh, o_b3 = o_w3 + dh * dh, o_w4 = o_b3 + dh, o_b4 = o_w4 + dout * dh;
     using PM = ParMat<TILED>;
-    auto mat = [&](const PRow<TILED> &r, int64_t off, int ld) { return PM{r, off, ld}; };
+    auto mat = [&](const PRow<TILED> &r, int off, int ld) { return PM{r, off, ld}; };
 
     // zero all of LDS: K tails and padded tiles then read only finite values (zeros where
     // they meet a zero-filled staged operand), and the activation pads start at zero
@@ -455,7 +460,7 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
     // ---- logits Z = H3 W4^T + b4 (waves 0-3, one 16 x 16 tile each), W4 image [16][LDW4]
     for (int e = tid; e < 16 * LDW4; e += NTHR) {
         const int n = e / LDW4, k = e % LDW4;
-        stage[e] = (n < dout && k < dh) ? *Xr.at(o_w4 + (int64_t)n * dh + k) : 0.f;
+        stage[e] = (n < dout && k < dh) ? *Xr.at(o_w4 + n * dh + k) : 0.f;
     }
     __syncthreads();
     if (wave < 4) {
@@ -505,7 +510,7 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int i = 4 * (lane >> 4) + r;
-                if (i < dout && j < dh) *Gr.at(o_w4 + (int64_t)i * dh + j) = acc[r];
+                if (i < dout && j < dh) *Gr.at(o_w4 + i * dh + j) = acc[r];
             }
         }
         if (tid < dout) {
@@ -550,6 +555,7 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
             }
         };
         const int nc = (din + CW - 1) / CW;
+        const PM gw1 = mat(Gr, o_w1, din);
         load(0);
         for (int ci = 0; ci < nc; ++ci) {
 #pragma unroll
@@ -577,15 +583,9 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
                     acc = mfma32(H1[b * LDH + 32 * t + (lane & 31)], xs[b * LDC + nl], acc);
                 }
 #endif
-                const int j = c0 + nl;
-                if (j < din && MLP_PROBE_MODE != 4) {   // measurement only: 4 = no dW1 stores
-                    const int i0 = 32 * t + 4 * (lane >> 5);
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const int i = i0 + (r & 3) + 8 * (r >> 2);
-                        if (i < dh) *Gr.at(o_w1 + (int64_t)i * din + j) = acc[r];
-                    }
-                }
+#if MLP_PROBE_MODE != 4   // measurement only: 4 = no dW1 stores
+                store_tile(acc, 32 * t + 4 * (lane >> 5), c0 + nl, gw1, dh, din);
+#endif
             }
             __syncthreads();
         }

@@ -315,7 +315,7 @@ def run_c3(args, dev, rank, world):
                 "launch_ms": mix_ms}
     dominant = grad_roof if grad_ms >= mix_ms else mix_roof
     cpu = None
-    if not args.no_cpu:
+    if not args.no_cpu and world == 1:   # the CPU baseline is an N=1 figure
         v, cores, tg, tm = c3_cpu_baseline(ann, csr, lr)
         cpu = {"value": v, "unit": "steps/s", "cores": cores, "kind": "port",
                "sample": f"torch CPU autograd step of ANNModel on 16 of {n} agents (B={B}), "
@@ -525,7 +525,7 @@ def run_c5(args, dev, rank, world):
                 "kernel": "sgd_step_kernel + mix_tile_kernel (+dev_reduce)",
                 "bytes_per_launch": mix_bytes, "launch_ms": mix_ms}
     cpu = None
-    if not args.no_cpu:
+    if not args.no_cpu and world == 1:   # the CPU baseline is an N=1 figure
         v, cores, tg, tm = c5_cpu_baseline(wl, csr)
         cpu = {"value": v, "unit": "steps/s", "cores": cores, "kind": "port",
                "sample": f"torch CPU forward/backward + optim.SGD step of Wide_ResNet(16, 4) on 2 "
@@ -649,7 +649,7 @@ def main():
         traffic, traffic_src = traffic_from_profile(kname)
         ceiling, triad, ceiling_variants = copy_ceiling(dev)
         cpu = None
-        if not args.no_cpu:
+        if not args.no_cpu and world == 1:   # the CPU baseline is an N=1 figure
             cb = cpu_baseline(csr, n, P, min(args.cpu_cols, P), sgd, lr)
             cpu = {"value": cb["numpy"], "unit": "rounds/s", "cores": 1, "kind": "port",
                    "sample": f"{n} agents x {min(args.cpu_cols, P)} of {P} columns, same graph; "

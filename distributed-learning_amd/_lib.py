@@ -81,6 +81,8 @@ SIGNATURES = {
     "dl_mix_plan_shape": (_i32, [_i32, _i32, _i64, _i32, _i32, _i32, _i32, _i32,
                                  ctypes.POINTER(DlMixPlan)]),
     "dl_mix_round": (_i32, [ctypes.POINTER(DlMixArgs), _vp, _sz, _vp]),
+    "dl_mix_rounds_plan": (_i32, [ctypes.POINTER(DlMixArgs), ctypes.POINTER(DlMixPlan)]),
+    "dl_mix_rounds": (_i32, [ctypes.POINTER(DlMixArgs), _i32, _vp, _sz, _vp]),
     "dl_deviation_workspace_bytes": (_sz, [_i32, _i64]),
     "dl_deviation": (_i32, [_vp, _i64, _i32, _i64, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "dl_deviation_tiled": (_i32, [_vp, _i32, _i64, _i32, _vp, _vp, _vp, _vp, _sz, _vp]),

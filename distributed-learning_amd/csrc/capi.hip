@@ -312,11 +312,124 @@ int zero_deviation(int32_t n_rows, float *dev_sq, float *dev_max, hipStream_t s)
     return DL_OK;
 }
 
+// Configuration of the multi-round kernel: two tile images of all agents in LDS beside the CSR.
+// Returns DL_ERR_UNSUPPORTED (no message needed by callers that fall back) when it cannot run.
+int plan_rounds(const dl_mix_args *a, Plan *pl) {
+    std::memset(pl, 0, sizeof *pl);
+    const int32_t R = a->W.n_rows;
+    const bool want_dev = a->dev_sq || a->dev_max || a->mean;
+    pl->dev = want_dev;
+    if (a->n_halo > 0)
+        return fail(DL_ERR_UNSUPPORTED, "dl_mix_rounds: halo rows need one exchange per round");
+    if (want_dev && !a->W.doubly_stochastic)
+        return fail(DL_ERR_UNSUPPORTED, "dl_mix_rounds: the fused final deviation needs a doubly "
+                                        "stochastic W");
+    const int reg = a->W.uniform_row_nnz > 0 ? 1 : 0;
+    const int32_t n_w = (reg && a->W.shared_row_weights) ? a->W.uniform_row_nnz : a->W.nnz;
+    const uint32_t csr = dl::csr_lds_bytes(R, a->W.nnz, reg, n_w);
+    if (csr == 0 || R > 65535) return fail(DL_ERR_UNSUPPORTED, "dl_mix_rounds: CSR too large");
+    auto fits = [&](int c) {
+        const int64_t tile = (int64_t)R * c * 16;
+        const int64_t scratch = want_dev ? (int64_t)(dl::kTileThreads / 64) * c * 16 : 0;
+        return (int64_t)R * c <= (int64_t)dl::kRowsPerThread * dl::kTileThreads &&
+               2 * tile + csr + scratch <= dl::kLdsBytes;
+    };
+    int c = 0;
+    if (a->tile_cols > 0) {
+        c = a->tile_cols / 4;
+        if (!fits(c))
+            return fail(DL_ERR_UNSUPPORTED, "dl_mix_rounds: two %d-column tiles of %d rows do "
+                                            "not fit LDS", a->tile_cols, R);
+    } else {
+        for (int cc = next_pow2_chunks(a->n_params); cc >= 1; cc >>= 1)
+            if (fits(cc) && a->n_params % (4 * cc) == 0) {
+                c = cc;
+                break;
+            }
+        if (c == 0)
+            return fail(DL_ERR_UNSUPPORTED, "dl_mix_rounds: no full-tile row-major configuration");
+    }
+    const int64_t T = 4 * c;
+    const int64_t n_tiles = (a->n_params + T - 1) / T;
+    const int64_t tile = (int64_t)R * c * 16;
+    pl->chunks = c;
+    pl->csr_off = (uint32_t)(2 * tile);
+    pl->scratch_off = (uint32_t)(2 * tile + csr);
+    pl->pub.path = 3;
+    pl->pub.tile_cols = (int32_t)T;
+    pl->pub.grid = (int32_t)(n_tiles < device_cus() ? n_tiles : device_cus());
+    pl->pub.lds_bytes = (int32_t)(2 * tile + csr +
+                                  (want_dev ? (dl::kTileThreads / 64) * c * 16 : 0));
+    pl->pub.n_tiles = (int32_t)n_tiles;
+    pl->pub.regular = reg;
+    return DL_OK;
+}
+
 }  // namespace
 
 extern "C" {
 
 int dl_abi_version(void) { return DLAMD_ABI_VERSION; }
+
+int dl_mix_rounds_plan(const dl_mix_args *args, dl_mix_plan *plan) {
+    g_err.clear();
+    if (!plan) return fail(DL_ERR_INVALID, "dl_mix_rounds_plan: plan is NULL");
+    int rc = check_mix_args(args);
+    if (rc) return rc;
+    Plan pl;
+    rc = plan_rounds(args, &pl);
+    if (rc) return rc;
+    *plan = pl.pub;
+    return DL_OK;
+}
+
+int dl_mix_rounds(const dl_mix_args *args, int32_t rounds, void *workspace, size_t ws_bytes,
+                  dl_stream_t stream) {
+    g_err.clear();
+    int rc = check_mix_args(args);
+    if (rc) return rc;
+    if (rounds < 1) return fail(DL_ERR_INVALID, "dl_mix_rounds: rounds must be >= 1");
+    Plan pl;
+    rc = plan_rounds(args, &pl);
+    if (rc) return rc;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int32_t Nr = args->W.n_rows;
+    dl::TileArgs t = tile_args(args);
+    if (!t.vec)
+        return fail(DL_ERR_UNSUPPORTED, "dl_mix_rounds: operands must be 16-byte aligned float4 "
+                                        "rows");
+    const int64_t T = pl.pub.tile_cols;
+    if (t.tiled) {
+        t.xts = t.gts = t.yts = (int64_t)Nr * T * 4;
+        t.xrs = t.grs = t.yrs = (uint32_t)(T * 4);
+    } else {
+        t.xts = t.gts = t.yts = T * 4;
+        t.xrs = (uint32_t)(args->ldx * 4);
+        t.grs = (uint32_t)(args->ldg * 4);
+        t.yrs = (uint32_t)(args->ldy * 4);
+    }
+    t.n_tiles = pl.pub.n_tiles;
+    t.col_base = 0;
+    t.csr_off = pl.csr_off;
+    t.scratch_off = pl.scratch_off;
+    char *ws = static_cast<char *>(workspace);
+    if (pl.dev) {
+        const size_t need = align_up((size_t)pl.pub.grid * Nr * 4);
+        if (!ws || (reinterpret_cast<uintptr_t>(ws) & 15u) || ws_bytes < need)
+            return fail(DL_ERR_WORKSPACE, "dl_mix_rounds: deviation outputs need a 16-byte "
+                                          "aligned workspace of %zu bytes", need);
+        t.dev_partial = reinterpret_cast<float *>(ws);
+    }
+    hipError_t e = dl::launch_mix_multi(t, pl.chunks, rounds, args->g != nullptr, pl.dev,
+                                        pl.pub.grid, pl.pub.lds_bytes, s);
+    if (e != hipSuccess) return hip_fail(e, "mix_multi_kernel launch");
+    if (pl.dev) {
+        if (Nr <= 1) return zero_deviation(Nr, args->dev_sq, args->dev_max, s);
+        e = dl::launch_dev_reduce(t.dev_partial, pl.pub.grid, Nr, args->dev_sq, args->dev_max, s);
+        if (e != hipSuccess) return hip_fail(e, "dev_reduce launch");
+    }
+    return DL_OK;
+}
 
 const char *dl_last_error(void) { return g_err.c_str(); }
 

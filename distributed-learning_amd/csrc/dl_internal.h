@@ -60,6 +60,11 @@ uint32_t csr_lds_bytes(int32_t n_rows, int32_t nnz, int32_t regular, int32_t n_w
 hipError_t launch_mix_tile(const TileArgs &a, int chunks, bool sgd, bool dev, bool mix, int grid,
                            int lds_bytes, bool fast, hipStream_t s);
 hipError_t launch_mix_gather(const TileArgs &a, bool sgd, hipStream_t s);
+// rows per thread (KV) the FAST tile kernels use for n_src rows at `chunks` float4 per row
+int tile_passes(int chunks, int n_src, bool fast);
+// K rounds of mixing on LDS-resident tiles (mix_multi.hip); FAST tiles only, no halo rows
+hipError_t launch_mix_multi(const TileArgs &a, int chunks, int rounds, bool sgd, bool dev,
+                            int grid, int lds, hipStream_t s);
 hipError_t launch_dev_reduce(const float *partial, int nparts, int n_rows, float *dev_sq,
                              float *dev_max, hipStream_t s);
 hipError_t launch_column_sum(const float *x, int64_t ldx, int n_rows, int64_t n_params,

@@ -1,0 +1,276 @@
+// Multi-round gossip mixing in one HBM pass (gfx950): Y = W^K (X - lr G) for K >= 1 rounds.
+//
+// `Mixer.mix(times=K)` (utils/consensus_simple/mixer.py:18-38, eps=None) runs K consecutive
+// rounds of `_mix_params_once` (:43-49) with nothing in between, and pure gossip averaging (the
+// BASELINE c2 config) is exactly that.  The mix is column-independent: column p of X' depends
+// only on column p of X.  So a workgroup that holds a column tile of ALL agents in LDS can run
+// every one of the K rounds on it before writing it back: HBM sees each element of X (and G) read
+// once and Y written once per K rounds instead of per round, and the rounds run at LDS speed.
+// Two tile images ping-pong in LDS (round r reads one, writes the other, one barrier per round);
+// the last round writes HBM directly from registers (non-temporal) and, for doubly stochastic W,
+// accumulates the final deviation against the column mean of the staged tile (mean(W t) =
+// mean(t)).  Every round folds in CSR order with separate fp32 products and sums
+// (-ffp-contract=off), so K rounds here are bit-identical to K launches of the one-round kernel
+// and to K calls of the reference's fold.  The next tile's X (and G) rows are prefetched into
+// registers while the current tile's rounds run.
+#include "dl_internal.h"
+
+namespace dl {
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float4 mm_zero4() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+
+__device__ __forceinline__ float4 mm_nt_load4(const float4 *p) {
+    const f32x4 x = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(p));
+    return make_float4(x.x, x.y, x.z, x.w);
+}
+
+__device__ __forceinline__ void mm_nt_store4(float4 v, float4 *p) {
+    f32x4 x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, reinterpret_cast<f32x4 *>(p));
+}
+
+__device__ __forceinline__ const float4 *mm_at(const void *base, uint32_t off) {
+    return reinterpret_cast<const float4 *>(reinterpret_cast<const char *>(base) + off);
+}
+
+// C: float4 chunks per tile row (T = 4C columns); KV: rows per thread (agents s + k*SLOTS);
+// SGD: local step x - lr g applied once, before the first round; DEV: final deviation.
+// FAST tiles only (every tile full and 16-byte aligned; the column-tiled layout always is).
+template <int C, int KV, bool SGD, bool DEV>
+__global__ void __launch_bounds__(kTileThreads) mix_multi_kernel(TileArgs a, int rounds) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int NT = kTileThreads;
+    constexpr int SLOTS = NT / C;
+    const int tid = threadIdx.x;
+    const int c = tid & (C - 1);
+    const int s = tid / C;
+    const int Nr = a.n_rows;
+    const int nnz = a.nnz;
+    float4 *img0 = reinterpret_cast<float4 *>(smem);
+    float4 *img1 = img0 + (size_t)Nr * C;
+    float *lw = reinterpret_cast<float *>(smem + a.csr_off);
+    uint16_t *lcol = reinterpret_cast<uint16_t *>(smem + a.csr_off + 4u * (uint32_t)a.n_w);
+    uint16_t *lrp = lcol + nnz;
+    float4 *scratch = reinterpret_cast<float4 *>(smem + a.scratch_off);
+    for (int i = tid; i < a.n_w; i += NT) lw[i] = a.w[i];
+    for (int i = tid; i < nnz; i += NT) lcol[i] = (uint16_t)a.col[i];
+    const int reg = a.regular;
+    if (!reg)
+        for (int i = tid; i <= Nr; i += NT) lrp[i] = (uint16_t)a.rowptr[i];
+    const bool wshared = a.n_w != nnz;
+
+    uint32_t ox = (uint32_t)s * a.xrs + 16u * c;
+    const uint32_t sx = (uint32_t)SLOTS * a.xrs;
+    uint32_t og = SGD ? (uint32_t)s * a.grs + 16u * c : 0u;
+    const uint32_t sg = SGD ? (uint32_t)SLOTS * a.grs : 0u;
+    uint32_t oy = (uint32_t)s * a.yrs + 16u * c;
+    const uint32_t sy = (uint32_t)SLOTS * a.yrs;
+    auto tile_base = [&](const void *p, int64_t ts, int tile_id) {
+        return reinterpret_cast<const char *>(p) + (a.tiled ? 0 : a.col_base * 4) +
+               (int64_t)tile_id * ts;
+    };
+
+    float4 px[KV], pg[KV];
+    auto prefetch = [&](int tile_id) {
+        const char *xt = tile_base(a.x, a.xts, tile_id);
+        const char *gt = SGD ? tile_base(a.g, a.gts, tile_id) : nullptr;
+#pragma unroll
+        for (int k = 0; k < KV; ++k) {
+            const bool ok = s + k * SLOTS < Nr;   // ragged last pass re-reads row 0 (L1 hit)
+            px[k] = mm_nt_load4(mm_at(xt, ok ? ox + k * sx : 16u * c));
+            if (SGD) pg[k] = mm_nt_load4(mm_at(gt, ok ? og + k * sg : 16u * c));
+        }
+    };
+
+    // one agent's output chunk from an LDS image: left fold in CSR order from +0.0 (mixer.py:47)
+    auto mix_row = [&](const float4 *src, int ag) {
+        int e0, e1;
+        if (reg) {
+            e0 = ag * reg;
+            e1 = e0 + reg;
+        } else {
+            e0 = lrp[ag];
+            e1 = lrp[ag + 1];
+        }
+        const float *wr = wshared ? lw - e0 : lw;
+        float4 acc = mm_zero4();
+        for (int e = e0; e < e1; ++e) {
+            const float w = wr[e];
+            const float4 v = src[lcol[e] * C + c];
+            acc.x = acc.x + w * v.x;
+            acc.y = acc.y + w * v.y;
+            acc.z = acc.z + w * v.z;
+            acc.w = acc.w + w * v.w;
+        }
+        return acc;
+    };
+
+    constexpr int ND = KV <= C ? 1 : KV / C;
+    float dacc[ND];
+#pragma unroll
+    for (int k = 0; k < ND; ++k) dacc[k] = 0.f;
+
+    int tile_id = blockIdx.x;
+    if (tile_id < a.n_tiles) prefetch(tile_id);
+    for (; tile_id < a.n_tiles; tile_id += gridDim.x) {
+        asm volatile("" : "+v"(ox), "+v"(og), "+v"(oy));
+        const int nxt = tile_id + gridDim.x;
+        float4 cst = mm_zero4();
+#pragma unroll
+        for (int k = 0; k < KV; ++k) {
+            const int r = s + k * SLOTS;
+            float4 t = px[k];
+            if (SGD) {
+                t.x = t.x - a.lr * pg[k].x;
+                t.y = t.y - a.lr * pg[k].y;
+                t.z = t.z - a.lr * pg[k].z;
+                t.w = t.w - a.lr * pg[k].w;
+            }
+            if (r < Nr) {
+                img0[r * C + c] = t;
+                if (DEV) {
+                    cst.x += t.x;
+                    cst.y += t.y;
+                    cst.z += t.z;
+                    cst.w += t.w;
+                }
+            }
+        }
+        if (DEV) {   // column sums of the staged tile (W doubly stochastic: the final mean)
+#pragma unroll
+            for (int m = C; m < 64; m <<= 1) {
+                cst.x += __shfl_xor(cst.x, m);
+                cst.y += __shfl_xor(cst.y, m);
+                cst.z += __shfl_xor(cst.z, m);
+                cst.w += __shfl_xor(cst.w, m);
+            }
+            if ((tid & 63) < C) scratch[(tid >> 6) * C + (tid & 63)] = cst;
+        }
+        __syncthreads();
+        float4 mean = mm_zero4();
+        if (DEV) {
+#pragma unroll
+            for (int wv = 0; wv < NT / 64; ++wv) {
+                const float4 q = scratch[wv * C + c];
+                mean.x += q.x;
+                mean.y += q.y;
+                mean.z += q.z;
+                mean.w += q.w;
+            }
+            const float n = (float)Nr;
+            mean.x = mean.x / n;
+            mean.y = mean.y / n;
+            mean.z = mean.z / n;
+            mean.w = mean.w / n;
+        }
+        if (nxt < a.n_tiles) prefetch(nxt);   // lands while this tile's rounds run in LDS
+        const float4 *src = img0;
+        float4 *dst = img1;
+        for (int r = 0; r + 1 < rounds; ++r) {
+#pragma unroll 1
+            for (int k = 0; k < KV; ++k) {
+                const int ag = s + k * SLOTS;
+                if (ag < Nr) dst[ag * C + c] = mix_row(src, ag);
+            }
+            __syncthreads();
+            const float4 *t = src;
+            src = dst;
+            dst = const_cast<float4 *>(t);
+        }
+        const char *yt = tile_base(a.y, a.yts, tile_id);
+#pragma unroll 1
+        for (int k = 0; k < KV; ++k) {
+            const int ag = s + k * SLOTS;
+            if (ag < Nr) {
+                const float4 y = mix_row(src, ag);
+                float4 *py = const_cast<float4 *>(mm_at(yt, oy + (uint32_t)k * sy));
+                if (a.nt_store)
+                    mm_nt_store4(y, py);
+                else
+                    *py = y;
+                if (DEV) {
+                    const float dx = y.x - mean.x, dy = y.y - mean.y;
+                    const float dz = y.z - mean.z, dw = y.w - mean.w;
+                    float v = (dx * dx + dy * dy) + (dz * dz + dw * dw);
+#pragma unroll
+                    for (int m = 1; m < C; m <<= 1) v += __shfl_xor(v, m);
+                    const bool mine = (k % C) == c;
+#pragma unroll
+                    for (int j = 0; j < ND; ++j) dacc[j] += (mine && j == k / C) ? v : 0.f;
+                }
+            }
+        }
+        if (DEV && a.mean != nullptr && s == 0) {
+            const int64_t col0 = a.col_base + (int64_t)tile_id * 4 * C + 4 * c;
+            *reinterpret_cast<float4 *>(a.mean + col0) = mean;
+        }
+        __syncthreads();   // both images and the scratch are rewritten by the next tile
+    }
+    if (DEV) {
+#pragma unroll
+        for (int j = 0; j < ND; ++j) {
+            const int k = j * C + c;
+            const int ag = s + k * SLOTS;
+            if (k < KV && ag < Nr) a.dev_partial[(int64_t)blockIdx.x * Nr + ag] = dacc[j];
+        }
+    }
+}
+
+template <int C, int KV>
+hipError_t launch_kv(const TileArgs &a, int rounds, bool sgd, bool dev, int grid, int lds,
+                     hipStream_t s) {
+    const void *k;
+    if (sgd)
+        k = dev ? reinterpret_cast<const void *>(mix_multi_kernel<C, KV, true, true>)
+                : reinterpret_cast<const void *>(mix_multi_kernel<C, KV, true, false>);
+    else
+        k = dev ? reinterpret_cast<const void *>(mix_multi_kernel<C, KV, false, true>)
+                : reinterpret_cast<const void *>(mix_multi_kernel<C, KV, false, false>);
+    hipError_t e = allow_full_lds(k);
+    if (e != hipSuccess) return e;
+    if (sgd) {
+        if (dev)
+            hipLaunchKernelGGL((mix_multi_kernel<C, KV, true, true>), dim3(grid), dim3(kTileThreads),
+                               lds, s, a, rounds);
+        else
+            hipLaunchKernelGGL((mix_multi_kernel<C, KV, true, false>), dim3(grid), dim3(kTileThreads),
+                               lds, s, a, rounds);
+    } else {
+        if (dev)
+            hipLaunchKernelGGL((mix_multi_kernel<C, KV, false, true>), dim3(grid),
+                               dim3(kTileThreads), lds, s, a, rounds);
+        else
+            hipLaunchKernelGGL((mix_multi_kernel<C, KV, false, false>), dim3(grid),
+                               dim3(kTileThreads), lds, s, a, rounds);
+    }
+    return hipGetLastError();
+}
+
+template <int C>
+hipError_t launch_c(const TileArgs &a, int rounds, bool sgd, bool dev, int grid, int lds,
+                    hipStream_t s) {
+    const int kv = tile_passes(C, a.n_rows, true);
+    if (kv <= 2) return launch_kv<C, 2>(a, rounds, sgd, dev, grid, lds, s);
+    if (kv <= 4) return launch_kv<C, 4>(a, rounds, sgd, dev, grid, lds, s);
+    return launch_kv<C, 8>(a, rounds, sgd, dev, grid, lds, s);
+}
+
+}  // namespace
+
+hipError_t launch_mix_multi(const TileArgs &a, int chunks, int rounds, bool sgd, bool dev,
+                            int grid, int lds, hipStream_t s) {
+    switch (chunks) {
+        case 1: return launch_c<1>(a, rounds, sgd, dev, grid, lds, s);
+        case 2: return launch_c<2>(a, rounds, sgd, dev, grid, lds, s);
+        case 4: return launch_c<4>(a, rounds, sgd, dev, grid, lds, s);
+        case 8: return launch_c<8>(a, rounds, sgd, dev, grid, lds, s);
+        case 16: return launch_c<16>(a, rounds, sgd, dev, grid, lds, s);
+        case 32: return launch_c<32>(a, rounds, sgd, dev, grid, lds, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace dl

@@ -166,6 +166,43 @@ def mix_round(W: DeviceCsr, X, Y, G=None, lr=0.0, halo=None, dev_sq=None, dev_ma
                "dl_mix_round")
 
 
+def mix_rounds(W: DeviceCsr, X, Y, rounds, G=None, lr=0.0, dev_sq=None, dev_max=None, mean=None,
+               workspace: Workspace = None, tiled=None):
+    """``rounds`` mixing rounds in one HBM pass: Y = W^rounds (X - lr G) (dl_mix_rounds; the local
+    step once, before the first round).  Returns False, launching nothing, when the multi-round
+    kernel does not fit this graph/layout (the caller then loops ``mix_round``)."""
+    lib = _lib.load()
+    if tiled is not None:
+        P = tiled[0]
+        args = mix_args_tiled(W, tiled[0], tiled[1], X, Y, G, lr, dev_sq, dev_max, mean)
+    else:
+        P = X.shape[1]
+        args = mix_args(W, X, Y, G, lr, None, dev_sq, dev_max, mean)
+    workspace = workspace or Workspace(W.device)
+    wp, wn = workspace.ptr_size(lib.dl_mix_workspace_bytes(W.n_rows, 0, P))
+    rc = lib.dl_mix_rounds(ctypes.byref(args), int(rounds), wp, wn, _lib.stream_handle(W.device))
+    if rc == _lib.DL_ERR_UNSUPPORTED:
+        return False
+    _lib.check(rc, "dl_mix_rounds")
+    return True
+
+
+def rounds_plan(W: DeviceCsr, X, Y, deviation=False, tiled=None):
+    """dl_mix_rounds_plan: the multi-round configuration, or None when it does not fit."""
+    lib = _lib.load()
+    dummy = torch.empty(1, dtype=torch.float32, device=W.device) if deviation else None
+    if tiled is not None:
+        args = mix_args_tiled(W, tiled[0], tiled[1], X, Y, None, 0.0, dummy, dummy, None)
+    else:
+        args = mix_args(W, X, Y, None, 0.0, None, dummy, dummy, None)
+    plan = _lib.DlMixPlan()
+    rc = lib.dl_mix_rounds_plan(ctypes.byref(args), ctypes.byref(plan))
+    if rc == _lib.DL_ERR_UNSUPPORTED:
+        return None
+    _lib.check(rc, "dl_mix_rounds_plan")
+    return {f: getattr(plan, f) for f, _ in plan._fields_}
+
+
 def mix_plan(W: DeviceCsr, X, Y, G=None, deviation=False):
     lib = _lib.load()
     dummy = torch.empty(1, dtype=torch.float32, device=W.device) if deviation else None
@@ -328,6 +365,25 @@ class GossipEngine:
                   dev_max=self.dev_max if deviation else None, mean=mean, workspace=self.ws,
                   tiled=(self.P, self.T) if self.layout == "tiled" else None)
         self.X, self.Y = self.Y, self.X
+
+    def rounds(self, k, G=None, lr=0.0, deviation=False, mean=None):
+        """k rounds  X <- W^k (X - lr G)  (the local step once, before the first round): one
+        dl_mix_rounds pass when the multi-round kernel fits, else k one-round launches.  With
+        ``deviation`` the final iterate's ||x_a - mean||^2 lands in ``dev_sq``."""
+        k = int(k)
+        if k < 1:
+            return
+        tiled = (self.P, self.T) if self.layout == "tiled" else None
+        if mix_rounds(self.W, self.X, self.Y, k, G=G, lr=lr,
+                      dev_sq=self.dev_sq if deviation else None,
+                      dev_max=self.dev_max if deviation else None, mean=mean, workspace=self.ws,
+                      tiled=tiled):
+            self.X, self.Y = self.Y, self.X
+            return
+        for i in range(k):
+            last = i == k - 1
+            self.round(G=G if i == 0 else None, lr=lr if i == 0 else 0.0,
+                       deviation=deviation and last, mean=mean if last else None)
 
     def deviation(self, mean_out=None):
         if self.layout == "tiled":

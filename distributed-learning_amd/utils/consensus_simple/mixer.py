@@ -5,8 +5,10 @@ difference is where the work runs.  Per ``mix()`` call the models are flattened 
 device matrix X[N, P] (rows in ``topology`` key order, mixer.py:26/69); each round is one
 ``dl_mix_round`` launch (the reference's ``_mix_params_once`` fold, :43-49, bit-identical in
 fp32), and when ``eps`` is given the same launch also produces the per-agent deviation
-(:51-66) so the stop test costs one 4-byte readback per round.  The results are written back
-into the models once at the end (:34-35, 71-76).
+(:51-66) so the stop test costs one 4-byte readback per round.  With ``eps=None`` the ``times``
+rounds have nothing in between, so they run as ONE ``dl_mix_rounds`` pass (every round on
+LDS-resident column tiles, bit-identical to ``times`` single rounds).  The results are written
+back into the models once at the end (:34-35, 71-76).
 """
 import numpy as np
 import torch
@@ -57,6 +59,16 @@ class Mixer(object):
             dev_max = torch.empty(1, dtype=torch.float32, device=X.device)
 
             stopping_criterion = self._update_stopping_criterion(X, times_done, times, eps)
+            if not stopping_criterion and eps is None:
+                # times rounds, no stop test in between: one pass over HBM (rows padded with
+                # zero columns to whole tiles; zeros mix to zeros)
+                P = X.shape[1]
+                Pp = -(-P // 64) * 64
+                Xp = torch.nn.functional.pad(X, (0, Pp - P)) if Pp != P else X
+                Yp = torch.empty_like(Xp)
+                if _engine.mix_rounds(W, Xp, Yp, times, workspace=self._wspace()):
+                    X, times_done = Yp[:, :P], int(times)
+                    stopping_criterion = True
             while not stopping_criterion:
                 _engine.mix_round(W, X, Y, dev_sq=dev_sq if fused_dev else None,
                                   dev_max=dev_max if fused_dev else None, workspace=self._wspace())

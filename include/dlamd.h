@@ -95,7 +95,8 @@ typedef struct dl_mix_args {
 
 /* Which kernel configuration dl_mix_round picks (introspection for tests and the bench). */
 typedef struct dl_mix_plan {
-    int32_t path;       /* 1 = LDS tile kernel (all agents x T columns per tile), 2 = gather kernel */
+    int32_t path;       /* 1 = LDS tile kernel (all agents x T columns per tile), 2 = gather kernel,
+                           3 = multi-round LDS kernel (dl_mix_rounds) */
     int32_t tile_cols;  /* T: columns per tile (path 1) */
     int32_t grid;       /* workgroups launched */
     int32_t lds_bytes;  /* dynamic LDS per workgroup */
@@ -116,6 +117,22 @@ int dl_mix_plan_shape(int32_t n_rows, int32_t n_halo, int64_t n_params, int32_t 
                       int32_t tile_cols, dl_mix_plan *plan);
 int dl_mix_plan_query(const dl_mix_args *args, dl_mix_plan *plan);
 int dl_mix_round(const dl_mix_args *args, void *workspace, size_t ws_bytes, dl_stream_t stream);
+
+/* `rounds` consecutive mixing rounds in ONE pass over HBM:  y = W^rounds (x - lr g).
+ * Replaces `Mixer.mix(times=rounds)` with eps=None (mixer.py:18-38: `times` calls of
+ * _mix_params_once, :43-49, nothing in between) and pure gossip averaging (BASELINE c2).  The
+ * mix is column-independent, so each workgroup runs every round on an LDS-resident tile of all
+ * agents before writing it back: HBM traffic is that of one round, whatever `rounds` is.  Bit-
+ * identical to `rounds` calls of dl_mix_round (same fold order each round).  g (nullable): the
+ * local step is applied once, before the first round.  dev_sq / dev_max / mean describe the
+ * final iterate and need a doubly stochastic W.  Needs two tile images of all agents in LDS, no
+ * halo rows, 16-byte aligned operands and (row-major) n_params a multiple of the tile width;
+ * otherwise returns DL_ERR_UNSUPPORTED and the caller loops dl_mix_round.  Workspace:
+ * dl_mix_workspace_bytes (deviation only).  dl_mix_rounds_plan reports the configuration
+ * (path 3) or DL_ERR_UNSUPPORTED. */
+int dl_mix_rounds_plan(const dl_mix_args *args, dl_mix_plan *plan);
+int dl_mix_rounds(const dl_mix_args *args, int32_t rounds, void *workspace, size_t ws_bytes,
+                  dl_stream_t stream);
 
 /* Deviation of x from its column mean: dev_sq[a] = ||x_a - mean||^2, dev_max = max sqrt(dev_sq).
  * mean_in nullable: when given (e.g. a global mean all-reduced across GPUs) it is used instead

@@ -1,0 +1,123 @@
+"""GPU parity of the multi-round kernel (dl_mix_rounds: K rounds on LDS-resident tiles, one HBM
+pass) against K one-round launches, the reference-generated fixtures and the Mixer drop-in.
+Mixing must be bit-exact; the final deviation within 1e-5 relative."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import mixer_ref as M
+from test_mix_gpu import bits, check_dev, dev_floor, graph_csr
+
+pytestmark = pytest.mark.gpu
+
+
+def engine():
+    from distributed_learning_amd import engine as E
+    return E
+
+
+@pytest.mark.parametrize("case,rounds", [("a", [10, 200]), ("b", [10])])
+def test_reference_fixture_in_one_pass(golden, cuda, case, rounds):
+    """X after 10 / 200 rounds of the reference's Mixer._mix_params_once, from one launch."""
+    from distributed_learning_amd.graph import Csr
+    E = engine()
+    d = golden("mix_rr4_n64.npz")
+    csr = Csr(d[f"{case}_rowptr"], d[f"{case}_cols"], d[f"{case}_w"])
+    for r in rounds:
+        eng = E.GossipEngine(csr, d[f"{case}_X0"].shape[1], device=cuda,
+                             X=torch.from_numpy(d[f"{case}_X0"]).to(cuda))
+        plan = E.rounds_plan(eng.W, eng.X, eng.Y, tiled=(eng.P, eng.T))
+        assert plan is not None and plan["path"] == 3
+        eng.rounds(r)
+        torch.cuda.synchronize()
+        assert np.array_equal(bits(eng.rows().cpu().numpy()), bits(d[f"{case}_X{r}"])), r
+
+
+@pytest.mark.parametrize("n,P,deg,layout", [(64, 4096, 4, "tiled"), (1024, 4096, 4, "tiled"),
+                                            (100, 1024, 5, "rows"), (256, 2048, 8, "tiled"),
+                                            (3, 64, 2, "rows"), (1500, 512, 3, "tiled")])
+@pytest.mark.parametrize("sgd", [False, True])
+def test_k_rounds_equal_k_launches(cuda, n, P, deg, layout, sgd):
+    E = engine()
+    rng = np.random.default_rng(n + P)
+    csr = graph_csr(n, deg, seed=n)
+    X = rng.standard_normal((n, P), dtype=np.float32)
+    G = rng.standard_normal((n, P), dtype=np.float32) if sgd else None
+    K = 7
+    a = E.GossipEngine(csr, P, device=cuda, X=torch.from_numpy(X).to(cuda), layout=layout)
+    b = E.GossipEngine(csr, P, device=cuda, X=torch.from_numpy(X).to(cuda), layout=layout)
+    Ga = a.layout_like(torch.from_numpy(G).to(cuda)) if sgd else None
+    tiled = (a.P, a.T) if layout == "tiled" else None
+    assert E.rounds_plan(a.W, a.X, a.Y, tiled=tiled) is not None
+    a.rounds(K, G=Ga, lr=0.01)
+    for i in range(K):
+        b.round(G=Ga if i == 0 else None, lr=0.01 if i == 0 else 0.0)
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(a.rows().cpu().numpy()), bits(b.rows().cpu().numpy()))
+
+
+@pytest.mark.parametrize("layout", ["tiled", "rows"])
+def test_final_deviation_doubly_stochastic(cuda, layout):
+    from distributed_learning_amd.graph import best_constant_weight, random_regular_edges, \
+        uniform_weights
+    E = engine()
+    n, P = 512, 8192
+    edges = random_regular_edges(4, n, seed=1)
+    csr = uniform_weights(edges, best_constant_weight(edges))
+    assert csr.doubly_stochastic and csr.shared_row_weights
+    rng = np.random.default_rng(7)
+    X = rng.standard_normal((n, P), dtype=np.float32)
+    eng = E.GossipEngine(csr, P, device=cuda, X=torch.from_numpy(X).to(cuda), layout=layout)
+    mean = torch.empty(P, device=cuda)
+    eng.rounds(5, deviation=True, mean=mean)
+    torch.cuda.synchronize()
+    Y = eng.rows().cpu().numpy()
+    Yw = X
+    for _ in range(5):
+        Yw = M.mix_once(Yw, csr.rowptr, csr.col, csr.w)
+    assert np.array_equal(bits(Y), bits(Yw))
+    check_dev(Y, eng.dev_sq.cpu().numpy(), float(eng.dev_max.item()), mean.cpu().numpy())
+
+
+def test_unsupported_falls_back_to_single_rounds(cuda):
+    """4096 agents: two tile images do not fit LDS beside the CSR -> k one-round launches."""
+    from distributed_learning_amd.graph import best_constant_weight, torus_edges, uniform_weights
+    E = engine()
+    edges = torus_edges(64, 64)
+    csr = uniform_weights(edges, best_constant_weight(edges))
+    rng = np.random.default_rng(2)
+    X = rng.standard_normal((4096, 256), dtype=np.float32)
+    a = E.GossipEngine(csr, 256, device=cuda, X=torch.from_numpy(X).to(cuda))
+    assert E.rounds_plan(a.W, a.X, a.Y, tiled=(a.P, a.T)) is None
+    b = E.GossipEngine(csr, 256, device=cuda, X=torch.from_numpy(X).to(cuda))
+    a.rounds(3)
+    for _ in range(3):
+        b.round()
+    torch.cuda.synchronize()
+    assert torch.equal(a.X, b.X)
+
+
+def test_mixer_times_uses_one_pass(cuda):
+    """Mixer.mix(times=K) with eps=None (one dl_mix_rounds pass over padded rows) equals the
+    reference fold applied K times to the flattened models."""
+    import logging
+
+    from distributed_learning_amd.networks import ANNModel
+    from distributed_learning_amd.utils.consensus_simple import Mixer
+    torch.manual_seed(0)
+    keys = ["a", "b", "c", "d", "e"]
+    models = {k: ANNModel(30, 17, 5).to(cuda) for k in keys}
+    topo = {"a": {"a": 0.5, "b": 0.25, "e": 0.25}, "b": {"b": 0.5, "a": 0.25, "c": 0.25},
+            "c": {"c": 0.5, "b": 0.25, "d": 0.25}, "d": {"d": 0.5, "c": 0.25, "e": 0.25},
+            "e": {"e": 0.5, "d": 0.25, "a": 0.25}}
+    X0 = np.stack([torch.cat([p.data.reshape(-1) for p in models[k].parameters()]).cpu().numpy()
+                   for k in keys])
+    rp, cl, w = M.topology_to_csr(topo)
+    want = X0
+    for _ in range(9):
+        want = M.mix_once(want, rp, cl, w)
+    mixer = Mixer(models, topo, logging.getLogger("t"))
+    assert mixer.mix(times=9) == 9
+    got = np.stack([torch.cat([p.data.reshape(-1) for p in models[k].parameters()]).cpu().numpy()
+                    for k in keys])
+    assert np.array_equal(bits(got), bits(want))

@@ -18,6 +18,9 @@ Other BASELINE configs (not the headline line; run on request):
       torus on one GPU (tiled layout).  N>1: agents partitioned into 2-D torus blocks, one per
       rank, boundary rows exchanged over RCCL send/recv every round (HaloShard), so the total
       work is fixed (strong scaling).
+  c2-gossip  pure gossip averaging as Mixer.mix(times=K) (eps=None): K rounds per HBM pass on
+      LDS-resident column tiles (dl_mix_rounds); rounds/s counts every round.  N>1: column
+      stripes, no exchange.
   c5  Wide-ResNet-16-4 consensus SGD, 64 agents x 2,751,146 params, B=64 synthetic CIFAR-shaped
       batches: per-agent PyTorch-ROCm (MIOpen) forward/backward into G's rows, dl_sgd_step
       (SGD momentum 0.9, wd 5e-4) and the fused round, one hipGraph per step.
@@ -38,6 +41,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 FP32_MFMA_PEAK_TFLOPS = 157.3  # dense f32-input MFMA (MI355X_MICROARCH.md, peak FP32 matrix)
+LDS_PEAK_GBS = 150000.0  # aggregate ds_read_b64/b128 with every CU streaming (MI355X_MICROARCH.md)
 
 
 def parse():
@@ -45,7 +49,12 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=10)
-    p.add_argument("--workload", default="c2", choices=["c2", "c2-mix", "c3", "c4", "c5"])
+    p.add_argument("--workload", default="c2",
+                   choices=["c2", "c2-mix", "c2-gossip", "c3", "c4", "c5"])
+    p.add_argument("--graph", default="rr4", choices=["rr4", "circ4"],
+                   help="c2-gossip: agent graph (circ4 = conflict-free control)")
+    p.add_argument("--rounds", type=int, default=64,
+                   help="c2-gossip: rounds per Mixer.mix(times=K) call (one HBM pass)")
     p.add_argument("--agents", type=int, default=1024)
     p.add_argument("--params", type=int, default=1 << 20)
     p.add_argument("--cpu-cols", type=int, default=1 << 18,
@@ -66,10 +75,16 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def build_graph(n):
+def build_graph(n, kind="rr4"):
+    """rr4: networkx random 4-regular graph (seed 0), the BASELINE graph; circ4: the circulant
+    graph a ~ a+-1, a+-2 (a measurement control: every neighbour is a fixed slot offset, so the
+    LDS reads of a lane group never conflict)."""
     from distributed_learning_amd.graph import (best_constant_weight, from_edge_weights,
                                                 first_appearance_vertices, random_regular_edges)
-    edges = random_regular_edges(4, n, seed=0)
+    if kind == "circ4":
+        edges = [(a, (a + d) % n) for a in range(n) for d in (1, 2)]
+    else:
+        edges = random_regular_edges(4, n, seed=0)
     verts = sorted(first_appearance_vertices(edges))
     w = best_constant_weight(edges, verts)
     return from_edge_weights(edges, [w] * len(edges), verts), w
@@ -564,6 +579,74 @@ def run_c5(args, dev, rank, world):
     print(json.dumps(rec), flush=True)
 
 
+def run_gossip(args, dev, rank, world):
+    """c2 as pure gossip averaging: one step = Mixer.mix(times=K) with eps=None, i.e. K rounds
+    X <- W X with nothing in between, run by dl_mix_rounds as ONE pass over HBM (every round on
+    LDS-resident column tiles of all 1024 agents) plus the final disagreement.  Every round is
+    bit-identical to the one-round kernel (tests/test_mix_rounds_gpu.py)."""
+    from distributed_learning_amd import engine
+    n, P, K = args.agents, args.params, args.rounds
+    csr, wconst = build_graph(n, args.graph)
+    g = torch.Generator(device=dev).manual_seed(1000 + rank)
+    eng = engine.GossipEngine(csr, P, device=dev, X=torch.randn(n, P, device=dev, generator=g))
+    plan = engine.rounds_plan(eng.W, eng.X, eng.Y, deviation=True, tiled=(eng.P, eng.T))
+    if plan is None:
+        raise SystemExit("c2-gossip: the multi-round kernel does not fit this graph")
+    stream = torch.cuda.current_stream(dev)
+    evs = event_pairs(args.steps, 2)
+
+    def step(i):
+        if i is not None:
+            evs[i][0].record(stream)
+        eng.rounds(K, deviation=True)
+        if i is not None:
+            evs[i][1].record(stream)
+
+    elapsed = timed_loop(step, args, world, dev)
+    launch_ms = max_over_ranks(float(np.mean([a.elapsed_time(b) for a, b in evs])), world, dev)
+    if rank != 0:
+        return
+    nel = n * P
+    hbm_bytes = 8 * nel                      # read X, write X' once per K rounds
+    lds_bytes = K * nel * 4 * (5 + 1)        # per round: d + 1 = 5 neighbour reads + 1 write
+    rounds_per_s = world * args.steps * K / elapsed
+    rec = {
+        "metric": "consensus rounds/sec, pure gossip averaging (Mixer.mix(times=K)), "
+                  "1024 agents x 1M fp32 params",
+        "value": rounds_per_s,
+        "unit": "rounds/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (X ~ N(0,1) resident in HBM; networkx random_regular_graph(4, 1024, "
+                "seed=0))",
+        "config": {"workload": f"c2-gossip: Mixer.mix(times={K}) eps=None as one dl_mix_rounds "
+                               "pass + final deviation",
+                   "agents": n, "params_per_gpu": P, "rounds_per_step": K,
+                   "graph": {"rr4": "random 4-regular", "circ4": "circulant a+-1, a+-2"}[
+                       args.graph], "weights": f"best-constant {wconst:.6f}",
+                   "plan": plan,
+                   "parallelism": f"column stripes x{world}" if world > 1 else "single GPU"},
+        "roofline": {"bound": "lds", "achieved": lds_bytes / (launch_ms / 1e3) / 1e9,
+                     "peak": LDS_PEAK_GBS, "unit": "GB/s",
+                     "frac": lds_bytes / (launch_ms / 1e3) / 1e9 / LDS_PEAK_GBS,
+                     "traffic": None,
+                     "kernel": "mix_multi_kernel (+dev_reduce) per-step HIP-event time",
+                     "bytes_per_launch": lds_bytes, "launch_ms": launch_ms,
+                     "hbm_bytes_per_launch": hbm_bytes,
+                     "hbm_GBs": hbm_bytes / (launch_ms / 1e3) / 1e9,
+                     "round_equivalent_hbm_GBs": K * hbm_bytes / (launch_ms / 1e3) / 1e9},
+        "cpu_baseline": None,
+        "final_max_deviation": float(eng.dev_max.item()),
+    }
+    print(json.dumps(rec), flush=True)
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -582,8 +665,9 @@ def main():
         else:
             dist.init_process_group(args.dist_backend)
 
-    if args.workload in ("c3", "c4", "c5"):
-        {"c3": run_c3, "c4": run_c4, "c5": run_c5}[args.workload](args, dev, rank, world)
+    if args.workload in ("c2-gossip", "c3", "c4", "c5"):
+        {"c2-gossip": run_gossip, "c3": run_c3, "c4": run_c4, "c5": run_c5}[args.workload](
+            args, dev, rank, world)
         if world > 1:
             dist.destroy_process_group()
         return

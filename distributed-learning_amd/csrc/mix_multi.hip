@@ -38,8 +38,12 @@ __device__ __forceinline__ const float4 *mm_at(const void *base, uint32_t off) {
 
 // C: float4 chunks per tile row (T = 4C columns); KV: rows per thread (agents s + k*SLOTS);
 // SGD: local step x - lr g applied once, before the first round; DEV: final deviation.
+// RE > 0: regular graph with RE entries per row whose weights every row shares (best-constant /
+// analytic FA weights): each thread keeps its rows' neighbour byte offsets and the RE weights in
+// registers for the whole launch, so a round issues only the RE neighbour reads and one write
+// per output chunk (no CSR reads from LDS).  RE = 0: CSR from LDS.
 // FAST tiles only (every tile full and 16-byte aligned; the column-tiled layout always is).
-template <int C, int KV, bool SGD, bool DEV>
+template <int C, int KV, bool SGD, bool DEV, int RE>
 __global__ void __launch_bounds__(kTileThreads) mix_multi_kernel(TileArgs a, int rounds) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int NT = kTileThreads;
@@ -108,6 +112,39 @@ __global__ void __launch_bounds__(kTileThreads) mix_multi_kernel(TileArgs a, int
         return acc;
     };
 
+    // register-cached CSR (RE > 0): byte offset of each neighbour's chunk c inside an image
+    uint32_t coff[KV][RE > 0 ? RE : 1];
+    float wreg[RE > 0 ? RE : 1];
+    if constexpr (RE > 0) {
+#pragma unroll
+        for (int e = 0; e < RE; ++e) wreg[e] = a.w[e];
+#pragma unroll
+        for (int k = 0; k < KV; ++k) {
+            const int ag = s + k * SLOTS < Nr ? s + k * SLOTS : 0;
+#pragma unroll
+            for (int e = 0; e < RE; ++e)
+                coff[k][e] = ((uint32_t)a.col[ag * RE + e] * C + c) * 16u;
+        }
+    }
+    auto mix_row_reg = [&](const float4 *src, int k) {
+        const char *base = reinterpret_cast<const char *>(src);
+        float4 acc = mm_zero4();
+#pragma unroll
+        for (int e = 0; e < (RE > 0 ? RE : 1); ++e) {
+            const float4 v = *reinterpret_cast<const float4 *>(base + coff[k][e]);
+            const float w = wreg[e];
+            acc.x = acc.x + w * v.x;
+            acc.y = acc.y + w * v.y;
+            acc.z = acc.z + w * v.z;
+            acc.w = acc.w + w * v.w;
+        }
+        return acc;
+    };
+    auto out_row = [&](const float4 *src, int k, int ag) {
+        if constexpr (RE > 0) return mix_row_reg(src, k);
+        return mix_row(src, ag);
+    };
+
     constexpr int ND = KV <= C ? 1 : KV / C;
     float dacc[ND];
 #pragma unroll
@@ -152,7 +189,7 @@ __global__ void __launch_bounds__(kTileThreads) mix_multi_kernel(TileArgs a, int
         __syncthreads();
         float4 mean = mm_zero4();
         if (DEV) {
-#pragma unroll
+#pragma unroll 2   // (fully unrolled, the 16 reads are hoisted: 64 VGPRs at once, spills)
             for (int wv = 0; wv < NT / 64; ++wv) {
                 const float4 q = scratch[wv * C + c];
                 mean.x += q.x;
@@ -170,10 +207,13 @@ __global__ void __launch_bounds__(kTileThreads) mix_multi_kernel(TileArgs a, int
         const float4 *src = img0;
         float4 *dst = img1;
         for (int r = 0; r + 1 < rounds; ++r) {
-#pragma unroll 1
+#pragma unroll
             for (int k = 0; k < KV; ++k) {
                 const int ag = s + k * SLOTS;
-                if (ag < Nr) dst[ag * C + c] = mix_row(src, ag);
+                if (ag < Nr) dst[ag * C + c] = out_row(src, k, ag);
+                // one output row at a time: keeps the RE neighbour reads of the next row from
+                // being hoisted above this one's (register pressure at 1024 threads)
+                __builtin_amdgcn_sched_barrier(0);
             }
             __syncthreads();
             const float4 *t = src;
@@ -181,11 +221,11 @@ __global__ void __launch_bounds__(kTileThreads) mix_multi_kernel(TileArgs a, int
             dst = const_cast<float4 *>(t);
         }
         const char *yt = tile_base(a.y, a.yts, tile_id);
-#pragma unroll 1
+#pragma unroll
         for (int k = 0; k < KV; ++k) {
             const int ag = s + k * SLOTS;
             if (ag < Nr) {
-                const float4 y = mix_row(src, ag);
+                const float4 y = out_row(src, k, ag);
                 float4 *py = const_cast<float4 *>(mm_at(yt, oy + (uint32_t)k * sy));
                 if (a.nt_store)
                     mm_nt_store4(y, py);
@@ -201,6 +241,7 @@ __global__ void __launch_bounds__(kTileThreads) mix_multi_kernel(TileArgs a, int
 #pragma unroll
                     for (int j = 0; j < ND; ++j) dacc[j] += (mine && j == k / C) ? v : 0.f;
                 }
+                __builtin_amdgcn_sched_barrier(0);
             }
         }
         if (DEV && a.mean != nullptr && s == 0) {
@@ -219,34 +260,33 @@ __global__ void __launch_bounds__(kTileThreads) mix_multi_kernel(TileArgs a, int
     }
 }
 
+template <int C, int KV, bool SGD, bool DEV, int RE>
+hipError_t launch_one(const TileArgs &a, int rounds, int grid, int lds, hipStream_t s) {
+    const void *k = reinterpret_cast<const void *>(mix_multi_kernel<C, KV, SGD, DEV, RE>);
+    hipError_t e = allow_full_lds(k);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((mix_multi_kernel<C, KV, SGD, DEV, RE>), dim3(grid), dim3(kTileThreads),
+                       lds, s, a, rounds);
+    return hipGetLastError();
+}
+
+template <int C, int KV, int RE>
+hipError_t launch_re(const TileArgs &a, int rounds, bool sgd, bool dev, int grid, int lds,
+                     hipStream_t s) {
+    if (sgd)
+        return dev ? launch_one<C, KV, true, true, RE>(a, rounds, grid, lds, s)
+                   : launch_one<C, KV, true, false, RE>(a, rounds, grid, lds, s);
+    return dev ? launch_one<C, KV, false, true, RE>(a, rounds, grid, lds, s)
+               : launch_one<C, KV, false, false, RE>(a, rounds, grid, lds, s);
+}
+
 template <int C, int KV>
 hipError_t launch_kv(const TileArgs &a, int rounds, bool sgd, bool dev, int grid, int lds,
                      hipStream_t s) {
-    const void *k;
-    if (sgd)
-        k = dev ? reinterpret_cast<const void *>(mix_multi_kernel<C, KV, true, true>)
-                : reinterpret_cast<const void *>(mix_multi_kernel<C, KV, true, false>);
-    else
-        k = dev ? reinterpret_cast<const void *>(mix_multi_kernel<C, KV, false, true>)
-                : reinterpret_cast<const void *>(mix_multi_kernel<C, KV, false, false>);
-    hipError_t e = allow_full_lds(k);
-    if (e != hipSuccess) return e;
-    if (sgd) {
-        if (dev)
-            hipLaunchKernelGGL((mix_multi_kernel<C, KV, true, true>), dim3(grid), dim3(kTileThreads),
-                               lds, s, a, rounds);
-        else
-            hipLaunchKernelGGL((mix_multi_kernel<C, KV, true, false>), dim3(grid), dim3(kTileThreads),
-                               lds, s, a, rounds);
-    } else {
-        if (dev)
-            hipLaunchKernelGGL((mix_multi_kernel<C, KV, false, true>), dim3(grid),
-                               dim3(kTileThreads), lds, s, a, rounds);
-        else
-            hipLaunchKernelGGL((mix_multi_kernel<C, KV, false, false>), dim3(grid),
-                               dim3(kTileThreads), lds, s, a, rounds);
-    }
-    return hipGetLastError();
+    // register-cached CSR for the degree-4 regular graphs with shared weights (c2, c4 shapes)
+    if (a.regular == 5 && a.n_w == 5 && KV <= 4)
+        return launch_re<C, KV, 5>(a, rounds, sgd, dev, grid, lds, s);
+    return launch_re<C, KV, 0>(a, rounds, sgd, dev, grid, lds, s);
 }
 
 template <int C>

@@ -66,6 +66,8 @@ def parse():
                    help="c3: resident layout of X and G (tiled: the fused gradient kernel "
                         "addresses the round's column tiles; measured equal overall)")
     p.add_argument("--batch", type=int, default=64, help="c5: images per agent per step")
+    p.add_argument("--cudnn-benchmark", action="store_true",
+                   help="c5: torch.backends.cudnn.benchmark (MIOpen exhaustive find)")
     p.add_argument("--dist-backend", default="nccl",
                    help="nccl (= RCCL, default) or gloo (multi-rank rehearsal on one GPU)")
     return p.parse_args()
@@ -488,6 +490,7 @@ def run_c5(args, dev, rank, world):
     from distributed_learning_amd.workloads import WRNConsensusSGD
     n, B = 64, args.batch
     csr, wconst = build_graph(n)
+    torch.backends.cudnn.benchmark = args.cudnn_benchmark
     t0 = time.perf_counter()
     wl = WRNConsensusSGD(csr, B, device=dev, seed=1000 * rank, streams=args.streams)
     stream = torch.cuda.current_stream(dev)
@@ -566,7 +569,7 @@ def run_c5(args, dev, rank, world):
                    "agents": n, "params": wl.P, "batch": B, "lr": wl.lr,
                    "momentum": wl.momentum, "weight_decay": wl.wd,
                    "graph": "random 4-regular", "weights": f"best-constant {wconst:.6f}",
-                   "streams": args.streams,
+                   "streams": args.streams, "cudnn_benchmark": args.cudnn_benchmark,
                    "miopen_find_mode": os.environ.get("MIOPEN_FIND_MODE", "default"),
                    "launch": "hipGraph replay per step" if use_graph else "eager",
                    "images_per_s": world * args.steps * n * B / elapsed,

@@ -41,7 +41,7 @@ def consensus_sgd_steps(models, optimizers, data, labels, rowptr, cols, w, steps
             loss = torch.nn.functional.cross_entropy(m(data[a]), labels[a])
             loss.backward()
             opt.step()
-            ls.append(float(loss))
+            ls.append(float(loss.detach()))
         X = np.stack([flatten(m) for m in models])
         Y = mixer_ref.mix_once(X, rowptr, cols, w)
         for m, y in zip(models, Y):

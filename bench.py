@@ -51,7 +51,7 @@ def parse():
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--workload", default="c2",
                    choices=["c2", "c2-mix", "c2-gossip", "c3", "c4", "c5"])
-    p.add_argument("--graph", default="rr4", choices=["rr4", "circ4"],
+    p.add_argument("--graph", default="rr4", choices=["rr4", "circ4", "torus"],
                    help="c2-gossip: agent graph (circ4 = conflict-free control)")
     p.add_argument("--rounds", type=int, default=64,
                    help="c2-gossip: rounds per Mixer.mix(times=K) call (one HBM pass)")
@@ -85,6 +85,10 @@ def build_graph(n, kind="rr4"):
                                                 first_appearance_vertices, random_regular_edges)
     if kind == "circ4":
         edges = [(a, (a + d) % n) for a in range(n) for d in (1, 2)]
+    elif kind == "torus":     # c4's periodic torus, side sqrt(n)
+        from distributed_learning_amd.graph import torus_edges
+        side = int(round(n ** 0.5))
+        edges = torus_edges(side, side)
     else:
         edges = random_regular_edges(4, n, seed=0)
     verts = sorted(first_appearance_vertices(edges))
@@ -631,8 +635,8 @@ def run_gossip(args, dev, rank, world):
         "config": {"workload": f"c2-gossip: Mixer.mix(times={K}) eps=None as one dl_mix_rounds "
                                "pass + final deviation",
                    "agents": n, "params_per_gpu": P, "rounds_per_step": K,
-                   "graph": {"rr4": "random 4-regular", "circ4": "circulant a+-1, a+-2"}[
-                       args.graph], "weights": f"best-constant {wconst:.6f}",
+                   "graph": {"rr4": "random 4-regular", "circ4": "circulant a+-1, a+-2",
+                             "torus": "2-D periodic torus"}[args.graph], "weights": f"best-constant {wconst:.6f}",
                    "plan": plan,
                    "parallelism": f"column stripes x{world}" if world > 1 else "single GPU"},
         "roofline": {"bound": "lds", "achieved": lds_bytes / (launch_ms / 1e3) / 1e9,

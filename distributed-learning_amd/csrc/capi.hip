@@ -326,9 +326,14 @@ int plan_rounds(const dl_mix_args *a, Plan *pl) {
                                         "stochastic W");
     const int reg = a->W.uniform_row_nnz > 0 ? 1 : 0;
     const int32_t n_w = (reg && a->W.shared_row_weights) ? a->W.uniform_row_nnz : a->W.nnz;
-    const uint32_t csr = dl::csr_lds_bytes(R, a->W.nnz, reg, n_w);
-    if (csr == 0 || R > 65535) return fail(DL_ERR_UNSUPPORTED, "dl_mix_rounds: CSR too large");
+    if (dl::csr_lds_bytes(R, a->W.nnz, reg, n_w) == 0 || R > 65535)
+        return fail(DL_ERR_UNSUPPORTED, "dl_mix_rounds: CSR too large");
     auto fits = [&](int c) {
+        // degree-4 regular graphs with shared weights keep the CSR in registers (mix_multi.hip
+        // launch_kv: uniform_row_nnz 5, 5 weights, <= 4 rows per thread): no LDS for it
+        const bool in_regs = a->W.uniform_row_nnz == 5 && n_w == 5 &&
+                             dl::tile_passes(c, R, true) <= 4;
+        const uint32_t csr = in_regs ? 0u : dl::csr_lds_bytes(R, a->W.nnz, reg, n_w);
         const int64_t tile = (int64_t)R * c * 16;
         const int64_t scratch = want_dev ? (int64_t)(dl::kTileThreads / 64) * c * 16 : 0;
         return (int64_t)R * c <= (int64_t)dl::kRowsPerThread * dl::kTileThreads &&
@@ -352,6 +357,8 @@ int plan_rounds(const dl_mix_args *a, Plan *pl) {
     const int64_t T = 4 * c;
     const int64_t n_tiles = (a->n_params + T - 1) / T;
     const int64_t tile = (int64_t)R * c * 16;
+    const bool in_regs = a->W.uniform_row_nnz == 5 && n_w == 5 && dl::tile_passes(c, R, true) <= 4;
+    const uint32_t csr = in_regs ? 0u : dl::csr_lds_bytes(R, a->W.nnz, reg, n_w);
     pl->chunks = c;
     pl->csr_off = (uint32_t)(2 * tile);
     pl->scratch_off = (uint32_t)(2 * tile + csr);

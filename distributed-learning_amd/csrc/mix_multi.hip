@@ -59,11 +59,13 @@ __global__ void __launch_bounds__(kTileThreads) mix_multi_kernel(TileArgs a, int
     uint16_t *lcol = reinterpret_cast<uint16_t *>(smem + a.csr_off + 4u * (uint32_t)a.n_w);
     uint16_t *lrp = lcol + nnz;
     float4 *scratch = reinterpret_cast<float4 *>(smem + a.scratch_off);
-    for (int i = tid; i < a.n_w; i += NT) lw[i] = a.w[i];
-    for (int i = tid; i < nnz; i += NT) lcol[i] = (uint16_t)a.col[i];
     const int reg = a.regular;
-    if (!reg)
-        for (int i = tid; i <= Nr; i += NT) lrp[i] = (uint16_t)a.rowptr[i];
+    if constexpr (RE == 0) {   // RE > 0 keeps its CSR in registers: nothing staged in LDS
+        for (int i = tid; i < a.n_w; i += NT) lw[i] = a.w[i];
+        for (int i = tid; i < nnz; i += NT) lcol[i] = (uint16_t)a.col[i];
+        if (!reg)
+            for (int i = tid; i <= Nr; i += NT) lrp[i] = (uint16_t)a.rowptr[i];
+    }
     const bool wshared = a.n_w != nnz;
 
     uint32_t ox = (uint32_t)s * a.xrs + 16u * c;
@@ -283,7 +285,8 @@ hipError_t launch_re(const TileArgs &a, int rounds, bool sgd, bool dev, int grid
 template <int C, int KV>
 hipError_t launch_kv(const TileArgs &a, int rounds, bool sgd, bool dev, int grid, int lds,
                      hipStream_t s) {
-    // register-cached CSR for the degree-4 regular graphs with shared weights (c2, c4 shapes)
+    // register-cached CSR for the degree-4 regular graphs with shared weights (c2, c4 shapes);
+    // the same test as csr_in_registers() on the host, which then reserves no LDS for the CSR
     if (a.regular == 5 && a.n_w == 5 && KV <= 4)
         return launch_re<C, KV, 5>(a, rounds, sgd, dev, grid, lds, s);
     return launch_re<C, KV, 0>(a, rounds, sgd, dev, grid, lds, s);

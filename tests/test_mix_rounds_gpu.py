@@ -79,8 +79,8 @@ def test_final_deviation_doubly_stochastic(cuda, layout):
     check_dev(Y, eng.dev_sq.cpu().numpy(), float(eng.dev_max.item()), mean.cpu().numpy())
 
 
-def test_unsupported_falls_back_to_single_rounds(cuda):
-    """4096 agents: two tile images do not fit LDS beside the CSR -> k one-round launches."""
+def test_torus_4096_csr_in_registers(cuda):
+    """c4's 64 x 64 torus: with the CSR in registers two 4096-agent tile images fit LDS."""
     from distributed_learning_amd.graph import best_constant_weight, torus_edges, uniform_weights
     E = engine()
     edges = torus_edges(64, 64)
@@ -88,8 +88,25 @@ def test_unsupported_falls_back_to_single_rounds(cuda):
     rng = np.random.default_rng(2)
     X = rng.standard_normal((4096, 256), dtype=np.float32)
     a = E.GossipEngine(csr, 256, device=cuda, X=torch.from_numpy(X).to(cuda))
-    assert E.rounds_plan(a.W, a.X, a.Y, tiled=(a.P, a.T)) is None
+    assert E.rounds_plan(a.W, a.X, a.Y, tiled=(a.P, a.T)) is not None
     b = E.GossipEngine(csr, 256, device=cuda, X=torch.from_numpy(X).to(cuda))
+    a.rounds(3, deviation=True)
+    for i in range(3):
+        b.round(deviation=i == 2)
+    torch.cuda.synchronize()
+    assert torch.equal(a.X, b.X)
+    torch.testing.assert_close(a.dev_sq, b.dev_sq, rtol=1e-5, atol=0)
+
+
+def test_unsupported_falls_back_to_single_rounds(cuda):
+    """6000 agents (general CSR): two tile images do not fit LDS -> k one-round launches."""
+    E = engine()
+    csr = graph_csr(6000, 3, seed=5)
+    rng = np.random.default_rng(2)
+    X = rng.standard_normal((6000, 64), dtype=np.float32)
+    a = E.GossipEngine(csr, 64, device=cuda, X=torch.from_numpy(X).to(cuda), layout="rows")
+    assert E.rounds_plan(a.W, a.X, a.Y) is None
+    b = E.GossipEngine(csr, 64, device=cuda, X=torch.from_numpy(X).to(cuda), layout="rows")
     a.rounds(3)
     for _ in range(3):
         b.round()

@@ -117,3 +117,35 @@ def test_tiled_width_choice(n, T):
     # at C = 4 one workgroup per CU, else two when LDS allows
     if T == 16:
         assert pl.grid <= 256
+
+
+def test_new_entry_points_validate_before_any_device_call():
+    """dl_sgd_step, dl_mlp_grad, dl_mix_rounds(_plan): bad arguments come back as status codes
+    with a message, nothing is launched (runs without a GPU)."""
+    from distributed_learning_amd import _lib
+    lib = _lib.load()
+    a = _lib.DlSgdArgs()
+    a.n_rows, a.n_params = 4, 16
+    assert lib.dl_sgd_step(ctypes.byref(a), None) == _lib.DL_ERR_INVALID   # null pointers
+    a.x = a.g = a.out = 16
+    a.ldx = a.ldg = a.ldo = 16
+    a.momentum = 0.9                                                        # ... no buffer
+    assert lib.dl_sgd_step(ctypes.byref(a), None) == _lib.DL_ERR_INVALID
+    assert b"momentum" in lib.dl_last_error()
+    a.momentum, a.nesterov = 0.0, 1
+    assert lib.dl_sgd_step(ctypes.byref(a), None) == _lib.DL_ERR_INVALID
+    assert b"Nesterov" in lib.dl_last_error()
+    m = _lib.DlMlpArgs(4, 32, 784, 150, 10)                                 # batch 32
+    assert lib.dl_mlp_grad(ctypes.byref(m), None) == _lib.DL_ERR_UNSUPPORTED
+    m = _lib.DlMlpArgs(4, 64, 784, 150, 10)
+    m.tile_cols = 6                                                         # not a power of 2
+    assert lib.dl_mlp_grad(ctypes.byref(m), None) == _lib.DL_ERR_INVALID
+    x = _lib.DlMixArgs()
+    x.x, x.y, x.n_params, x.ldx, x.ldy = 256, 1 << 20, 64, 64, 64
+    x.W = _lib.DlCsr(16, 16, 16, 4, 12, 3, 1, 1)
+    assert lib.dl_mix_rounds(ctypes.byref(x), 0, None, 0, None) == _lib.DL_ERR_INVALID
+    assert b"rounds" in lib.dl_last_error()
+    x.n_halo, x.halo, x.ldh = 2, 4096, 64
+    pl = _lib.DlMixPlan()
+    assert lib.dl_mix_rounds_plan(ctypes.byref(x), ctypes.byref(pl)) == _lib.DL_ERR_UNSUPPORTED
+    assert b"halo" in lib.dl_last_error()

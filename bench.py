@@ -53,6 +53,9 @@ def parse():
                    choices=["c2", "c2-mix", "c2-gossip", "c3", "c4", "c5"])
     p.add_argument("--graph", default="rr4", choices=["rr4", "circ4", "torus"],
                    help="c2-gossip: agent graph (circ4 = conflict-free control)")
+    p.add_argument("--relabel", type=int, default=0,
+                   help="c2-gossip: greedy slot-swap moves of graph.lds_slot_order (0 = agent "
+                        "order); spreads each ds_read_b128 lane group over distinct banks")
     p.add_argument("--rounds", type=int, default=64,
                    help="c2-gossip: rounds per Mixer.mix(times=K) call (one HBM pass)")
     p.add_argument("--agents", type=int, default=1024)
@@ -595,7 +598,17 @@ def run_gossip(args, dev, rank, world):
     n, P, K = args.agents, args.params, args.rounds
     csr, wconst = build_graph(n, args.graph)
     g = torch.Generator(device=dev).manual_seed(1000 + rank)
-    eng = engine.GossipEngine(csr, P, device=dev, X=torch.randn(n, P, device=dev, generator=g))
+    order, conflicts = None, None
+    if args.relabel > 0:
+        from distributed_learning_amd.graph import lds_slot_order
+        T = engine.plan_shape(engine.DeviceCsr(csr, dev), P, deviation=True,
+                              tile_cols=-1)["tile_cols"]
+        t0 = time.perf_counter()
+        order, c0, c1 = lds_slot_order(csr, T // 4, moves=args.relabel)
+        conflicts = {"before": c0, "after": c1, "search_s": time.perf_counter() - t0}
+        log(f"c2-gossip: LDS slot order, bank conflicts {c0} -> {c1}")
+    eng = engine.GossipEngine(csr, P, device=dev, X=torch.randn(n, P, device=dev, generator=g),
+                              order=order)
     plan = engine.rounds_plan(eng.W, eng.X, eng.Y, deviation=True, tiled=(eng.P, eng.T))
     if plan is None:
         raise SystemExit("c2-gossip: the multi-round kernel does not fit this graph")
@@ -637,7 +650,7 @@ def run_gossip(args, dev, rank, world):
                    "agents": n, "params_per_gpu": P, "rounds_per_step": K,
                    "graph": {"rr4": "random 4-regular", "circ4": "circulant a+-1, a+-2",
                              "torus": "2-D periodic torus"}[args.graph], "weights": f"best-constant {wconst:.6f}",
-                   "plan": plan,
+                   "plan": plan, "lds_slot_order": conflicts,
                    "parallelism": f"column stripes x{world}" if world > 1 else "single GPU"},
         "roofline": {"bound": "lds", "achieved": lds_bytes / (launch_ms / 1e3) / 1e9,
                      "peak": LDS_PEAK_GBS, "unit": "GB/s",

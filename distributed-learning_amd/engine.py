@@ -309,10 +309,22 @@ class GossipEngine:
     Row-major data goes in and out through ``load_rows`` / ``rows`` / ``layout_like``.
     """
 
-    def __init__(self, csr: Csr, n_params, device="cuda", X=None, layout="auto", tile_cols=None):
+    def __init__(self, csr: Csr, n_params, device="cuda", X=None, layout="auto", tile_cols=None,
+                 order=None):
+        """order (optional, ``graph.lds_slot_order``): order[slot] = agent, the row order of the
+        resident matrices.  ``load_rows`` / ``layout_like`` / ``rows`` take and return agent
+        order; ``dev_sq`` is per slot (``agent_dev_sq()`` in agent order)."""
         self.device = torch.device(device)
         if self.device.type == "cuda" and self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
+        self.order = None
+        if order is not None:
+            from .graph import permuted
+            order = np.asarray(order, np.int64)
+            if sorted(order.tolist()) != list(range(csr.n_rows)):
+                raise ValueError("order must be a permutation of the agents")
+            csr = permuted(csr, order)
+            self.order = torch.as_tensor(order, device=self.device)
         self.W = DeviceCsr(csr, self.device)
         self.n, self.P = csr.n_rows, int(n_params)
         plan = plan_shape(self.W, self.P, deviation=True,
@@ -341,6 +353,8 @@ class GossipEngine:
         if A.shape != (self.n, self.P):
             raise ValueError(f"expected shape ({self.n}, {self.P}), got {tuple(A.shape)}")
         A = A.to(self.device, torch.float32)
+        if self.order is not None:
+            A = A.index_select(0, self.order)          # agent order -> slot order (a copy)
         # always a buffer of its own: the engine ping-pongs X/Y and must never write into the
         # caller's tensor
         return to_tiled(A, self.T) if self.layout == "tiled" else A.contiguous().clone()
@@ -349,8 +363,22 @@ class GossipEngine:
         self.X = self.layout_like(X)
 
     def rows(self):
-        """The agent matrix as a row-major [N, P] tensor (a conversion in the tiled layout)."""
-        return from_tiled(self.X, self.P) if self.layout == "tiled" else self.X
+        """The agent matrix as a row-major [N, P] tensor in agent order (a conversion in the
+        tiled layout or under a slot order)."""
+        R = from_tiled(self.X, self.P) if self.layout == "tiled" else self.X
+        if self.order is not None:
+            out = torch.empty_like(R)
+            out[self.order] = R
+            return out
+        return R
+
+    def agent_dev_sq(self):
+        """dev_sq in agent order."""
+        if self.order is None:
+            return self.dev_sq
+        out = torch.empty_like(self.dev_sq)
+        out[self.order] = self.dev_sq
+        return out
 
     def reserve_workspace(self, deviation=True):
         """Allocate the round's scratch now (so a hipGraph capture allocates nothing)."""

@@ -138,3 +138,29 @@ def test_mixer_times_uses_one_pass(cuda):
     got = np.stack([torch.cat([p.data.reshape(-1) for p in models[k].parameters()]).cpu().numpy()
                     for k in keys])
     assert np.array_equal(bits(got), bits(want))
+
+
+def test_lds_slot_order_is_transparent(cuda):
+    """An engine holding its rows in an LDS slot order (graph.lds_slot_order) gives every agent
+    the same bits as the agent-order engine, one round or K rounds."""
+    from distributed_learning_amd.graph import (best_constant_weight, lds_conflicts,
+                                                lds_slot_order, random_regular_edges,
+                                                uniform_weights)
+    E = engine()
+    n, P = 1024, 2048
+    edges = random_regular_edges(4, n, seed=0)
+    csr = uniform_weights(edges, best_constant_weight(edges), list(range(n)))
+    order, c0, c1 = lds_slot_order(csr, 4, moves=20000)
+    assert c1 < c0 and lds_conflicts(csr, 4, order) == c1
+    rng = np.random.default_rng(3)
+    X = torch.from_numpy(rng.standard_normal((n, P), dtype=np.float32)).to(cuda)
+    G = torch.from_numpy(rng.standard_normal((n, P), dtype=np.float32)).to(cuda)
+    a = E.GossipEngine(csr, P, device=cuda, X=X)
+    b = E.GossipEngine(csr, P, device=cuda, X=X, order=order)
+    a.round(G=a.layout_like(G), lr=0.1, deviation=True)
+    b.round(G=b.layout_like(G), lr=0.1, deviation=True)
+    a.rounds(9, deviation=True)
+    b.rounds(9, deviation=True)
+    torch.cuda.synchronize()
+    assert torch.equal(a.rows(), b.rows())
+    torch.testing.assert_close(a.agent_dev_sq(), b.agent_dev_sq(), rtol=1e-5, atol=0)

@@ -14,9 +14,11 @@
 //   * weight gradients go from the MFMA accumulators straight into the agent's row of G (the
 //     Mixer flatten order, mixer.py:69), bias gradients are fixed-order column sums, and the
 //     per-agent loss is summed in a fixed order (deterministic, hipGraph-replay stable).
-// LDS strides are chosen per access so the MFMA fragment reads are bank-conflict free:
-//   [row][k] images read by 16 rows x 4 k   -> stride = 4 (mod 8)  floats  (36, 156)
-//   [k][col] images read by 16 cols x 4 k   -> stride = 16 (mod 32) floats (176)
+// LDS strides per access (ds_read_b32 banks are dword mod 32 per 32-lane half,
+// MI355X_MICROARCH.md §LDS):
+//   [row][k] images read by 16 rows x 4 k   -> stride = 4 (mod 8)  floats  (36, 156): 2-way (a
+//     ds_read_b64 pairing of k that is conflict-free measured no faster: not the bottleneck)
+//   [k][col] images read by 16 cols x 4 k   -> stride = 16 (mod 32) floats (176): conflict-free
 //   [k][col] images read by 32 cols x 2 k (32x32x2) -> stride = 32 (mod 64) floats (288)
 // f32 MFMA (16x16x4) products are exact fp32 fma chains; summation order differs from
 // autograd's BLAS, so parity is a tolerance (tests/test_batched_ann_gpu.py).

@@ -18,6 +18,10 @@ Other BASELINE configs (not the headline line; run on request):
       torus on one GPU (tiled layout).  N>1: agents partitioned into 2-D torus blocks, one per
       rank, boundary rows exchanged over RCCL send/recv every round (HaloShard), so the total
       work is fixed (strong scaling).
+  c1  Titanic logistic-regression consensus GD, 8 agents on a ring (the reference's asyncio
+      notebook run, convergence_eps 10): --steps GD iterations through the ConsensusNetwork /
+      ConsensusAgent facade (one dl_perron_round launch per consensus round); the CPU baseline
+      is the synchronous numpy restatement of the same run.  Latency-bound by design (7 params).
   c2-gossip  pure gossip averaging as Mixer.mix(times=K) (eps=None): K rounds per HBM pass on
       LDS-resident column tiles (dl_mix_rounds); rounds/s counts every round.  N>1: column
       stripes, no exchange.
@@ -50,7 +54,7 @@ def parse():
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--workload", default="c2",
-                   choices=["c2", "c2-mix", "c2-gossip", "c3", "c4", "c5"])
+                   choices=["c1", "c2", "c2-mix", "c2-gossip", "c3", "c4", "c5"])
     p.add_argument("--graph", default="rr4", choices=["rr4", "circ4", "torus"],
                    help="c2-gossip: agent graph (circ4 = conflict-free control)")
     p.add_argument("--relabel", type=int, default=0,
@@ -589,6 +593,86 @@ def run_c5(args, dev, rank, world):
     print(json.dumps(rec), flush=True)
 
 
+def c1_cpu_baseline(Xtr, ytr, topo, steps):
+    """The reference's c1 run restated synchronously in numpy (oracle/mixer_ref.jacobi_round,
+    pinned bit for bit to the reference's 4000-step asyncio run by tests/test_oracle_golden.py)."""
+    from oracle import mixer_ref as M
+    toks = M.asyncio_tokens(topo)
+    sh, tX, ty = {}, Xtr.copy(), ytr.copy()
+    for i in range(len(toks)):
+        ln = len(tX) // (len(toks) - i)
+        sh[toks[i]] = (tX[:ln], ty[:ln])
+        tX, ty = tX[ln:], ty[ln:]
+
+    def grad(X, y, w, tau=1e-4):
+        s = 1 / (1 + np.exp(y * (X @ w)))
+        return -np.array([np.dot(y * s, X[:, j]) for j in range(X.shape[1])]) / X.shape[0] \
+            + tau * w
+    w = {t: np.zeros(Xtr.shape[1]) for t in toks}
+    t0 = time.perf_counter()
+    for it in range(steps):
+        for t in toks:
+            w[t] = w[t] - 0.1 * np.power(it + 1, -0.5) * grad(*sh[t], w[t])
+        w, _ = M.jacobi_round(topo, w, {t: sh[t][0].shape[0] for t in toks}, 10)
+    return steps / (time.perf_counter() - t0)
+
+
+def run_c1(args, dev, rank, world):
+    """Config c1: the Titanic consensus-GD notebook run (ring of 8 agents, fp64 logistic
+    regression on the preprocessed data committed in tests/golden/titanic.npz) through the
+    asyncio facade: every GD iteration each agent takes its local step on the host and awaits
+    ConsensusAgent.run_round, whose Jacobi iterations run in one dl_perron_round launch."""
+    import asyncio
+
+    from distributed_learning_amd import workloads
+    d = np.load(os.path.join(ROOT, "tests", "golden", "titanic.npz"))
+    nt = int(d["n_test"])
+    Xtr, ytr = d["X"][nt:], d["y"][nt:]
+    topo = [(i, (i + 1) % 8) for i in range(8)]
+    asyncio.run(workloads.consensus_gd(topo, Xtr, ytr, max(args.warmup, 1), convergence_eps=10,
+                                       device=dev))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    w = asyncio.run(workloads.consensus_gd(topo, Xtr, ytr, args.steps, convergence_eps=10,
+                                           device=dev))
+    torch.cuda.synchronize()
+    elapsed = max_over_ranks(time.perf_counter() - t0, world, dev)
+    if rank != 0:
+        return
+    acc = workloads.accuracy(w[0], d["X"][:nt], d["y"][:nt])
+    cpu = None
+    if not args.no_cpu and world == 1:
+        cpu = {"value": c1_cpu_baseline(Xtr, ytr, topo, args.steps), "unit": "steps/s",
+               "cores": 1, "kind": "port",
+               "sample": f"the same {args.steps} GD iterations, synchronous numpy restatement of "
+                         "the asyncio rounds (oracle/mixer_ref.jacobi_round)"}
+    rec = {
+        "metric": "c1 Titanic consensus GD iterations/sec (8 agents, ring, asyncio facade)",
+        "value": world * args.steps / elapsed,
+        "unit": "steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "Titanic train.csv preprocessed as the notebook does (tests/golden/titanic.npz)",
+        "config": {"workload": "c1: ring-8 asyncio consensus GD, convergence_eps 10, step "
+                               "0.1 (it+1)^-0.5, tau 1e-4",
+                   "agents": 8, "params": int(Xtr.shape[1]),
+                   "test_accuracy_agent0": acc,
+                   "parallelism": f"{world} independent replicas" if world > 1 else "single GPU"},
+        "roofline": {"bound": "latency", "achieved": None, "peak": None, "unit": None,
+                     "frac": None, "traffic": None,
+                     "kernel": "dl_perron_round (one launch + 4-byte readback per round); "
+                               "7 fp64 params per agent: launch/synchronisation-bound"},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(rec), flush=True)
+
+
 def run_gossip(args, dev, rank, world):
     """c2 as pure gossip averaging: one step = Mixer.mix(times=K) with eps=None, i.e. K rounds
     X <- W X with nothing in between, run by dl_mix_rounds as ONE pass over HBM (every round on
@@ -685,9 +769,9 @@ def main():
         else:
             dist.init_process_group(args.dist_backend)
 
-    if args.workload in ("c2-gossip", "c3", "c4", "c5"):
-        {"c2-gossip": run_gossip, "c3": run_c3, "c4": run_c4, "c5": run_c5}[args.workload](
-            args, dev, rank, world)
+    if args.workload in ("c1", "c2-gossip", "c3", "c4", "c5"):
+        {"c1": run_c1, "c2-gossip": run_gossip, "c3": run_c3, "c4": run_c4,
+         "c5": run_c5}[args.workload](args, dev, rank, world)
         if world > 1:
             dist.destroy_process_group()
         return

@@ -710,6 +710,21 @@ def run_gossip(args, dev, rank, world):
     launch_ms = max_over_ranks(float(np.mean([a.elapsed_time(b) for a, b in evs])), world, dev)
     if rank != 0:
         return
+    cpu = None
+    if not args.no_cpu and world == 1:
+        # the reference's Mixer.mix(times=K), eps=None: K _mix_params_once folds (numpy
+        # restatement, one host core) on all agents x a column sample, scaled to the full P
+        from oracle import mixer_ref as M
+        cols = min(args.cpu_cols, P)
+        Xs = np.random.default_rng(0).standard_normal((n, cols), dtype=np.float32)
+        M.mix_once(Xs, csr.rowptr, csr.col, csr.w)
+        t0 = time.perf_counter()
+        for _ in range(3):
+            Xs = M.mix_once(Xs, csr.rowptr, csr.col, csr.w)
+        dt = (time.perf_counter() - t0) / 3
+        cpu = {"value": (cols / P) / dt, "unit": "rounds/s", "cores": 1, "kind": "port",
+               "sample": f"{n} agents x {cols} of {P} columns, 3 rounds of the numpy "
+                         "restatement of Mixer._mix_params_once, scaled to the full column count"}
     nel = n * P
     hbm_bytes = 8 * nel                      # read X, write X' once per K rounds
     lds_bytes = K * nel * 4 * (5 + 1)        # per round: d + 1 = 5 neighbour reads + 1 write
@@ -745,7 +760,7 @@ def run_gossip(args, dev, rank, world):
                      "hbm_bytes_per_launch": hbm_bytes,
                      "hbm_GBs": hbm_bytes / (launch_ms / 1e3) / 1e9,
                      "round_equivalent_hbm_GBs": K * hbm_bytes / (launch_ms / 1e3) / 1e9},
-        "cpu_baseline": None,
+        "cpu_baseline": cpu,
         "final_max_deviation": float(eng.dev_max.item()),
     }
     print(json.dumps(rec), flush=True)

@@ -33,6 +33,12 @@ class DlMixArgs(ctypes.Structure):
                 ("mean", _vp), ("tile_cols", _i32)]
 
 
+class DlMixUntilArgs(ctypes.Structure):
+    _fields_ = [("x", _vp), ("ldx", _i64), ("y", _vp), ("ldy", _i64), ("n_params", _i64),
+                ("W", DlCsr), ("times", _i32), ("use_eps", _i32), ("eps", _f32),
+                ("max_rounds", _i32), ("status", _vp), ("dev_trace", _vp)]
+
+
 class DlMixPlan(ctypes.Structure):
     _fields_ = [("path", _i32), ("tile_cols", _i32), ("grid", _i32), ("lds_bytes", _i32),
                 ("n_tiles", _i32), ("regular", _i32)]
@@ -83,6 +89,8 @@ SIGNATURES = {
     "dl_mix_round": (_i32, [ctypes.POINTER(DlMixArgs), _vp, _sz, _vp]),
     "dl_mix_rounds_plan": (_i32, [ctypes.POINTER(DlMixArgs), ctypes.POINTER(DlMixPlan)]),
     "dl_mix_rounds": (_i32, [ctypes.POINTER(DlMixArgs), _i32, _vp, _sz, _vp]),
+    "dl_mix_until_fits": (_i32, [_i32, _i64, _i32]),
+    "dl_mix_until": (_i32, [ctypes.POINTER(DlMixUntilArgs), _vp]),
     "dl_deviation_workspace_bytes": (_sz, [_i32, _i64]),
     "dl_deviation": (_i32, [_vp, _i64, _i32, _i64, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "dl_deviation_tiled": (_i32, [_vp, _i32, _i64, _i32, _vp, _vp, _vp, _vp, _sz, _vp]),

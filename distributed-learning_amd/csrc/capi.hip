@@ -438,6 +438,57 @@ int dl_mix_rounds(const dl_mix_args *args, int32_t rounds, void *workspace, size
     return DL_OK;
 }
 
+int dl_mix_until_fits(int32_t n_rows, int64_t n_params, int32_t nnz) {
+    if (n_rows <= 0 || n_params <= 0 || nnz < 0) return 0;
+    return dl::until_lds_bytes(n_rows, n_params, nnz) <= dl::kLdsBytes ? 1 : 0;
+}
+
+int dl_mix_until(const dl_mix_until_args *a, dl_stream_t stream) {
+    g_err.clear();
+    if (!a) return fail(DL_ERR_INVALID, "dl_mix_until: args is NULL");
+    const dl_csr &W = a->W;
+    if (W.n_rows <= 0 || a->n_params <= 0 || W.nnz < 0)
+        return fail(DL_ERR_INVALID, "dl_mix_until: n_rows, n_params must be > 0, nnz >= 0");
+    if (!a->x || !a->y || !a->status || !W.row_ptr || (W.nnz > 0 && (!W.col || !W.w)))
+        return fail(DL_ERR_INVALID, "dl_mix_until: null x/y/status/row_ptr/col/w");
+    if (a->ldx < a->n_params || a->ldy < a->n_params)
+        return fail(DL_ERR_INVALID, "dl_mix_until: ldx/ldy smaller than n_params");
+    if (a->times < 0 || a->max_rounds < 1)
+        return fail(DL_ERR_INVALID, "dl_mix_until: times must be >= 0 and max_rounds >= 1");
+    if (W.uniform_row_nnz < 0 ||
+        (W.uniform_row_nnz > 0 && (int64_t)W.uniform_row_nnz * W.n_rows != W.nnz))
+        return fail(DL_ERR_INVALID, "dl_mix_until: uniform_row_nnz * n_rows != nnz");
+    const size_t xb = ((size_t)(W.n_rows - 1) * a->ldx + a->n_params) * 4;
+    const size_t yb = ((size_t)(W.n_rows - 1) * a->ldy + a->n_params) * 4;
+    if (!(a->x == a->y && a->ldx == a->ldy) && overlaps(a->x, xb, a->y, yb))
+        return fail(DL_ERR_INVALID, "dl_mix_until: y overlaps x (in place needs y == x, ldy == ldx)");
+    if (!dl_mix_until_fits(W.n_rows, a->n_params, W.nnz))
+        return fail(DL_ERR_UNSUPPORTED, "dl_mix_until: %d agents x %lld parameters (%lld bytes of "
+                                        "LDS) do not fit one workgroup", W.n_rows,
+                    (long long)a->n_params,
+                    (long long)dl::until_lds_bytes(W.n_rows, a->n_params, W.nnz));
+    dl::UntilArgs u{};
+    u.x = a->x;
+    u.ldx = a->ldx;
+    u.y = a->y;
+    u.ldy = a->ldy;
+    u.n_params = a->n_params;
+    u.chunks = (int32_t)((a->n_params + 3) / 4);
+    u.n_rows = W.n_rows;
+    u.nnz = W.nnz;
+    u.rowptr = W.row_ptr;
+    u.col = W.col;
+    u.w = W.w;
+    u.times = a->times;
+    u.use_eps = a->use_eps ? 1 : 0;
+    u.eps = a->eps;
+    u.max_rounds = a->max_rounds;
+    u.status = a->status;
+    u.dev_trace = a->use_eps ? a->dev_trace : nullptr;
+    hipError_t e = dl::launch_mix_until(u, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? DL_OK : hip_fail(e, "mix_until_kernel launch");
+}
+
 const char *dl_last_error(void) { return g_err.c_str(); }
 
 size_t dl_mix_workspace_bytes(int32_t n_rows, int32_t n_halo, int64_t n_params) {

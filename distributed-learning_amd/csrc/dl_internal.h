@@ -108,6 +108,29 @@ hipError_t launch_perron_single(const PerronArgs &a, int dtype, int tile_cols, h
 hipError_t launch_perron_step(const PerronArgs &a, int dtype, int tile_cols, const void *yin,
                               void *yout, bool prescale, hipStream_t s);
 
+// Mixer.mix(times, eps) loop in one workgroup (mix_until.hip)
+struct UntilArgs {
+    const float *x;
+    int64_t ldx;
+    float *y;
+    int64_t ldy;
+    int64_t n_params;
+    int32_t chunks;   // float4 chunks per LDS row: ceil(n_params / 4)
+    int32_t n_rows;
+    int32_t nnz;
+    const int32_t *rowptr;
+    const int32_t *col;
+    const float *w;
+    int32_t times;
+    int32_t use_eps;
+    float eps;
+    int32_t max_rounds;
+    int32_t *status;
+    float *dev_trace;
+};
+int64_t until_lds_bytes(int n_rows, int64_t n_params, int nnz);
+hipError_t launch_mix_until(const UntilArgs &a, hipStream_t s);
+
 enum Epi {
     EPI_NONE = 0,
     EPI_BIAS = 1,

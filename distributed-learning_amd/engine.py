@@ -203,6 +203,37 @@ def rounds_plan(W: DeviceCsr, X, Y, deviation=False, tiled=None):
     return {f: getattr(plan, f) for f, _ in plan._fields_}
 
 
+def until_fits(W: DeviceCsr, n_params):
+    """True when dl_mix_until holds these agents' whole vectors in one workgroup's LDS."""
+    return W.n_src == W.n_rows and bool(_lib.load().dl_mix_until_fits(W.n_rows, int(n_params),
+                                                                       W.nnz))
+
+
+def mix_until(W: DeviceCsr, X, Y, times, eps=None, max_rounds=4096, status=None,
+              dev_trace=None):
+    """``Mixer.mix``'s loop (mixer.py:18-41) in one launch on the current stream: rounds until
+    ``(eps is None or max deviation < float32(eps)) and done >= times`` or ``max_rounds``.
+    Y may be X.  ``status`` (device int32[2]) receives (rounds done, 1 if the stop rule held);
+    ``dev_trace`` (device float32[max_rounds + 1], eps only) every evaluated max deviation.
+    Does not synchronise."""
+    P = X.shape[1]
+    _check(X, "X", W.n_rows, P, W.device)
+    _check(Y, "Y", W.n_rows, P, W.device)
+    if W.n_src != W.n_rows:
+        raise ValueError("mix_until needs a square W (no halo rows)")
+    if status is None or status.dtype != torch.int32 or status.numel() < 2:
+        raise ValueError("status must be a device int32 tensor of >= 2 elements")
+    if dev_trace is not None and (dev_trace.dtype != torch.float32 or
+                                  dev_trace.numel() < max_rounds + 1):
+        raise ValueError("dev_trace must be float32 with >= max_rounds + 1 elements")
+    args = _lib.DlMixUntilArgs(
+        _lib.ptr(X), _ld(X), _lib.ptr(Y), _ld(Y), P, W.c_struct(), int(times),
+        0 if eps is None else 1, float(np.float32(eps)) if eps is not None else 0.0,
+        int(max_rounds), _lib.ptr(status), _lib.ptr(dev_trace) if eps is not None else None)
+    _lib.check(_lib.load().dl_mix_until(ctypes.byref(args), _lib.stream_handle(W.device)),
+               "dl_mix_until")
+
+
 def mix_plan(W: DeviceCsr, X, Y, G=None, deviation=False):
     lib = _lib.load()
     dummy = torch.empty(1, dtype=torch.float32, device=W.device) if deviation else None

@@ -2,7 +2,11 @@
 
 Same constructor, methods, return values, logging and stopping rule as the reference; the
 difference is where the work runs.  Per ``mix()`` call the models are flattened once into a
-device matrix X[N, P] (rows in ``topology`` key order, mixer.py:26/69); each round is one
+device matrix X[N, P] (rows in ``topology`` key order, mixer.py:26/69).  When two copies of X
+fit one workgroup's LDS (the reference's own use: small models on a handful of agents) the
+whole loop -- rounds, deviation, stop test -- is ONE ``dl_mix_until`` launch and one readback
+of the round count; the reference's per-evaluation debug log is replayed from the device's
+trace of max deviations.  Otherwise each round is one
 ``dl_mix_round`` launch (the reference's ``_mix_params_once`` fold, :43-49, bit-identical in
 fp32), and when ``eps`` is given the same launch also produces the per-agent deviation
 (:51-66) so the stop test costs one 4-byte readback per round.  With ``eps=None`` the ``times``
@@ -10,6 +14,8 @@ rounds have nothing in between, so they run as ONE ``dl_mix_rounds`` pass (every
 LDS-resident column tiles, bit-identical to ``times`` single rounds).  The results are written
 back into the models once at the end (:34-35, 71-76).
 """
+import logging
+
 import numpy as np
 import torch
 
@@ -41,6 +47,7 @@ class Mixer(object):
             self.dev_metric = dev_metric
         self._device = torch.device(device) if device is not None else None
         self._ws = None
+        self._csr = None   # (host Csr, DeviceCsr) of the last topology seen
 
     # ------------------------------------------------------------------ public API (:18-38)
     def mix(self, times=1, eps=None):
@@ -53,6 +60,11 @@ class Mixer(object):
             times_done = 0
             W = self._device_csr()
             X = self._flatten_all()
+            if not self._custom_metric and _engine.until_fits(W, X.shape[1]):
+                times_done = self._mix_resident(W, X, times, eps)
+                self._write_back(X)
+                self.logger.debug('Mixer finished with {} times'.format(times_done))
+                return times_done
             Y = torch.empty_like(X)
             fused_dev = eps is not None and not self._custom_metric
             dev_sq = torch.empty(X.shape[0], dtype=torch.float32, device=X.device)
@@ -96,6 +108,30 @@ class Mixer(object):
             return np.float32(_engine.max_column_std(X).item())
 
     # ------------------------------------------------------------------ internals
+    _UNTIL_ROUNDS = 4096   # rounds per dl_mix_until launch (bounds one launch; the loop re-enters)
+
+    def _mix_resident(self, W, X, times, eps):
+        """mixer.py:27-32 on the device (dl_mix_until), X updated in place.  A launch cut by the
+        round cap is continued with the remaining ``times``; its first evaluation repeats the
+        previous launch's last one, so that log line is not repeated."""
+        status = torch.empty(2, dtype=torch.int32, device=X.device)
+        trace = None
+        if eps is not None:
+            trace = torch.empty(self._UNTIL_ROUNDS + 1, dtype=torch.float32, device=X.device)
+        log = eps is not None and self.logger.isEnabledFor(logging.DEBUG)
+        done, first = 0, True
+        while True:
+            _engine.mix_until(W, X, X, max(int(times) - done, 0), eps, self._UNTIL_ROUNDS,
+                              status, trace)
+            n, stopped = status.tolist()
+            if log:
+                for d in trace[:n + 1].tolist()[0 if first else 1:]:
+                    self.logger.debug('Mixer calculate max deviation= {}'.format(np.float32(d)))
+            done += n
+            first = False
+            if stopped:
+                return done
+
     def _update_stopping_criterion(self, X, times_done, max_times, eps, fused=None):
         """mixer.py:40-41; the deviation is only evaluated when eps is set (short circuit)."""
         if eps is None:
@@ -128,8 +164,16 @@ class Mixer(object):
         return {agent: d[i] for i, agent in enumerate(keys)}
 
     def _device_csr(self):
+        """The topology as a device CSR; re-uploaded only when the topology changed (the
+        reference re-reads self.topology on every call, so it is re-derived every call)."""
         csr = from_topology(self.topology)
-        return _engine.DeviceCsr(csr, self._dev())
+        if self._csr is not None:
+            old = self._csr[0]
+            if (np.array_equal(old.rowptr, csr.rowptr) and np.array_equal(old.col, csr.col) and
+                    np.array_equal(old.w, csr.w) and old.n_src == csr.n_src):
+                return self._csr[1]
+        self._csr = (csr, _engine.DeviceCsr(csr, self._dev()))
+        return self._csr[1]
 
     def _dev(self):
         if self._device is None:
@@ -142,8 +186,19 @@ class Mixer(object):
         return self._ws
 
     def _flatten_all(self):
-        rows = [self._get_flatten_model_params(self.models[agent]) for agent in self.topology]
-        return torch.stack(rows).contiguous()
+        """X[N, P], rows in topology order: one concatenation of every parameter of every
+        model (mixer.py:26/68-69)."""
+        dev = self._dev()
+        parts, sizes = [], []
+        for agent in self.topology:
+            n = 0
+            for p in self.models[agent].parameters():
+                parts.append(p.data.to(device=dev, dtype=torch.float32).view(-1))
+                n += p.numel()
+            sizes.append(n)
+        if len(set(sizes)) != 1:
+            raise ValueError(f"models differ in parameter count: {sizes}")
+        return torch.cat(parts).view(len(sizes), sizes[0])
 
     def _get_flatten_model_params(self, model):
         """mixer.py:68-69, kept on the device."""
@@ -160,5 +215,17 @@ class Mixer(object):
             used_params += cnt_params
 
     def _write_back(self, X):
+        """mixer.py:34-35 / 71-76 for every model, as one fused multi-tensor copy."""
+        dst, src = [], []
         for i, agent in enumerate(self.topology):
-            self._load_flatten_params_to_model(self.models[agent], X[i])
+            used = 0
+            for p in self.models[agent].parameters():
+                n = p.numel()
+                dst.append(p.data)
+                src.append(X[i, used:used + n].view(p.shape))
+                used += n
+        if dst and all(d.device == s.device for d, s in zip(dst, src)):
+            torch._foreach_copy_(dst, src)
+        else:
+            for d, s in zip(dst, src):
+                d.copy_(s)

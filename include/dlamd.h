@@ -134,6 +134,37 @@ int dl_mix_rounds_plan(const dl_mix_args *args, dl_mix_plan *plan);
 int dl_mix_rounds(const dl_mix_args *args, int32_t rounds, void *workspace, size_t ws_bytes,
                   dl_stream_t stream);
 
+/* Mixer.mix(times, eps) (utils/consensus_simple/mixer.py:18-41) as ONE launch: the loop
+ *     stop = (!use_eps || max_a ||x_a - mean|| < eps) && done >= times
+ *     while (!stop && done < max_rounds) { x <- W x; ++done; }
+ * runs on one workgroup with x resident in LDS (two images of n_rows x ceil(n_params/4)*4 fp32
+ * plus the CSR: dl_mix_until_fits).  Rounds are the dl_mix_round fold (bit-identical); the
+ * deviation is evaluated before the first round and after each one, as the reference does; the
+ * test is float32 against float32(eps) (numpy >= 2 semantics of np.float32 < float).
+ * status (device int32[2]) receives {rounds done, 1 if the stop rule held / 0 if max_rounds cut
+ * the loop}; a caller continues a cut loop with times' = times - done on y.  dev_trace (nullable,
+ * device float[max_rounds + 1], use_eps only) receives the max deviation of every evaluation in
+ * order (index 0 = before the first round) for the reference's per-round debug log.  y may be x
+ * itself (same ld); otherwise it must not overlap x.  W must be square (col < n_rows). */
+typedef struct dl_mix_until_args {
+    const float *x;     /* [n_rows, ldx] */
+    int64_t ldx;
+    float *y;           /* [n_rows, ldy]: x after the last round */
+    int64_t ldy;
+    int64_t n_params;
+    dl_csr W;
+    int32_t times;      /* minimum rounds (mixer.py:18 `times`, >= 0) */
+    int32_t use_eps;    /* 0 = eps None: exactly `times` rounds */
+    float eps;          /* float32(eps) */
+    int32_t max_rounds; /* >= 1: rounds this launch may run */
+    int32_t *status;    /* device int32[2] */
+    float *dev_trace;   /* nullable device float[max_rounds + 1] */
+} dl_mix_until_args;
+
+/* 1 when dl_mix_until takes these sizes in one workgroup's LDS, else 0. */
+int dl_mix_until_fits(int32_t n_rows, int64_t n_params, int32_t nnz);
+int dl_mix_until(const dl_mix_until_args *args, dl_stream_t stream);
+
 /* Deviation of x from its column mean: dev_sq[a] = ||x_a - mean||^2, dev_max = max sqrt(dev_sq).
  * mean_in nullable: when given (e.g. a global mean all-reduced across GPUs) it is used instead
  * of the local column mean.  mean_out nullable.  Returns zeros when n_rows <= 1 (mixer.py:58-59). */

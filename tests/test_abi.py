@@ -149,3 +149,32 @@ def test_new_entry_points_validate_before_any_device_call():
     pl = _lib.DlMixPlan()
     assert lib.dl_mix_rounds_plan(ctypes.byref(x), ctypes.byref(pl)) == _lib.DL_ERR_UNSUPPORTED
     assert b"halo" in lib.dl_last_error()
+
+
+def test_mix_until_validates_and_sizes():
+    """dl_mix_until / dl_mix_until_fits: argument errors and the LDS fit come back as status
+    codes before any launch (runs without a GPU)."""
+    from distributed_learning_amd import _lib
+    lib = _lib.load()
+    assert lib.dl_mix_until_fits(8, 617, 24) == 1
+    assert lib.dl_mix_until_fits(8, 2048, 24) == 1     # 2 x 64 KiB images + mean + CSR
+    assert lib.dl_mix_until_fits(8, 4096, 24) == 0
+    assert lib.dl_mix_until_fits(8, 1 << 20, 24) == 0
+    assert lib.dl_mix_until_fits(0, 10, 0) == 0
+    u = _lib.DlMixUntilArgs()
+    assert lib.dl_mix_until(None, None) == _lib.DL_ERR_INVALID
+    assert lib.dl_mix_until(ctypes.byref(u), None) == _lib.DL_ERR_INVALID
+    u.x = u.y = 256
+    u.status = 64
+    u.n_params = u.ldx = u.ldy = 64
+    u.W = _lib.DlCsr(16, 16, 16, 4, 12, 3, 0, 0)
+    assert lib.dl_mix_until(ctypes.byref(u), None) == _lib.DL_ERR_INVALID   # max_rounds 0
+    assert b"max_rounds" in lib.dl_last_error()
+    u.max_rounds = 1
+    u.y = 512                                                                # partial overlap
+    assert lib.dl_mix_until(ctypes.byref(u), None) == _lib.DL_ERR_INVALID
+    assert b"overlaps" in lib.dl_last_error()
+    u.y = 256                                                                # in place
+    u.n_params = u.ldx = u.ldy = 1 << 20
+    assert lib.dl_mix_until(ctypes.byref(u), None) == _lib.DL_ERR_UNSUPPORTED
+    assert b"LDS" in lib.dl_last_error()

@@ -115,21 +115,25 @@ def test_unsupported_falls_back_to_single_rounds(cuda):
 
 
 def test_mixer_times_uses_one_pass(cuda):
-    """Mixer.mix(times=K) with eps=None (one dl_mix_rounds pass over padded rows) equals the
-    reference fold applied K times to the flattened models."""
+    """Mixer.mix(times=K) with eps=None on models too large for the one-workgroup loop
+    (dl_mix_until): one dl_mix_rounds pass over padded rows, equal to the reference fold applied
+    K times to the flattened models."""
     import logging
 
     from distributed_learning_amd.networks import ANNModel
     from distributed_learning_amd.utils.consensus_simple import Mixer
     torch.manual_seed(0)
     keys = ["a", "b", "c", "d", "e"]
-    models = {k: ANNModel(30, 17, 5).to(cuda) for k in keys}
+    models = {k: ANNModel(300, 40, 5).to(cuda) for k in keys}
     topo = {"a": {"a": 0.5, "b": 0.25, "e": 0.25}, "b": {"b": 0.5, "a": 0.25, "c": 0.25},
             "c": {"c": 0.5, "b": 0.25, "d": 0.25}, "d": {"d": 0.5, "c": 0.25, "e": 0.25},
             "e": {"e": 0.5, "d": 0.25, "a": 0.25}}
     X0 = np.stack([torch.cat([p.data.reshape(-1) for p in models[k].parameters()]).cpu().numpy()
                    for k in keys])
     rp, cl, w = M.topology_to_csr(topo)
+    from distributed_learning_amd import engine as E
+    from distributed_learning_amd.graph import from_topology
+    assert not E.until_fits(E.DeviceCsr(from_topology(topo), cuda), X0.shape[1])
     want = X0
     for _ in range(9):
         want = M.mix_once(want, rp, cl, w)

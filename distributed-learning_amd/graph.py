@@ -133,6 +133,37 @@ def from_edge_weights(edges, weights, vertices=None):
     return Csr(rowptr, col, w, keys=vertices)
 
 
+def tcp_neighbors(edges, weights, token):
+    """What a consensus_tcp agent folds: its neighbours in the order the master's set
+    comprehension yields them (master.py:230-234, kept by the agent's dict, agent.py:92-96), each
+    with the weight of the first topology edge joining the two (master.py:235-241)."""
+    nbrs = {u if token == v else v for (u, v) in edges if token == u or token == v}
+    own = [((u, v), c) for (u, v), c in zip(edges, weights) if u == token or v == token]
+    return [(n, [c for ((u, v), c) in own if u == n or v == n][0]) for n in nbrs]
+
+
+def from_tcp_weights(edges, weights, vertices=None):
+    """W for ``ConsensusAgent.run_once`` (consensus_tcp/agent.py:204-207)::
+
+        value = (1.0 - sum_j w_j) * value + np.sum([x_j * w_j for j in neighbours], axis=0)
+
+    Row a lists the neighbours in ``tcp_neighbors`` order, then the diagonal ``1 - sum w`` (summed
+    as np.sum does) LAST: the CSR left fold ``((x_1 w_1 + x_2 w_2) + ...) + d x_a`` is the
+    neighbour sum followed by the diagonal term, bit for bit in the arithmetic's own dtype."""
+    vertices = first_appearance_vertices(edges) if vertices is None else list(vertices)
+    index = {k: i for i, k in enumerate(vertices)}
+    rowptr, col, w = [0], [], []
+    for a in vertices:
+        nb = tcp_neighbors(edges, weights, a)
+        for n, c in nb:
+            col.append(index[n])
+            w.append(float(c))
+        col.append(index[a])
+        w.append(float(1.0 - np.sum([c for _, c in nb])))
+        rowptr.append(len(col))
+    return Csr(rowptr, col, w, keys=vertices)
+
+
 def asyncio_tokens(edges):
     """``ConsensusNetwork.tokens`` = ``list(set(np.array(topology).flatten()))`` (:40)."""
     return list(set(np.array(edges).flatten()))

@@ -90,6 +90,23 @@ def mixer_mix(X, rowptr, cols, w, times=1, eps=None):
     return X, done
 
 
+# ------------------------------------------------------------------ consensus_tcp update
+def tcp_run_once(edges, weights, values):
+    """One synchronous ``ConsensusAgent.run_once`` round of every agent
+    (utils/consensus_tcp/agent.py:204-207; neighbours and weights as the master hands them out,
+    master.py:227-243).  values: dict token -> ndarray; returns the new dict.  Restated directly
+    (no CSR), in numpy's own promotion: np.float64(1 - S) * fp32 value is fp64."""
+    out = {}
+    for t, x in values.items():
+        nbrs = {u if t == v else v for (u, v) in edges if t == u or t == v}
+        own = list(filter(lambda uv_c: (uv_c[0][0] == t or uv_c[0][1] == t),
+                          list(zip(edges, weights))))
+        ew = {n: [c for ((u, v), c) in own if (u == n or v == n)][0] for n in nbrs}
+        s = np.sum([ew[n] for n in ew])
+        out[t] = (1.0 - s) * x + np.sum([values[n] * ew[n] for n in ew], axis=0)
+    return out
+
+
 # ------------------------------------------------------------------ asyncio consensus round
 def asyncio_tokens(topology):
     """``ConsensusNetwork.tokens`` (utils/consensus_asyncio.py:40)."""

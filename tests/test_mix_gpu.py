@@ -239,6 +239,33 @@ def test_full_size_round_column_slices(cuda):
                                rtol=DEV_RTOL)
 
 
+@pytest.mark.parametrize("layout,P", [("rows", 10 ** 6), ("rows", 10 ** 6 + 3),
+                                      ("tiled", 10 ** 6 + 8)])
+def test_full_size_tail_columns(cuda, layout, P):
+    """the tail test at P = 10^6 (and ragged widths: 10^6 + 3 is not float4-aligned, so
+    the row-major round takes the guarded tail launch; 10^6 + 8 pads the last 16-column tile),
+    1024 agents, fused local step + deviation.  Column slices at both ends equal the oracle;
+    the fused deviation equals the two-pass dl_deviation of the result."""
+    from distributed_learning_amd.graph import from_edge_weights, random_regular_edges
+    E = eng_mod()
+    n = 1024
+    edges = random_regular_edges(4, n, seed=0)
+    csr = from_edge_weights(edges, [0.2] * len(edges))
+    g = torch.Generator(device=cuda).manual_seed(1)
+    X = torch.randn(n, P, device=cuda, generator=g)
+    G = torch.randn(n, P, device=cuda, generator=g)
+    eng = E.GossipEngine(csr, P, device=cuda, X=X, layout=layout)
+    eng.round(G=eng.layout_like(G), lr=1e-3, deviation=True)
+    torch.cuda.synchronize()
+    Y = eng.rows()
+    for c0, c1 in [(0, 1000), (P - 1037, P)]:
+        want = cref.mix_round(X[:, c0:c1].cpu().numpy(), csr.rowptr, csr.col, csr.w,
+                              G=G[:, c0:c1].cpu().numpy(), lr=1e-3)
+        assert np.array_equal(bits(Y[:, c0:c1].cpu().numpy()), bits(want)), (c0, c1)
+    dsq, _ = E.deviation(Y.contiguous())
+    torch.testing.assert_close(eng.dev_sq, dsq, rtol=DEV_RTOL, atol=0)
+
+
 @pytest.mark.parametrize("n,P,deg", [(64, 4096, 4), (100, 1000, 5), (1024, 4100, 4), (7, 33, 3),
                                      (300, 777, 8)])
 def test_tiled_layout_round_trip_and_parity(cuda, n, P, deg):
@@ -323,3 +350,24 @@ def test_torus_4096_shared_weights_bit_exact(cuda, layout):
     E.mix_round(W, torch.from_numpy(X).to(cuda), Y, G=torch.from_numpy(G).to(cuda), lr=0.01)
     torch.cuda.synchronize()
     assert np.array_equal(bits(Y.cpu().numpy()), bits(want))
+
+
+
+@pytest.mark.parametrize("edges,w", [
+    ([(0, 1), (0, 2), (0, 3), (1, 4), (4, 2)], [1 / 3, 1 / 3, 1 / 2, 1 / 3, 1 / 3]),
+    ([(9, 1), (1, 17), (17, 33), (33, 9), (9, 17)], [0.2, 0.25, 0.3, 0.15, 0.1])])
+def test_tcp_run_once_round(cuda, edges, w):
+    """a7: ConsensusAgent.run_once of every agent (consensus_tcp/agent.py:204-207) as one
+    dl_mix_round over graph.from_tcp_weights: bit-exact with the fp32 CSR fold, within fp32
+    rounding of the reference's fp64-promoted update."""
+    from distributed_learning_amd.graph import from_tcp_weights
+    E = eng_mod()
+    csr = from_tcp_weights(edges, w)
+    rng = np.random.default_rng(3)
+    X = rng.standard_normal((csr.n_rows, 1000), dtype=np.float32)
+    Y = torch.empty(X.shape, device=cuda)
+    E.mix_round(E.DeviceCsr(csr, cuda), torch.from_numpy(X).to(cuda), Y)
+    got = Y.cpu().numpy()
+    assert np.array_equal(bits(got), bits(M.mix_once(X, csr.rowptr, csr.col, csr.w)))
+    want = M.tcp_run_once(edges, w, {k: X[i] for i, k in enumerate(csr.keys)})
+    np.testing.assert_allclose(got, np.stack([want[k] for k in csr.keys]), rtol=1e-5, atol=1e-6)

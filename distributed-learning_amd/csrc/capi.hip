@@ -426,13 +426,15 @@ int dl_mix_rounds(const dl_mix_args *args, int32_t rounds, void *workspace, size
             return fail(DL_ERR_WORKSPACE, "dl_mix_rounds: deviation outputs need a 16-byte "
                                           "aligned workspace of %zu bytes", need);
         t.dev_partial = reinterpret_cast<float *>(ws);
+        t.dev_max_zero = reinterpret_cast<unsigned int *>(args->dev_max);
     }
     hipError_t e = dl::launch_mix_multi(t, pl.chunks, rounds, args->g != nullptr, pl.dev,
                                         pl.pub.grid, pl.pub.lds_bytes, s);
     if (e != hipSuccess) return hip_fail(e, "mix_multi_kernel launch");
     if (pl.dev) {
         if (Nr <= 1) return zero_deviation(Nr, args->dev_sq, args->dev_max, s);
-        e = dl::launch_dev_reduce(t.dev_partial, pl.pub.grid, Nr, args->dev_sq, args->dev_max, s);
+        e = dl::launch_dev_reduce(t.dev_partial, pl.pub.grid, Nr, args->dev_sq, args->dev_max, s,
+                                  true);
         if (e != hipSuccess) return hip_fail(e, "dev_reduce launch");
     }
     return DL_OK;
@@ -587,6 +589,7 @@ int dl_mix_round(const dl_mix_args *args, void *workspace, size_t ws_bytes, dl_s
         t.csr_off = pl.csr_off;
         t.scratch_off = pl.scratch_off;
         float *partial = pl.dev ? reinterpret_cast<float *>(ws) : nullptr;
+        if (pl.dev) t.dev_max_zero = reinterpret_cast<unsigned int *>(args->dev_max);
         if (grid_full > 0) {
             t.n_tiles = (int32_t)n_full;
             t.col_base = 0;
@@ -606,7 +609,7 @@ int dl_mix_round(const dl_mix_args *args, void *workspace, size_t ws_bytes, dl_s
         if (pl.dev) {
             if (Nr <= 1) return zero_deviation(Nr, args->dev_sq, args->dev_max, s);
             hipError_t e = dl::launch_dev_reduce(partial, grid_full + grid_tail, Nr, args->dev_sq,
-                                                 args->dev_max, s);
+                                                 args->dev_max, s, true);
             if (e != hipSuccess) return hip_fail(e, "dev_reduce launch");
         }
         return DL_OK;

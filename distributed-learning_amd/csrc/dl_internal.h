@@ -46,6 +46,8 @@ struct TileArgs {
     uint32_t hrs;     // halo row stride in bytes (ldh*4)
     float *dev_partial;  // [gridDim.x][n_rows] per-workgroup partial ||y_a - mean||^2
     float *mean;         // [n_params] nullable
+    unsigned int *dev_max_zero;  // nullable: workgroup 0 zeroes it (dev_reduce's atomicMax target,
+                                 // so that launch needs no memset of its own)
 };
 
 // LDS bytes the staged CSR needs (0 if it cannot be staged: > 65535 rows/entries).
@@ -65,8 +67,9 @@ int tile_passes(int chunks, int n_src, bool fast);
 // K rounds of mixing on LDS-resident tiles (mix_multi.hip); FAST tiles only, no halo rows
 hipError_t launch_mix_multi(const TileArgs &a, int chunks, int rounds, bool sgd, bool dev,
                             int grid, int lds, hipStream_t s);
+// max_zeroed: an earlier launch on the stream already zeroed dev_max (TileArgs::dev_max_zero)
 hipError_t launch_dev_reduce(const float *partial, int nparts, int n_rows, float *dev_sq,
-                             float *dev_max, hipStream_t s);
+                             float *dev_max, hipStream_t s, bool max_zeroed = false);
 hipError_t launch_column_sum(const float *x, int64_t ldx, int n_rows, int64_t n_params,
                              float *colsum, float scale, hipStream_t s);
 hipError_t launch_dev_rows(const float *x, int64_t ldx, int n_rows, int64_t n_params,

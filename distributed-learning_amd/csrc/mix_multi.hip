@@ -259,6 +259,7 @@ __global__ void __launch_bounds__(kTileThreads) mix_multi_kernel(TileArgs a, int
             const int ag = s + k * SLOTS;
             if (k < KV && ag < Nr) a.dev_partial[(int64_t)blockIdx.x * Nr + ag] = dacc[j];
         }
+        if (a.dev_max_zero != nullptr && blockIdx.x == 0 && tid == 0) *a.dev_max_zero = 0u;
     }
 }
 

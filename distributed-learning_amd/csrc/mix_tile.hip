@@ -374,6 +374,7 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
             const int ag = s + k * SLOTS;
             if (k < KV && ag < Nr) a.dev_partial[(int64_t)blockIdx.x * Nr + ag] = dacc[j];
         }
+        if (a.dev_max_zero != nullptr && blockIdx.x == 0 && tid == 0) *a.dev_max_zero = 0u;
     }
 }
 
@@ -578,8 +579,8 @@ hipError_t launch_mix_gather(const TileArgs &a, bool sgd, hipStream_t s) {
 }
 
 hipError_t launch_dev_reduce(const float *partial, int nparts, int n_rows, float *dev_sq,
-                             float *dev_max, hipStream_t s) {
-    if (dev_max) {
+                             float *dev_max, hipStream_t s, bool max_zeroed) {
+    if (dev_max && !max_zeroed) {
         hipError_t e = hipMemsetAsync(dev_max, 0, sizeof(float), s);
         if (e != hipSuccess) return e;
     }

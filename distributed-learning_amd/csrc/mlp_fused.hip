@@ -12,8 +12,11 @@
 //   * weights stream through one LDS staging area, two slices ahead in registers while the
 //     MFMAs consume the current one (pipeline2);
 //   * weight gradients go from the MFMA accumulators straight into the agent's row of G (the
-//     Mixer flatten order, mixer.py:69), bias gradients are fixed-order column sums, and the
-//     per-agent loss is summed in a fixed order (deterministic, hipGraph-replay stable).
+//     Mixer flatten order, mixer.py:69), and the per-agent loss is summed in a fixed order
+//     (deterministic, hipGraph-replay stable);
+//   * bias gradients db = sum_b dZ[b][:] ride along in the weight-gradient MFMAs: the layer's
+//     input image carries a column of ones at index K (H1/H2/H3 column dh, the last x chunk's
+//     column din), whose tile column is db -- no serial 64-row column sums at the phase ends.
 // LDS strides per access (ds_read_b32 banks are dword mod 32 per 32-lane half,
 // MI355X_MICROARCH.md §LDS):
 //   [row][k] images read by 16 rows x 4 k   -> stride = 4 (mod 8)  floats  (36, 156): 2-way (a
@@ -59,7 +62,6 @@ __device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
 
-__device__ __forceinline__ int round4(int v) { return (v + 3) & ~3; }
 
 // Two slices in flight: while the MFMAs consume slice s from LDS, the global loads of slices
 // s + 1 and s + 2 are outstanding in two register sets (HBM latency under full load is longer
@@ -129,6 +131,7 @@ struct PRow {
 // [rows][ld] matrix inside a parameter row (a weight or bias, Mixer order offsets)
 template <bool TILED>
 struct ParMat {
+    static constexpr bool kLinear = !TILED;   // element (r, c) at a fixed row stride ld
     PRow<TILED> row;
     int off;
     int ld;
@@ -138,10 +141,33 @@ struct ParMat {
 // Store a finished 32 x 32 MFMA tile: register r holds row i0 + (r & 3) + 8 (r >> 2) of this
 // lane's column j (C/D map); every store instruction writes two 128-B runs.  (Issuing these
 // stores interleaved with the next tile's MFMA chain measured slower: dW1 53 -> 64 us.)
+// Column j == cols is the ones column of the input image: its values are the bias gradient.
 template <typename M>
 __device__ __forceinline__ void store_tile(const f32x16 &v, int i0, int j, const M &m, int rows,
-                                           int cols) {
-    if (j >= cols) return;
+                                           int cols, const M &bias) {
+    if (j > cols) return;
+    if (j == cols) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int i = i0 + (r & 3) + 8 * (r >> 2);
+            if (i < rows) *bias.at(0, i) = v[r];
+        }
+        return;
+    }
+    if (i0 + 27 < rows) {   // every row of this lane's 16 (i0 + 0..3, + 8.., + 16.., + 24..)
+        // one base address per lane, the 16 rows as ld-strided 32-bit offsets from it: no
+        // per-store bounds branch (exec juggling) and no 64-bit address math per store
+        if constexpr (M::kLinear) {
+            float *p = m.at(i0, j);
+            const int ld = m.ld;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) p[((r & 3) + 8 * (r >> 2)) * ld] = v[r];
+        } else {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) *m.at(i0 + (r & 3) + 8 * (r >> 2), j) = v[r];
+        }
+        return;
+    }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         const int i = i0 + (r & 3) + 8 * (r >> 2);
@@ -295,12 +321,38 @@ __device__ __forceinline__ void epi_rows64(const f32x4 (&acc)[5], F f) {
               acc[t][r]);
 }
 
+// The five bias values of this lane's output columns (epi_rows64's n for t = 0..4), loaded
+// before the layer's MFMAs so their latency hides behind them instead of stalling the epilogue.
+template <typename M>
+__device__ __forceinline__ void load_bias5(const M &bias, int dh, float (&bv)[5]) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int t = 0; t < 5; ++t) {
+        const int n = (wave >> 2) * 80 + 16 * t + (lane & 15);
+        bv[t] = n < dh ? *bias.at(0, n) : 0.f;
+    }
+}
+
+// epi_rows64 with the N-tile index t passed along (for per-column values held in registers)
+template <typename F>
+__device__ __forceinline__ void epi_rows64_t(const f32x4 (&acc)[5], F f) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int t = 0; t < 5; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            f((wave & 3) * 16 + 4 * (lane >> 4) + r, (wave >> 2) * 80 + 16 * t + (lane & 15), t,
+              acc[t][r]);
+}
+
 // Forward layer on an LDS-resident input: H = act(Hin W^T + b), K = N = dh, W staged by slices.
 template <typename M>
 __device__ __forceinline__ void forward_hidden(const M &W, const M &bias, int dh, const float *Hin,
                                                float *Hout, float *stage, int layer) {
     f32x4 acc[5];
     zero(acc);
+    float bv[5];
+    load_bias5(bias, dh, bv);
     pipeline2<RowSlice<160>>(
         (dh + BK - 1) / BK,
         [&](RowSlice<160> &w, int s) { w.load(W, dh, dh, s * BK); },
@@ -309,8 +361,8 @@ __device__ __forceinline__ void forward_hidden(const M &W, const M &bias, int dh
             const int k0 = s * BK;
             mma_rows64<false>(acc, Hin + k0, LDH, stage);
         });
-    epi_rows64(acc, [&](int m, int n, float v) {
-        if (n < dh) Hout[m * LDH + n] = act_fwd(layer, v + *bias.at(0, n));
+    epi_rows64_t(acc, [&](int m, int n, int t, float v) {
+        if (n < dh) Hout[m * LDH + n] = act_fwd(layer, v + bv[t]);
     });
 }
 
@@ -334,7 +386,8 @@ __device__ __forceinline__ void backward_dz(const M &W, int dk, int dh, const fl
 }
 
 // Weight gradient of a hidden layer: dW[i][j] = sum_b dZ[b][i] Hin[b][j] (both LDS-resident,
-// [64][LDH]), i, j < dh, straight into G; bias gradient db[i] = sum_b dZ[b][i] in order.
+// [64][LDH]), i, j < dh, straight into G; bias gradient db[i] = sum_b dZ[b][i] from Hin's ones
+// column j = dh (N-tile 4).
 // 25 tiles of 32 x 32 (v_mfma_f32_32x32x2_f32: half the operand reads of 16x16x4 per flop),
 // wave w computes tiles w, w + 8, w + 16 (, 24) one after the other, so each tile's stores
 // overlap the next tile's MFMAs (one accumulator: the 32x32x2 issue interval equals its
@@ -349,17 +402,16 @@ __device__ __forceinline__ void weight_grad_hidden(const float *dZ, const float 
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[r] = 0.f;
         const int ia = (t / 5) * 32 + (lane & 31), jb = (t % 5) * 32 + (lane & 31);
+#if MLP_PROBE_MODE != 7   // measurement only: 7 = no hidden-layer dW MFMAs
 #pragma unroll 8
         for (int ks = 0; ks < MB / 2; ++ks) {
             const int b = 2 * ks + (lane >> 5);
             acc = mfma32(dZ[b * LDH + ia], Hin[b * LDH + jb], acc);
         }
-        store_tile(acc, (t / 5) * 32 + 4 * (lane >> 5), jb, gW, dh, dh);
-    }
-    if (threadIdx.x < dh) {
-        float s = 0.f;
-        for (int b = 0; b < MB; ++b) s += dZ[b * LDH + threadIdx.x];
-        *gb.at(0, threadIdx.x) = s;
+#endif
+#if MLP_PROBE_MODE != 6   // measurement only: 6 = no hidden-layer dW stores
+        store_tile(acc, (t / 5) * 32 + 4 * (lane >> 5), jb, gW, dh, dh, gb);
+#endif
     }
 }
 
@@ -414,12 +466,15 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
     for (int e = tid; e < LDS_FLOATS / 4; e += NTHR)
         reinterpret_cast<f32x4 *>(lds)[e] = f32x4{0.f, 0.f, 0.f, 0.f};
     __syncthreads();
+    if (tid < MB) H1[tid * LDH + dh] = 1.f;   // ones column: db2 in dW2's MFMAs
 
     // ---- layer 1: H1 = relu(x W1^T + b1), K = din from HBM: x and W1 slices double-buffered in
     // LDS (the H2/H3 space, free until layer 2), the next two register-prefetched
     {
         f32x4 acc[5];
         zero(acc);
+        float bv[5];
+        load_bias5(mat(Xr, o_b1, 0), dh, bv);
         constexpr int IMG = MB * LDS1 + 160 * LDS1;   // one [x | W1] slice image
         static_assert(2 * IMG <= 2 * H_FLOATS, "two slice images fit the H2/H3 space");
         struct L1 {
@@ -448,47 +503,71 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
                 mma_rows64<false>(acc, H2 + buf * IMG, LDS1, H2 + buf * IMG + MB * LDS1);
 #endif
             });
-        epi_rows64(acc, [&](int m, int n, float v) {
-            if (n < dh) H1[m * LDH + n] = act_fwd(0, v + *Xr.at(o_b1 + n));
+        epi_rows64_t(acc, [&](int m, int n, int t, float v) {
+            if (n < dh) H1[m * LDH + n] = act_fwd(0, v + bv[t]);
         });
+    }
+    if (tid < MB) {   // ones columns: db3 in dW3's MFMAs (H2), db4 in dW4's (H3)
+        H2[tid * LDH + dh] = 1.f;
+        H3[tid * LDH + dh] = 1.f;
     }
     __syncthreads();
     STAMP(1);
     forward_hidden(mat(Xr, o_w2, dh), mat(Xr, o_b2, 0), dh, H1, H2, stage, 1);
     __syncthreads();
     STAMP(2);
+    // the logits' operands from HBM (W4 image values, b4, this wave's labels), issued now so they
+    // land while layer 3 runs instead of stalling the head
+    constexpr int W4PER = (16 * LDW4 + NTHR - 1) / NTHR;
+    float w4v[W4PER];
+#pragma unroll
+    for (int i = 0; i < W4PER; ++i) {
+        const int e = tid + i * NTHR;
+        const int n = e / LDW4, k = e % LDW4;
+        w4v[i] = (e < 16 * LDW4 && n < dout && k < dh) ? *Xr.at(o_w4 + n * dh + k) : 0.f;
+    }
+    const float b4v = (lane & 15) < dout ? *Xr.at(o_b4 + (lane & 15)) : 0.f;
+    int lab[MB / 8];
+#pragma unroll
+    for (int i = 0; i < MB / 8; ++i) lab[i] = p.labels[(int64_t)a * p.s_lab + wave + 8 * i];
     forward_hidden(mat(Xr, o_w3, dh), mat(Xr, o_b3, 0), dh, H2, H3, stage, 2);
     STAMP(3);
     // ---- logits Z = H3 W4^T + b4 (waves 0-3, one 16 x 16 tile each), W4 image [16][LDW4]
-    for (int e = tid; e < 16 * LDW4; e += NTHR) {
-        const int n = e / LDW4, k = e % LDW4;
-        stage[e] = (n < dout && k < dh) ? *Xr.at(o_w4 + n * dh + k) : 0.f;
+#pragma unroll
+    for (int i = 0; i < W4PER; ++i) {
+        const int e = tid + i * NTHR;
+        if (e < 16 * LDW4) stage[e] = w4v[i];
     }
     __syncthreads();
     if (wave < 4) {
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
         const int m = wave * 16 + (lane & 15);
-        for (int kk = 0; kk < round4(dh); kk += 4) {
+        // fixed trip count (dh <= 152): columns dh.. of the W4 image are zero, so the extra
+        // k-steps add exact zeros (H3's ones column meets a zero)
+#pragma unroll
+        for (int kk = 0; kk < 152; kk += 4) {
             const int k = kk + (lane >> 4);
             acc = mfma4(H3[m * LDH + k], stage[(lane & 15) * LDW4 + k], acc);
         }
         const int n = lane & 15;
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-            if (n < dout) Zs[(wave * 16 + 4 * (lane >> 4) + r) * LDZ + n] = acc[r] + *Xr.at(o_b4 + n);
+            if (n < dout) Zs[(wave * 16 + 4 * (lane >> 4) + r) * LDZ + n] = acc[r] + b4v;
     }
     __syncthreads();
     // ---- cross-entropy head (torch.nn.CrossEntropyLoss, mean): dZ4 = (softmax - onehot) / 64
     {
         float lsum = 0.f;
-        for (int m = wave; m < MB; m += 8) {
+#pragma unroll
+        for (int i = 0; i < MB / 8; ++i) {
+            const int m = wave + 8 * i;
             const float v = lane < dout ? Zs[m * LDZ + lane] : 0.f;
             float mx = lane < dout ? v : -INFINITY;
             for (int s = 32; s >= 1; s >>= 1) mx = fmaxf(mx, __shfl_xor(mx, s));
             const float e = lane < dout ? expf(v - mx) : 0.f;
             float sum = e;
             for (int s = 32; s >= 1; s >>= 1) sum += __shfl_xor(sum, s);
-            const int label = p.labels[(int64_t)a * p.s_lab + m];
+            const int label = lab[i];
             const float zl = __shfl(v, label);
             if (lane < dout) Zs[m * LDZ + lane] = (e / sum - (lane == label ? 1.f : 0.f)) / (float)MB;
             lsum += (logf(sum) + mx - zl) / (float)MB;
@@ -513,12 +592,8 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
             for (int r = 0; r < 4; ++r) {
                 const int i = 4 * (lane >> 4) + r;
                 if (i < dout && j < dh) *Gr.at(o_w4 + i * dh + j) = acc[r];
+                if (i < dout && j == dh) *Gr.at(o_b4 + i) = acc[r];   // H3's ones column
             }
-        }
-        if (tid < dout) {
-            float s = 0.f;
-            for (int b = 0; b < MB; ++b) s += Zs[b * LDZ + tid];
-            *Gr.at(o_b4 + tid) = s;
         }
     }
     __syncthreads();
@@ -552,12 +627,13 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
             for (int i = 0; i < PER; ++i) {
                 const int e = tid + i * NTHR;
                 const int b = e / (CW / 4), c = 4 * (e % (CW / 4));
+                // column din is the ones column (db1); din % 4 == 0 puts it at a float4 start
                 xv[i] = c0 + c < din ? *reinterpret_cast<const f32x4 *>(x + (int64_t)b * din + c0 + c)
-                                     : f32x4{0.f, 0.f, 0.f, 0.f};
+                        : c0 + c == din ? f32x4{1.f, 0.f, 0.f, 0.f} : f32x4{0.f, 0.f, 0.f, 0.f};
             }
         };
-        const int nc = (din + CW - 1) / CW;
-        const PM gw1 = mat(Gr, o_w1, din);
+        const int nc = (din + CW) / CW;          // through column din (the ones column)
+        const PM gw1 = mat(Gr, o_w1, din), gb1 = mat(Gr, o_b1, 0);
         load(0);
         for (int ci = 0; ci < nc; ++ci) {
 #pragma unroll
@@ -571,7 +647,7 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
             // (N-tile, M-tile) items of this chunk round-robin over the waves, one 32 x 32 tile at a
             // time: its 16 stores go out while the wave's next tile runs on the matrix core (the
             // G writes of dW1 are a quarter of the kernel's HBM traffic)
-            const int ntc = min(CW / 32, (din - c0 + 31) / 32);
+            const int ntc = min(CW / 32, (din + 1 - c0 + 31) / 32);
             for (int it = wave; it < 5 * ntc; it += 8) {
                 const int nt = it % ntc, t = it / ntc;
                 const int nl = 32 * nt + (lane & 31);
@@ -586,15 +662,10 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
                 }
 #endif
 #if MLP_PROBE_MODE != 4   // measurement only: 4 = no dW1 stores
-                store_tile(acc, 32 * t + 4 * (lane >> 5), c0 + nl, gw1, dh, din);
+                store_tile(acc, 32 * t + 4 * (lane >> 5), c0 + nl, gw1, dh, din, gb1);
 #endif
             }
             __syncthreads();
-        }
-        if (tid < dh) {
-            float s = 0.f;
-            for (int b = 0; b < MB; ++b) s += H1[b * LDH + tid];
-            *Gr.at(o_b1 + tid) = s;
         }
     }
     STAMP(10);

@@ -287,12 +287,19 @@ __device__ __forceinline__ void mma_rows64(f32x4 (&acc)[5], const float *A, int 
     float a[2], b[2][5];
     auto read = [&](int s, int buf) {
         const int k = 4 * s + (lane >> 4);
+#if MLP_PROBE_MODE == 8   // measurement only: fragments from registers, not LDS
+        a[buf] = (float)(k + m);
+#pragma unroll
+        for (int t = 0; t < 5; ++t) b[buf][t] = (float)(n0 + 16 * t + k);
+        (void)A; (void)lda; (void)Bs;
+#else
         a[buf] = A[m * lda + k];
 #pragma unroll
         for (int t = 0; t < 5; ++t) {
             const int n = n0 + 16 * t;
             b[buf][t] = B_KMAJOR ? Bs[k * LDT + n] : Bs[n * LDS1 + k];
         }
+#endif
     };
     read(0, 0);
 #pragma unroll

@@ -39,6 +39,13 @@ class DlMixUntilArgs(ctypes.Structure):
                 ("max_rounds", _i32), ("status", _vp), ("dev_trace", _vp)]
 
 
+class DlConsensusGdArgs(ctypes.Structure):
+    _fields_ = [("X", _vp), ("y", _vp), ("shard_ptr", _vp), ("n_agents", _i32),
+                ("n_features", _i32), ("row_ptr", _vp), ("col", _vp), ("eps", _f64),
+                ("conv_eps", _f64), ("mean_weight", _f64), ("tau", _f64), ("steps", _vp),
+                ("iterations", _i32), ("max_iter", _i32), ("w", _vp), ("iters_out", _vp)]
+
+
 class DlMixPlan(ctypes.Structure):
     _fields_ = [("path", _i32), ("tile_cols", _i32), ("grid", _i32), ("lds_bytes", _i32),
                 ("n_tiles", _i32), ("regular", _i32)]
@@ -91,6 +98,7 @@ SIGNATURES = {
     "dl_mix_rounds": (_i32, [ctypes.POINTER(DlMixArgs), _i32, _vp, _sz, _vp]),
     "dl_mix_until_fits": (_i32, [_i32, _i64, _i32]),
     "dl_mix_until": (_i32, [ctypes.POINTER(DlMixUntilArgs), _vp]),
+    "dl_consensus_gd": (_i32, [ctypes.POINTER(DlConsensusGdArgs), _i32, _vp]),
     "dl_deviation_workspace_bytes": (_sz, [_i32, _i64]),
     "dl_deviation": (_i32, [_vp, _i64, _i32, _i64, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "dl_deviation_tiled": (_i32, [_vp, _i32, _i64, _i32, _vp, _vp, _vp, _vp, _sz, _vp]),

@@ -491,6 +491,48 @@ int dl_mix_until(const dl_mix_until_args *a, dl_stream_t stream) {
     return e == hipSuccess ? DL_OK : hip_fail(e, "mix_until_kernel launch");
 }
 
+int dl_consensus_gd(const dl_consensus_gd_args *a, int32_t total_rows, dl_stream_t stream) {
+    g_err.clear();
+    if (!a) return fail(DL_ERR_INVALID, "dl_consensus_gd: args is NULL");
+    if (!a->X || !a->y || !a->shard_ptr || !a->row_ptr || !a->steps || !a->w)
+        return fail(DL_ERR_INVALID, "dl_consensus_gd: null X/y/shard_ptr/row_ptr/steps/w");
+    if (a->n_agents <= 0 || a->n_features <= 0 || a->n_features > 16 || total_rows <= 0 ||
+        a->iterations < 0 || a->max_iter < 1)
+        return fail(DL_ERR_INVALID, "dl_consensus_gd: need n_agents > 0, 0 < n_features <= 16, "
+                                    "rows > 0, iterations >= 0, max_iter >= 1");
+    if (!(a->mean_weight > 0.0))
+        return fail(DL_ERR_INVALID, "dl_consensus_gd: mean_weight must be > 0");
+    int64_t x_off = 0;
+    bool in_lds = dl::gd_lds_bytes(a->n_agents, a->n_features, total_rows, true, &x_off) <=
+                  dl::kLdsBytes;
+    const int64_t lds = dl::gd_lds_bytes(a->n_agents, a->n_features, total_rows, in_lds, &x_off);
+    if (lds > dl::kLdsBytes)
+        return fail(DL_ERR_UNSUPPORTED, "dl_consensus_gd: %d agents x %d features do not fit LDS",
+                    a->n_agents, a->n_features);
+    if (a->iterations == 0) return DL_OK;
+    dl::GdArgs g{};
+    g.X = a->X;
+    g.y = a->y;
+    g.shard_ptr = a->shard_ptr;
+    g.n_agents = a->n_agents;
+    g.n_features = a->n_features;
+    g.rowptr = a->row_ptr;
+    g.col = a->col;
+    g.eps = a->eps;
+    g.conv_eps = a->conv_eps;
+    g.mean_weight = a->mean_weight;
+    g.tau = a->tau;
+    g.steps = a->steps;
+    g.iterations = a->iterations;
+    g.max_iter = a->max_iter;
+    g.w = a->w;
+    g.iters_out = a->iters_out;
+    g.x_in_lds = in_lds ? 1 : 0;
+    g.x_off = x_off;
+    hipError_t e = dl::launch_consensus_gd(g, (int)lds, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? DL_OK : hip_fail(e, "consensus_gd_kernel launch");
+}
+
 const char *dl_last_error(void) { return g_err.c_str(); }
 
 size_t dl_mix_workspace_bytes(int32_t n_rows, int32_t n_halo, int64_t n_params) {

@@ -134,6 +134,30 @@ struct UntilArgs {
 int64_t until_lds_bytes(int n_rows, int64_t n_params, int nnz);
 hipError_t launch_mix_until(const UntilArgs &a, hipStream_t s);
 
+// c1 consensus GD, all agents and iterations in one workgroup (consensus_gd.hip)
+struct GdArgs {
+    const double *X;
+    const double *y;
+    const int32_t *shard_ptr;
+    int32_t n_agents;
+    int32_t n_features;
+    const int32_t *rowptr;
+    const int32_t *col;
+    double eps;
+    double conv_eps;
+    double mean_weight;
+    double tau;
+    const double *steps;
+    int32_t iterations;
+    int32_t max_iter;
+    double *w;
+    int32_t *iters_out;
+    int32_t x_in_lds;
+    int64_t x_off;
+};
+int64_t gd_lds_bytes(int n_agents, int n_features, int rows, bool x_in_lds, int64_t *x_off);
+hipError_t launch_consensus_gd(const GdArgs &a, int lds_bytes, hipStream_t s);
+
 enum Epi {
     EPI_NONE = 0,
     EPI_BIAS = 1,

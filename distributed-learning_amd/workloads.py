@@ -54,6 +54,71 @@ async def consensus_gd(topology, X, y, iterations, alpha=1e-1, tau=1e-4, converg
     return {a.token: w for a, w in zip(agents, res)}
 
 
+class ConsensusGDRun:
+    """``consensus_gd`` with every agent and every iteration in ONE launch (dl_consensus_gd):
+    the same shards (``split_data`` in ``ConsensusNetwork.tokens`` order), local steps and
+    consensus rounds (weighted by shard size, ``convergence_eps`` one-sided test), fp64 on the
+    device with no host round trip per iteration.  The constructor makes everything resident
+    (shards, adjacency, step sizes, zero weights); ``launch()`` is stream-ordered; ``result()``
+    copies back ({token: final w}, Jacobi iterations per round)."""
+
+    def __init__(self, topology, X, y, iterations, alpha=1e-1, tau=1e-4, convergence_eps=1e-10,
+                 schedule="sqrt", device=None, max_iter=10_000_000):
+        import torch
+
+        from . import _lib
+        from .graph import asyncio_adjacency, perron_eps
+        self._torch, self._lib = torch, _lib
+        self.dev = torch.device(device) if device is not None else torch.device(
+            "cuda", torch.cuda.current_device())
+        self.tokens, rp, cl = asyncio_adjacency(topology)
+        shards = split_data(X, y, self.tokens)
+        Xs = np.concatenate([shards[t][0] for t in self.tokens]).astype(np.float64)
+        ys = np.concatenate([shards[t][1] for t in self.tokens]).astype(np.float64)
+        sizes = [shards[t][0].shape[0] for t in self.tokens]
+        sp = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int32)
+        steps = np.asarray([alpha * np.power(it + 1, -0.5) if schedule == "sqrt" else alpha
+                            for it in range(iterations)], np.float64)
+        self.rows, self.iterations = int(Xs.shape[0]), int(iterations)
+        F = X.shape[1]
+        self.t = {k: torch.as_tensor(v, device=self.dev) for k, v in
+                  dict(X=Xs, y=ys, sp=sp, rp=rp.astype(np.int32), cl=cl.astype(np.int32),
+                       steps=steps if iterations else np.zeros(1),
+                       w=np.zeros((len(self.tokens), F))).items()}
+        self.iters = torch.zeros(max(iterations, 1), dtype=torch.int32, device=self.dev)
+        t = self.t
+        self.args = _lib.DlConsensusGdArgs(
+            _lib.ptr(t["X"]), _lib.ptr(t["y"]), _lib.ptr(t["sp"]), len(self.tokens), F,
+            _lib.ptr(t["rp"]), _lib.ptr(t["cl"]), float(perron_eps(topology, self.tokens)),
+            float(convergence_eps), sum(sizes) / len(sizes), float(tau), _lib.ptr(t["steps"]),
+            self.iterations, int(max_iter), _lib.ptr(t["w"]), _lib.ptr(self.iters))
+
+    def launch(self, reset=True):
+        """All iterations from zero weights (reset) on the current stream."""
+        import ctypes
+        if reset:
+            self.t["w"].zero_()
+        with self._torch.cuda.device(self.dev):
+            self._lib.check(self._lib.load().dl_consensus_gd(
+                ctypes.byref(self.args), self.rows, self._lib.stream_handle(self.dev)),
+                "dl_consensus_gd")
+
+    def result(self):
+        wf = self.t["w"].cpu().numpy()
+        return ({tok: wf[i] for i, tok in enumerate(self.tokens)},
+                self.iters[:self.iterations].cpu().numpy())
+
+
+def consensus_gd_device(topology, X, y, iterations, alpha=1e-1, tau=1e-4, convergence_eps=1e-10,
+                        schedule="sqrt", device=None, max_iter=10_000_000):
+    """One-launch ``consensus_gd`` (ConsensusGDRun).  Returns ({token: final w}, Jacobi
+    iterations per round)."""
+    run = ConsensusGDRun(topology, X, y, iterations, alpha, tau, convergence_eps, schedule,
+                         device, max_iter)
+    run.launch()
+    return run.result()
+
+
 def accuracy(w, X, y):
     m = LogRegTitanic(X.shape[1])
     m.W = w

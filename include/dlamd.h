@@ -14,6 +14,13 @@
  *   dl_step_rows        <- (multi-GPU) boundary rows x - lr*g packed for the halo exchange that
  *                          replaces the per-neighbour value messages of consensus_asyncio.py:236-284
  *   dl_column_sum       <- the np.mean numerator of mixer.py:61 (multi-GPU global mean)
+ *   dl_mix_rounds       <- Mixer.mix(times=K) with eps=None: K rounds in one HBM pass  mixer.py:18-38
+ *   dl_mix_until        <- Mixer.mix(times, eps): loop, deviation and stop rule in one launch
+ *                          mixer.py:18-41
+ *   dl_consensus_gd     <- the Titanic notebook's consensus GD run (local logreg steps,
+ *                          networks/logreg_model_titanic.py:16-20, + run_round per iteration)
+ *   dl_sgd_step, dl_mlp_grad, dl_bgemm, dl_xent_grad <- the per-agent training steps of configs
+ *                          c3/c5 (torch.optim.SGD, ANNModel autograd)
  *
  * Conventions
  *   - Every pointer argument is a DEVICE pointer owned by the caller; nothing is allocated inside.
@@ -160,6 +167,39 @@ typedef struct dl_mix_until_args {
     int32_t *status;    /* device int32[2] */
     float *dev_trace;   /* nullable device float[max_rounds + 1] */
 } dl_mix_until_args;
+
+/* BASELINE config c1 as one launch: `iterations` rounds of the Titanic notebook's consensus GD
+ * (cells 12-14) for every agent, fp64 -- per agent a local step on its shard of the L2-regularised
+ * logistic loss (networks/logreg_model_titanic.py:16-20)
+ *     w <- w - steps[it] * ( -(sum_i y_i sigmoid(-y_i x_i.w) x_i) / n_a + tau w )
+ * then one asyncio consensus round (consensus_asyncio.py:209-312) weighted by the shard sizes n_a:
+ * the dl_perron_round Jacobi (pre-scale w n_a / mean_weight, y <- y (1 - eps deg) + eps sum_nbr y,
+ * until every agent's one-sided test against its neighbours' previous values holds, at most
+ * max_iter iterations).  Agent a owns rows [shard_ptr[a], shard_ptr[a+1]) of X [rows][n_features]
+ * and y; row_ptr/col list each agent's neighbours in its socket order (no self loops).  w (device,
+ * [n_agents][n_features]) holds the start weights and receives the final ones; iters_out
+ * (nullable, device int32[iterations]) the Jacobi iterations of each round.  One workgroup:
+ * n_features <= 16, and the agents' values, shards (if they fit LDS, else read from L2) and the
+ * step sizes (host-computed, e.g. alpha (it+1)^-0.5) are device memory. */
+typedef struct dl_consensus_gd_args {
+    const double *X;
+    const double *y;
+    const int32_t *shard_ptr;   /* [n_agents + 1], shard_ptr[0] == 0 */
+    int32_t n_agents;
+    int32_t n_features;
+    const int32_t *row_ptr;     /* [n_agents + 1] neighbour lists */
+    const int32_t *col;
+    double eps;                 /* 0.95 / max degree (consensus_asyncio.py:78-86) */
+    double conv_eps;
+    double mean_weight;         /* mean shard size */
+    double tau;
+    const double *steps;        /* [iterations] */
+    int32_t iterations;
+    int32_t max_iter;
+    double *w;
+    int32_t *iters_out;
+} dl_consensus_gd_args;
+int dl_consensus_gd(const dl_consensus_gd_args *args, int32_t total_rows, dl_stream_t stream);
 
 /* 1 when dl_mix_until takes these sizes in one workgroup's LDS, else 0. */
 int dl_mix_until_fits(int32_t n_rows, int64_t n_params, int32_t nnz);

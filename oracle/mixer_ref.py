@@ -151,3 +151,34 @@ def jacobi_round(topology, values, weights, conv_eps, max_iter=1_000_000):
         if all(flags):
             return y, k
     return y, max_iter
+
+
+def logreg_gradient(X, y, w, tau=1e-4):
+    """``LogRegTitanic.gradient`` (networks/logreg_model_titanic.py:16-20)."""
+    def sig(x):
+        return 1.0 / (1.0 + np.exp(-x))
+    return -np.array([np.dot(y * sig(-y * (X @ w)), X[:, j])
+                      for j in range(X.shape[1])]) / X.shape[0] + tau * w
+
+
+def consensus_gd(topology, X, y, iterations, alpha=1e-1, tau=1e-4, conv_eps=1e-10,
+                 schedule="sqrt"):
+    """The Titanic notebook's consensus GD run (cells 12-14) restated synchronously: shards split
+    in ``ConsensusNetwork.tokens`` order, a local step per agent, then ``jacobi_round`` weighted
+    by shard size.  Pinned bit for bit to the reference's 4000-step asyncio run by
+    tests/test_oracle_golden.py.  Returns ({token: w}, [Jacobi iterations per round])."""
+    toks = asyncio_tokens(topology)
+    sh, tX, ty = {}, X.copy(), y.copy()
+    for i in range(len(toks)):
+        ln = len(tX) // (len(toks) - i)
+        sh[toks[i]] = (tX[:ln], ty[:ln])
+        tX, ty = tX[ln:], ty[ln:]
+    w = {t: np.zeros(X.shape[1]) for t in toks}
+    ks = []
+    for it in range(iterations):
+        step = alpha * np.power(it + 1, -0.5) if schedule == "sqrt" else alpha
+        for t in toks:
+            w[t] = w[t] - step * logreg_gradient(*sh[t], w[t], tau)
+        w, k = jacobi_round(topology, w, {t: sh[t][0].shape[0] for t in toks}, conv_eps)
+        ks.append(k)
+    return w, ks

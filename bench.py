@@ -415,7 +415,7 @@ def run_c4(args, dev, rank, world):
     else:
         parts = sharding.torus_block_partition(rows, cols, world)
         rp = sharding.halo_plans(csr, parts)[rank]
-        shard = sharding.HaloShard(rp, P, dev, sharding.DistTransport(), chunk_cols=P // 8,
+        shard = sharding.HaloShard(rp, P, dev, sharding.dist_transport(), chunk_cols=P // 8,
                                    n_agents_total=n)
         shard.X.normal_(generator=gen)
         G = torch.randn(rp.n_local, P, device=dev, generator=gen)
@@ -451,8 +451,9 @@ def run_c4(args, dev, rank, world):
         "data": "synthetic (X, G ~ N(0,1) resident in HBM)",
         "config": {"workload": "c4: 64x64 torus, fused local step + mix + deviation",
                    "agents": n, "params": P, "weights": f"best-constant {wconst:.6f}",
-                   "parallelism": f"2-D torus blocks x{world}, RCCL halo exchange"
-                   if world > 1 else "single GPU", "plan": plan,
+                   "parallelism": f"2-D torus blocks x{world}, "
+                                  f"{'RCCL' if args.dist_backend == 'nccl' else args.dist_backend}"
+                                  f" halo exchange" if world > 1 else "single GPU", "plan": plan,
                    "halo_rows_rank0": halo_rows,
                    "halo_bytes_per_round_rank0": halo_rows * P * 4},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

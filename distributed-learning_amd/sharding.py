@@ -184,6 +184,44 @@ class DistTransport:
         return t
 
 
+class _StagedWork:
+    def __init__(self, works, host, dev):
+        self.works, self.host, self.dev = works, host, dev
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
+        for q, t in self.dev.items():
+            t.copy_(self.host[q], non_blocking=False)
+
+
+class StagedTransport(DistTransport):
+    """DistTransport for a backend that moves only host tensors (gloo): device buffers are
+    copied to the host before the send and back after the receive.  This is how several ranks
+    that share ONE GPU (the single-GPU box's rehearsal of the multi-GPU path) run the real
+    protocol with the real kernels; RCCL ranks use DistTransport directly."""
+
+    def exchange(self, sends, recvs):
+        hs = {q: t.cpu() for q, t in sends.items()}          # synchronises the packing kernels
+        hr = {q: torch.empty(t.shape, dtype=t.dtype) for q, t in recvs.items()}
+        works = super().exchange(hs, hr)
+        return [_StagedWork(works, hr, recvs)] if recvs else works
+
+    def all_reduce_(self, t, op="sum"):
+        h = t.cpu()
+        super().all_reduce_(h, op)
+        t.copy_(h)
+        return t
+
+
+def dist_transport(backend=None, group=None):
+    """The transport for the current process group: RCCL moves device buffers itself, gloo
+    needs them staged through the host."""
+    import torch.distributed as dist
+    backend = backend or dist.get_backend(group)
+    return StagedTransport(group) if backend == "gloo" else DistTransport(group)
+
+
 class LocalTransport:
     """In-process virtual ranks (threads) sharing one device: tests and single-GPU rehearsal of
     the halo protocol.  ``endpoint(r)`` gives rank r a transport with the DistTransport API."""

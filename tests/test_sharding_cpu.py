@@ -71,7 +71,9 @@ def _worker(rank, world, port, P, chunk, out_dir):
     rng = np.random.default_rng(0)
     X = rng.standard_normal((64, P), dtype=np.float32)
     G = rng.standard_normal((64, P), dtype=np.float32)
-    sh = sharding.HaloShard(plan, P, "cpu", sharding.DistTransport(), chunk_cols=chunk,
+    # chunked case through the host-staged transport that gloo ranks sharing a GPU use
+    tr = sharding.dist_transport() if chunk else sharding.DistTransport()
+    sh = sharding.HaloShard(plan, P, "cpu", tr, chunk_cols=chunk,
                             n_agents_total=64, ops=OracleOps())
     sh.X = torch.from_numpy(X[plan.local].copy())
     Gl = torch.from_numpy(G[plan.local].copy())

@@ -57,3 +57,58 @@ def test_virtual_ranks_equal_single_device(cuda, world, chunk):
     for sh, _, ids in shards:
         assert float(sh.dev[1].item()) == pytest.approx(float(dmax.item()), rel=1e-5)
         np.testing.assert_allclose(sh.dev[0].cpu().numpy(), dsq[ids].cpu().numpy(), rtol=1e-5)
+
+
+def _gloo_worker(rank, world, port, chunk, out_dir):
+    """One rank of a real multi-process run on the shared GPU: torch.distributed gloo with the
+    host-staged transport, the HIP halo path, checked against the single-device round."""
+    import os
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from distributed_learning_amd import engine as E
+    dev = torch.device("cuda", 0)
+    R, C, P = 16, 16, 2048
+    edges = torus_edges(R, C)
+    verts = list(range(R * C))
+    csr = from_edge_weights(edges, [best_constant_weight(edges, verts)] * len(edges), verts)
+    g = torch.Generator(device=dev).manual_seed(9)
+    X = torch.randn(R * C, P, device=dev, generator=g)
+    G = torch.randn(R * C, P, device=dev, generator=g)
+    plan = sharding.halo_plans(csr, sharding.torus_block_partition(R, C, world))[rank]
+    tr = sharding.dist_transport()
+    assert isinstance(tr, sharding.StagedTransport)
+    sh = sharding.HaloShard(plan, P, dev, tr, chunk_cols=chunk, n_agents_total=R * C)
+    ids = torch.as_tensor(plan.local, device=dev)
+    sh.X = X[ids].contiguous()
+    Gl = G[ids].contiguous()
+    for _ in range(3):
+        sh.round(G=Gl, lr=0.01)
+    dsq, dmax = sh.deviation()
+    ref = E.GossipEngine(csr, P, device=dev, X=X, layout="rows")
+    for _ in range(3):
+        ref.round(G=G, lr=0.01)
+    rsq, rmax = ref.deviation()
+    torch.cuda.synchronize()
+    ok = torch.equal(sh.X.view(torch.int32), ref.rows()[ids].view(torch.int32))
+    ok = ok and abs(float(dmax.item()) - float(rmax.item())) <= 1e-5 * float(rmax.item())
+    ok = ok and bool(torch.allclose(dsq, rsq[ids], rtol=1e-5, atol=0))
+    with open(os.path.join(out_dir, f"ok{rank}"), "w") as f:
+        f.write(f"{int(ok)} halo={plan.n_halo} peers={sorted(plan.halo_from)}")
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,chunk", [(2, None), (4, 700)])
+def test_processes_over_gloo_equal_single_device(cuda, tmp_path, world, chunk):
+    """world processes share the GPU and exchange halos through torch.distributed (gloo, staged
+    through the host): the multi-process protocol of bench --workload c4 with the HIP kernels."""
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.spawn(_gloo_worker, args=(world, port, chunk, str(tmp_path)), nprocs=world, join=True)
+    for r in range(world):
+        txt = (tmp_path / f"ok{r}").read_text()
+        assert txt.startswith("1 "), (r, txt)

@@ -44,6 +44,7 @@ import torch
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+XGMI_LINK_GBS = 153.0  # one xGMI link, one direction (MI355X: 7 links per GPU)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 FP32_MFMA_PEAK_TFLOPS = 157.3  # dense f32-input MFMA (MI355X_MICROARCH.md, peak FP32 matrix)
 LDS_PEAK_GBS = 150000.0  # aggregate ds_read_b64/b128 with every CU streaming (MI355X_MICROARCH.md)
@@ -76,6 +77,9 @@ def parse():
     p.add_argument("--batch", type=int, default=64, help="c5: images per agent per step")
     p.add_argument("--cudnn-benchmark", action="store_true",
                    help="c5: torch.backends.cudnn.benchmark (MIOpen exhaustive find)")
+    p.add_argument("--no-halo-probe", action="store_true",
+                   help="N>1: skip the c4 agent-partition (RCCL halo exchange) probe that the "
+                        "c2 line carries as its 'c4_halo' object")
     p.add_argument("--dist-backend", default="nccl",
                    help="nccl (= RCCL, default) or gloo (multi-rank rehearsal on one GPU)")
     return p.parse_args()
@@ -143,7 +147,7 @@ def kernel_name(plan, sgd, dev, n_src):
     return f"mix_tile_kernel<{c}, {kv}, {b(sgd)}, {b(dev)}, true, false, true>"
 
 
-def traffic_from_profile(kname, path=os.path.join(ROOT, "profiles", "r03", "summary.json")):
+def traffic_from_profile(kname, path=os.path.join(ROOT, "profiles", "r04", "summary.json")):
     """HBM bytes per launch of this kernel from the committed rocprofv3 PMC summary
     (FETCH_SIZE x 2 + WRITE_SIZE, gfx950 correction), or None if it was not profiled."""
     try:
@@ -436,6 +440,18 @@ def run_c4(args, dev, rank, world):
     if rank != 0:
         return
     achieved = bytes_per_round / (launch_ms / 1e3) / 1e9
+    xgmi = None
+    if world > 1:
+        # halo bytes rank 0 receives per round (it sends as many); every peer is one xGMI link
+        # of the fully connected 8-GPU node
+        n_peers = len(plan["peers"])
+        hb = halo_rows * P * 4
+        xgmi = {"halo_bytes_per_round": hb, "peers": n_peers,
+                "achieved_GBs": hb / (launch_ms / 1e3) / 1e9,
+                "peak_GBs": XGMI_LINK_GBS * n_peers,
+                "frac": hb / (launch_ms / 1e3) / 1e9 / (XGMI_LINK_GBS * n_peers),
+                "note": "received halo bytes over the rank's round time (HIP events); one "
+                        "link per peer"}
     rec = {
         "metric": "c4 torus consensus rounds/sec (4096 agents x 2^18 fp32 params)",
         "value": args.steps / elapsed,
@@ -460,6 +476,7 @@ def run_c4(args, dev, rank, world):
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "kernel": "per-round HIP-event time (rank 0 local work)",
                      "bytes_per_launch": bytes_per_round, "launch_ms": launch_ms},
+        "xgmi": xgmi,
         "cpu_baseline": None,
     }
     print(json.dumps(rec), flush=True)
@@ -791,6 +808,47 @@ def run_gossip(args, dev, rank, world):
     print(json.dumps(rec), flush=True)
 
 
+def halo_probe(world, backend, steps=20, warmup=3, timeout_s=240):
+    """The agent-partitioned path at this GPU count: bench --workload c4 (64 x 64 torus, 2-D
+    blocks, boundary rows exchanged with RCCL send/recv over xGMI each round, overlapped with
+    the mix of the previous column chunk) as a CHILD job on the same GPUs, after this job's own
+    process group is gone.  It runs as a child under a time limit, so whatever it does, the c2
+    line is still printed.  Returns the child's figures (or its failure)."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    env = {k: v for k, v in os.environ.items()
+           if not k.startswith("TORCHELASTIC_") and k not in (
+               "RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK",
+               "GROUP_WORLD_SIZE", "ROLE_RANK", "ROLE_WORLD_SIZE", "ROLE_NAME", "MASTER_ADDR",
+               "MASTER_PORT")}
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={world}", "--master-addr", "127.0.0.1", f"--master-port={port}",
+           os.path.join(ROOT, "bench.py"), "--workload", "c4", "--gpus", str(world),
+           "--steps", str(steps), "--warmup", str(warmup), "--dist-backend", backend]
+    t0 = time.perf_counter()
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, env=env,
+                         start_new_session=True, text=True)
+    try:
+        out, _ = p.communicate(timeout=timeout_s)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        p.wait()
+        return {"status": f"timeout after {timeout_s} s"}
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    if p.returncode != 0 or not lines:
+        return {"status": f"exit {p.returncode}"}
+    r = json.loads(lines[-1])
+    return {"status": "ok", "metric": r["metric"], "value": r["value"], "unit": r["unit"],
+            "scaling": r["scaling"], "ms_per_step": r["ms_per_step"], "steps": r["steps"],
+            "parallelism": r["config"]["parallelism"], "plan": r["config"]["plan"],
+            "hbm": {k: r["roofline"][k] for k in ("achieved", "peak", "frac", "launch_ms")},
+            "xgmi": r["xgmi"], "wall_s": time.perf_counter() - t0}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -920,9 +978,15 @@ def main():
             "cpu_baseline": cpu,
             "final_max_deviation": dev_max,
         }
-        print(json.dumps(rec), flush=True)
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
+    if rank == 0:
+        if world > 1 and not args.no_halo_probe and sgd:
+            del eng, G
+            torch.cuda.empty_cache()
+            rec["c4_halo"] = halo_probe(world, args.dist_backend)
+        print(json.dumps(rec), flush=True)
 
 
 if __name__ == "__main__":

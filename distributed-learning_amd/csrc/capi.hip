@@ -75,6 +75,22 @@ int wg_per_cu_cap() {
     return (v && v[0] == '1') ? 1 : 2;
 }
 
+// Persistent grid for n_tiles tiles and at most gmax workgroups: the fewest workgroups that
+// still finish in the same number of passes, so every workgroup walks ceil(n_tiles/gmax) or one
+// fewer tiles.  The time of a persistent HBM-bound launch is its longest workgroup's tile
+// count; with gmax workgroups and a ragged last pass (c3: 1286 tiles on 256 CUs = 6 passes for
+// an average of 5.02) the idle CUs of that pass are pure tail.  Fewer, evenly loaded workgroups
+// keep the same number of passes while each one gets a larger share of HBM.
+// DLAMD_BALANCE_GRID=0 (a measurement knob) keeps gmax.
+int64_t balanced_grid(int64_t n_tiles, int64_t gmax) {
+    if (gmax <= 0) return 1;
+    if (n_tiles <= gmax) return n_tiles;
+    const char *v = getenv("DLAMD_BALANCE_GRID");
+    if (v && v[0] == '0') return gmax;
+    const int64_t passes = (n_tiles + gmax - 1) / gmax;
+    return (n_tiles + passes - 1) / passes;
+}
+
 int next_pow2_chunks(int64_t n_params) {
     int64_t need = (n_params + 3) / 4;
     int c = 1;
@@ -108,7 +124,12 @@ int plan_mix(const dl_mix_args *a, Plan *pl) {
     const int reg = a->W.uniform_row_nnz > 0 ? 1 : 0;
     const int32_t n_w = (reg && a->W.shared_row_weights) ? a->W.uniform_row_nnz : nnz;
     const uint32_t csr = dl::csr_lds_bytes(a->W.n_rows, nnz, reg, n_w);
-    const int cmax = next_pow2_chunks(a->n_params);
+    int cmax = next_pow2_chunks(a->n_params);
+    // DLAMD_MAX_TILE_CHUNKS=c (a measurement knob) caps the row-major tile at 4c columns
+    if (const char *mc = getenv("DLAMD_MAX_TILE_CHUNKS")) {
+        const int m = atoi(mc);
+        while (m >= 1 && cmax > m) cmax >>= 1;
+    }
     // DLAMD_FORCE_GATHER=1 (tests only) forces the general gather kernel
     const char *force = getenv("DLAMD_FORCE_GATHER");
     const bool force_gather = force && force[0] == '1';
@@ -129,8 +150,7 @@ int plan_mix(const dl_mix_args *a, Plan *pl) {
         int bpc = (int)(dl::kLdsBytes / lds);
         if (bpc > wg_per_cu_cap()) bpc = wg_per_cu_cap();
         if (c == 4) bpc = 1;
-        int64_t grid = (int64_t)device_cus() * (bpc < 1 ? 1 : bpc);
-        if (grid > n_tiles) grid = n_tiles;
+        const int64_t grid = balanced_grid(n_tiles, (int64_t)device_cus() * (bpc < 1 ? 1 : bpc));
         pl->pub.path = 1;
         pl->pub.tile_cols = a->tile_cols;
         pl->pub.grid = (int32_t)grid;
@@ -154,8 +174,7 @@ int plan_mix(const dl_mix_args *a, Plan *pl) {
             if (n_tiles > 0x7fffffff) continue;
             int bpc = (int)(dl::kLdsBytes / lds);
             if (bpc > wg_per_cu_cap()) bpc = wg_per_cu_cap();  // 1024 threads: <= 2 per CU
-            int64_t grid = (int64_t)device_cus() * bpc;
-            if (grid > n_tiles) grid = n_tiles;
+            const int64_t grid = balanced_grid(n_tiles, (int64_t)device_cus() * bpc);
             pl->pub.path = 1;
             pl->pub.tile_cols = (int32_t)T;
             pl->pub.grid = (int32_t)grid;
@@ -364,7 +383,7 @@ int plan_rounds(const dl_mix_args *a, Plan *pl) {
     pl->scratch_off = (uint32_t)(2 * tile + csr);
     pl->pub.path = 3;
     pl->pub.tile_cols = (int32_t)T;
-    pl->pub.grid = (int32_t)(n_tiles < device_cus() ? n_tiles : device_cus());
+    pl->pub.grid = (int32_t)balanced_grid(n_tiles, device_cus());
     pl->pub.lds_bytes = (int32_t)(2 * tile + csr +
                                   (want_dev ? (dl::kTileThreads / 64) * c * 16 : 0));
     pl->pub.n_tiles = (int32_t)n_tiles;

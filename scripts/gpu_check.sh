@@ -19,7 +19,7 @@ step() {  # name, timeout, cmd...
 MODE=${1:-all}
 if [ "$MODE" = all ] || [ "$MODE" = test ]; then
     step smoke 400 python -c "import __graft_entry__ as g; g.smoke()"
-    step pytest_gpu 1200 python -m pytest tests -x -q -m gpu
+    step pytest_gpu 1200 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread
 fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
     step bench 600 python bench.py --steps 50 --warmup 5

@@ -110,8 +110,8 @@ def build_graph(n, kind="rr4"):
 
 def copy_ceiling(dev, nbytes=4 << 30, reps=10):
     """Measured HBM ceilings (libdlamd dl_stream_copy) over 4 GiB streams: float4 copies
-    (variants 0-3, read + write bytes) and the triad y = x - lr g (variants 4-5: two reads, one
-    write -- the fused round's own traffic, 12 B per element).  Returns (best copy GB/s, best
+    (variants 0-3, read + write bytes) and the triad y = x - lr g (variants 4-6: two reads, one
+    write -- the fused round's own traffic, 12 B per element; 6 in the round's access shape).  Returns (best copy GB/s, best
     triad GB/s, per-variant GB/s)."""
     from distributed_learning_amd import _lib
     lib = _lib.load()
@@ -120,7 +120,7 @@ def copy_ceiling(dev, nbytes=4 << 30, reps=10):
     n = b.numel()
 
     best = {}
-    for variant in (0, 1, 2, 3, 4, 5):
+    for variant in (0, 1, 2, 3, 4, 5, 6):
         def cp():
             _lib.check(lib.dl_stream_copy(_lib.ptr(a), _lib.ptr(b), n, variant,
                                           _lib.stream_handle(dev)), "dl_stream_copy")
@@ -135,7 +135,7 @@ def copy_ceiling(dev, nbytes=4 << 30, reps=10):
         moved = (3 if variant >= 4 else 2) * nbytes
         best[variant] = moved / (s.elapsed_time(e) / 1e3 / reps) / 1e9
     del a, b
-    return (max(best[v] for v in (0, 1, 2, 3)), max(best[v] for v in (4, 5)), best)
+    return (max(best[v] for v in (0, 1, 2, 3)), max(best[v] for v in (4, 5, 6)), best)
 
 
 def kernel_name(plan, sgd, dev, n_src):
@@ -147,7 +147,7 @@ def kernel_name(plan, sgd, dev, n_src):
     return f"mix_tile_kernel<{c}, {kv}, {b(sgd)}, {b(dev)}, true, false, true>"
 
 
-def traffic_from_profile(kname, path=os.path.join(ROOT, "profiles", "r04", "summary.json")):
+def traffic_from_profile(kname, path=os.path.join(ROOT, "profiles", "r05", "summary.json")):
     """HBM bytes per launch of this kernel from the committed rocprofv3 PMC summary
     (FETCH_SIZE x 2 + WRITE_SIZE, gfx950 correction), or None if it was not profiled."""
     try:

@@ -50,9 +50,22 @@ constexpr size_t kAlign = 256;
 size_t align_up(size_t v) { return (v + kAlign - 1) & ~(kAlign - 1); }
 bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
+// Workgroups of the one-round tile kernel per resident slot on the column-tiled layout: its
+// persistent grid is oversubscribed 2x, the second half of the workgroups starting as the first ones retire.
+// Measured on MI355X (scripts/grid_sweep.py, profiles/r05/grid_sweep.log): the c2 and c4 rounds
+// stream at 5.90-5.93 TB/s with 2x against 5.28-5.41 TB/s with exactly one workgroup per CU, on
+// the same box (3x: 5.74-5.80, 4x: 5.75-5.84).  Forcing one resident workgroup per CU through
+// LDS changes nothing, so the gain is not co-residency.  Row-major operands (c3's N = 256 rows)
+// keep one slot's grid (3247 vs 3206 steps/s).  DLAMD_GRID_MULT=k (1..8) overrides it.
+int grid_mult() {
+    const char *m = getenv("DLAMD_GRID_MULT");
+    const int k = m ? atoi(m) : 2;
+    return k < 1 ? 1 : (k > 8 ? 8 : k);
+}
+
 // Upper bound of per-workgroup partial rows any path writes.
 int max_parts() {
-    int p = 2 * device_cus();
+    int p = 2 * device_cus() * grid_mult();
     return p < 256 ? 256 : p;
 }
 
@@ -150,7 +163,8 @@ int plan_mix(const dl_mix_args *a, Plan *pl) {
         int bpc = (int)(dl::kLdsBytes / lds);
         if (bpc > wg_per_cu_cap()) bpc = wg_per_cu_cap();
         if (c == 4) bpc = 1;
-        const int64_t grid = balanced_grid(n_tiles, (int64_t)device_cus() * (bpc < 1 ? 1 : bpc));
+        const int64_t grid =
+            balanced_grid(n_tiles, (int64_t)device_cus() * (bpc < 1 ? 1 : bpc) * grid_mult());
         pl->pub.path = 1;
         pl->pub.tile_cols = a->tile_cols;
         pl->pub.grid = (int32_t)grid;
@@ -174,7 +188,8 @@ int plan_mix(const dl_mix_args *a, Plan *pl) {
             if (n_tiles > 0x7fffffff) continue;
             int bpc = (int)(dl::kLdsBytes / lds);
             if (bpc > wg_per_cu_cap()) bpc = wg_per_cu_cap();  // 1024 threads: <= 2 per CU
-            const int64_t grid = balanced_grid(n_tiles, (int64_t)device_cus() * bpc);
+            const int64_t grid =
+                balanced_grid(n_tiles, (int64_t)device_cus() * bpc);
             pl->pub.path = 1;
             pl->pub.tile_cols = (int32_t)T;
             pl->pub.grid = (int32_t)grid;
@@ -651,12 +666,17 @@ int dl_mix_round(const dl_mix_args *args, void *workspace, size_t ws_bytes, dl_s
         t.scratch_off = pl.scratch_off;
         float *partial = pl.dev ? reinterpret_cast<float *>(ws) : nullptr;
         if (pl.dev) t.dev_max_zero = reinterpret_cast<unsigned int *>(args->dev_max);
+        int lds = pl.pub.lds_bytes;
+        if (const char *v = getenv("DLAMD_LDS_MIN")) {  // measurement knob: LDS per workgroup
+            const int m = atoi(v);                        // bounds workgroups per CU
+            if (m > lds) lds = m < (int)dl::kLdsBytes ? m : (int)dl::kLdsBytes;
+        }
         if (grid_full > 0) {
             t.n_tiles = (int32_t)n_full;
             t.col_base = 0;
             t.dev_partial = partial;
             hipError_t e = dl::launch_mix_tile(t, pl.chunks, sgd, pl.dev, true, grid_full,
-                                               pl.pub.lds_bytes, true, s);
+                                               lds, true, s);
             if (e != hipSuccess) return hip_fail(e, "mix_tile_kernel launch");
         }
         if (grid_tail > 0) {
@@ -664,7 +684,7 @@ int dl_mix_round(const dl_mix_args *args, void *workspace, size_t ws_bytes, dl_s
             t.col_base = n_full * T;
             t.dev_partial = pl.dev ? partial + (size_t)grid_full * Nr : nullptr;
             hipError_t e = dl::launch_mix_tile(t, pl.chunks, sgd, pl.dev, true, grid_tail,
-                                               pl.pub.lds_bytes, false, s);
+                                               lds, false, s);
             if (e != hipSuccess) return hip_fail(e, "mix_tile_kernel (tail) launch");
         }
         if (pl.dev) {
@@ -934,9 +954,9 @@ int dl_stream_copy(const float *src, float *dst, int64_t n_floats, int32_t varia
                    dl_stream_t stream) {
     g_err.clear();
     if (!src || !dst || n_floats < 0 || (n_floats & 3) || !aligned16(src) || !aligned16(dst) ||
-        variant < 0 || variant > 5)
+        variant < 0 || variant > 6 || (variant == 6 && n_floats % 16384))
         return fail(DL_ERR_INVALID, "dl_stream_copy: needs 16-byte aligned buffers, n %% 4 == 0, "
-                                    "variant 0..5");
+                                    "variant 0..6 (6: n %% 16384 == 0)");
     hipError_t e = dl::launch_stream_copy(src, dst, n_floats, variant,
                                           static_cast<hipStream_t>(stream));
     return e == hipSuccess ? DL_OK : hip_fail(e, "stream_copy launch");

@@ -312,7 +312,10 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
                 mean_t.z = mean_t.z / n;
                 mean_t.w = mean_t.w / n;
             }
-            if (nxt < a.n_tiles) prefetch(nxt);  // lands while we mix from LDS
+            // lands while we mix from LDS.  Issued after the staging barrier: issuing it before
+            // (right after the staging writes) measured 10 % slower (scripts/grid_sweep.py,
+            // profiles/r05/grid_sweep_early_prefetch.log)
+            if (nxt < a.n_tiles) prefetch(nxt);
             float *yt = const_cast<float *>(
                 reinterpret_cast<const float *>(tile_base(a.y, a.yts, tile_id)));
             float4 cs = zero4();
@@ -484,6 +487,38 @@ __global__ void stream_triad_kernel(const float4 *__restrict__ x, const float4 *
     }
 }
 
+// The same triad in the round's own access shape: persistent 1024-thread workgroups on a 2x
+// oversubscribed grid, each streaming whole 64-KiB blocks per operand (4 float4 per thread per
+// stream), the next block's loads issued before the current block's stores.  Ragged tails are
+// not handled: n4 must be a multiple of 4096 (checked by the launcher).
+__global__ void __launch_bounds__(1024) stream_triad_tile_kernel(const float4 *__restrict__ x,
+                                                                 const float4 *__restrict__ g,
+                                                                 float4 *__restrict__ y,
+                                                                 int64_t n_blocks) {
+    constexpr int R = 4;
+    int64_t t = blockIdx.x;
+    if (t >= n_blocks) return;
+    float4 a[R], b[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        a[r] = nt_load4(x + t * 4096 + r * 1024 + threadIdx.x);
+        b[r] = nt_load4(g + t * 4096 + r * 1024 + threadIdx.x);
+    }
+    for (; t < n_blocks; t += gridDim.x) {
+        float4 o[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) o[r] = local_step(a[r], b[r], 1e-3f);
+        const int64_t tn = t + gridDim.x < n_blocks ? t + gridDim.x : t;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            a[r] = nt_load4(x + tn * 4096 + r * 1024 + threadIdx.x);
+            b[r] = nt_load4(g + tn * 4096 + r * 1024 + threadIdx.x);
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) nt_store4(o[r], y + t * 4096 + r * 1024 + threadIdx.x);
+    }
+}
+
 template <int C, int KV, bool SGD, bool DEV, bool MIX, bool HALO, bool FAST>
 hipError_t launch_one(const TileArgs &a, int grid, int lds, hipStream_t s) {
     auto k = mix_tile_kernel<C, KV, SGD, DEV, MIX, HALO, FAST>;
@@ -595,7 +630,20 @@ hipError_t launch_stream_copy(const float *src, float *dst, int64_t n_floats, in
     if (variant >= 4) {
         auto x = reinterpret_cast<const float4 *>(src);
         auto y = reinterpret_cast<float4 *>(dst);
-        if (variant == 4)
+        if (variant == 6) {
+            if (n4 % 4096) return hipErrorInvalidValue;
+            const int64_t nb = n4 / 4096;
+            int dev = 0, cus = 0;
+            if (hipGetDevice(&dev) != hipSuccess ||
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+                cus <= 0)
+                cus = 256;
+            int64_t grid = 2 * (int64_t)cus;
+            if (grid > nb) grid = nb;
+            if (grid < 1) return hipSuccess;
+            hipLaunchKernelGGL(stream_triad_tile_kernel, dim3((unsigned)grid), dim3(1024), 0, s, x,
+                               x + n4, y, nb);
+        } else if (variant == 4)
             hipLaunchKernelGGL(stream_triad_kernel<1>, dim3(256), dim3(512), 0, s, x, x + n4, y, n4);
         else
             hipLaunchKernelGGL(stream_triad_kernel<4>, dim3(1024), dim3(256), 0, s, x, x + n4, y, n4);

@@ -7,6 +7,7 @@ fresh fp32 array per agent and term.  Flattening models to X happens once per ``
 (mixer.py:26), not per round.
 """
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -327,6 +328,28 @@ def perron_round(Y, rowptr, col, eps, conv_eps, weight=None, mean_weight=1.0, ma
     return int(iters.item())
 
 
+# Resident operands of the one-round kernel are streamed together, tile t of X, G and Y at the
+# same moment.  When their buffers start an exact multiple of a large power of two apart (4 GiB
+# allocations placed back to back), the three streams alias in HBM and the round loses up to
+# 15 % (scripts/skew_probe.py, profiles/r05/skew_probe.log: 5.08-5.18 TB/s with X | G | Y packed
+# at 4 GiB spacing vs 5.68-5.98 TB/s staggered).  Each large resident buffer therefore gets a
+# padded allocation of its own and starts `slot` x (2 MiB + 64 KiB) into it.
+STAGGER_BYTES = (2 << 20) + (64 << 10)
+_STAGGER_MIN_BYTES = 64 << 20
+
+
+def staggered_zeros(shape, slot, device):
+    """torch.zeros(shape) fp32 on ``device``, placed at a stagger of ``slot`` (0..3) inside a
+    padded allocation when it is large; DLAMD_STAGGER=0 turns the stagger off (measurements)."""
+    numel = int(np.prod(shape))
+    if numel * 4 < _STAGGER_MIN_BYTES or os.environ.get("DLAMD_STAGGER", "1") == "0":
+        return torch.zeros(shape, dtype=torch.float32, device=device)
+    step = STAGGER_BYTES // 4
+    off = (int(slot) % 4) * step
+    buf = torch.zeros(numel + 4 * step, dtype=torch.float32, device=device)
+    return buf[off:off + numel].view(shape)
+
+
 class GossipEngine:
     """N agents x P params resident in HBM, mixed by a fixed sparse W.
 
@@ -370,14 +393,15 @@ class GossipEngine:
         self.dev_sq = torch.zeros(self.n, dtype=torch.float32, device=self.device)
         self.dev_max = torch.zeros(1, dtype=torch.float32, device=self.device)
         self.ws = Workspace(self.device)
+        self._slot = 0      # stagger slot of the next resident buffer (X, Y, G, ...)
         self.X = self.layout_like(X) if X is not None else self._empty()
         self.Y = self._empty()
 
     def _empty(self):
-        if self.layout == "tiled":
-            return torch.zeros(tiled_shape(self.n, self.P, self.T), dtype=torch.float32,
-                               device=self.device)
-        return torch.zeros(self.n, self.P, dtype=torch.float32, device=self.device)
+        shape = (tiled_shape(self.n, self.P, self.T) if self.layout == "tiled"
+                 else (self.n, self.P))
+        self._slot += 1
+        return staggered_zeros(shape, self._slot - 1, self.device)
 
     def layout_like(self, A):
         """A row-major [N, P] tensor in this engine's resident layout (G, X, ...)."""
@@ -388,7 +412,10 @@ class GossipEngine:
             A = A.index_select(0, self.order)          # agent order -> slot order (a copy)
         # always a buffer of its own: the engine ping-pongs X/Y and must never write into the
         # caller's tensor
-        return to_tiled(A, self.T) if self.layout == "tiled" else A.contiguous().clone()
+        out = self._empty()
+        if self.layout == "tiled":
+            return to_tiled(A, self.T, out=out)
+        return out.copy_(A)
 
     def load_rows(self, X):
         self.X = self.layout_like(X)

@@ -266,7 +266,9 @@ int dl_sgd_step(const dl_sgd_args *args, dl_stream_t stream);
  * stores on a 8192-workgroup grid).  Variants 4 and 5 are the triad
  * dst[i] = src[i] - 1e-3 * src[n_floats + i] (src holds 2 * n_floats floats): two read streams
  * and one write stream, the traffic of the fused local step + mix round (12 B per element);
- * 4: one float4 per stream in flight, 512-thread workgroups x 256; 5: four, 256 x 1024; all
+ * 4: one float4 per stream in flight, 512-thread workgroups x 256; 5: four, 256 x 1024; 6: the
+ * round's own shape (persistent 1024-thread workgroups on 2 x CUs, 64-KiB blocks per stream,
+ * next block loaded before the current one is stored; n_floats % 16384 == 0); all
  * non-temporal.  Not on the reference path: the bench uses them to measure the HBM streaming
  * ceilings next to the mix kernel's achieved bandwidth. */
 int dl_stream_copy(const float *src, float *dst, int64_t n_floats, int32_t variant,

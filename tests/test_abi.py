@@ -114,8 +114,16 @@ def test_tiled_width_choice(n, T):
     _lib.check(lib.dl_mix_plan_shape(n, 0, 1 << 20, nnz, 5, 1, 1, -1, ctypes.byref(pl)), "plan")
     assert pl.path == 1 and pl.tile_cols == T
     assert pl.tile_cols * n * 4 <= 65536 or pl.tile_cols == 4
-    # at C = 4 one workgroup per CU, else two when LDS allows
+    # at C = 4 one resident workgroup per CU, else two when LDS allows; the persistent grid is
+    # oversubscribed 2x by default (DLAMD_GRID_MULT)
     if T == 16:
+        assert pl.grid <= 2 * 256
+        os.environ["DLAMD_GRID_MULT"] = "1"
+        try:
+            _lib.check(lib.dl_mix_plan_shape(n, 0, 1 << 20, nnz, 5, 1, 1, -1, ctypes.byref(pl)),
+                       "plan")
+        finally:
+            os.environ.pop("DLAMD_GRID_MULT")
         assert pl.grid <= 256
 
 

@@ -337,13 +337,22 @@ def run_c3(args, dev, rank, world):
     gbs = mix_bytes / (mix_ms / 1e3) / 1e9
     if rank != 0:
         return
+    # HBM bytes per launch from the committed PMC passes of this workload (profiles/r05/c3)
+    c3_path = os.path.join(ROOT, "profiles", "r05", "c3", "summary.json")
+    c3_grad_traffic, c3_src = (traffic_from_profile("mlp_fused_kernel", c3_path)
+                               if ann.path == "fused" and args.c3_layout == "rows"
+                               else (None, None))
+    c3_mix_traffic, _ = (traffic_from_profile("mix_tile_kernel<", c3_path)
+                         if args.c3_layout == "rows" else (None, None))
     grad_roof = {"bound": "mfma", "achieved": tflops, "peak": FP32_MFMA_PEAK_TFLOPS,
-                 "unit": "TFLOP/s", "frac": tflops / FP32_MFMA_PEAK_TFLOPS, "traffic": None,
+                 "unit": "TFLOP/s", "frac": tflops / FP32_MFMA_PEAK_TFLOPS,
+                 "traffic": c3_grad_traffic, "traffic_source": c3_src if c3_grad_traffic else None,
                  "kernel": ("mlp_fused_kernel" if ann.path == "fused" else
                             "dl_bgemm x11 + dl_xent_grad") + " (per-step HIP-event time)",
                  "flops_per_launch": flops, "launch_ms": grad_ms}
     mix_roof = {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": gbs / HBM_PEAK_GBS, "traffic": None,
+                "frac": gbs / HBM_PEAK_GBS, "traffic": c3_mix_traffic,
+                "traffic_source": c3_src if c3_mix_traffic else None,
                 "kernel": "mix_tile_kernel (+dev_reduce)", "bytes_per_launch": mix_bytes,
                 "launch_ms": mix_ms}
     dominant = grad_roof if grad_ms >= mix_ms else mix_roof
@@ -440,6 +449,10 @@ def run_c4(args, dev, rank, world):
     if rank != 0:
         return
     achieved = bytes_per_round / (launch_ms / 1e3) / 1e9
+    # single GPU: HBM bytes per launch from the committed PMC passes (profiles/r05/c4)
+    c4_traffic, c4_src = (traffic_from_profile(
+        "mix_tile_kernel<", os.path.join(ROOT, "profiles", "r05", "c4", "summary.json"))
+        if world == 1 else (None, None))
     xgmi = None
     if world > 1:
         # halo bytes rank 0 receives per round (it sends as many); every peer is one xGMI link
@@ -473,7 +486,8 @@ def run_c4(args, dev, rank, world):
                    "halo_rows_rank0": halo_rows,
                    "halo_bytes_per_round_rank0": halo_rows * P * 4},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": c4_traffic,
+                     "traffic_source": c4_src,
                      "kernel": "per-round HIP-event time (rank 0 local work)",
                      "bytes_per_launch": bytes_per_round, "launch_ms": launch_ms},
         "xgmi": xgmi,

@@ -4,9 +4,10 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 TAG=${1:-r01}
+shift
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
-ARGS="--steps 20 --warmup 3 --no-cpu"
+ARGS=${@:-"--steps 20 --warmup 3 --no-cpu"}
 run() {
     local name=$1; shift
     echo "=== $name"

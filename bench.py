@@ -69,6 +69,8 @@ def parse():
     p.add_argument("--cpu-cols", type=int, default=1 << 18,
                    help="columns of the bounded CPU-baseline sample (all agents)")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--trace", action="store_true",
+                   help="c2-gossip: traced passes (Mixer.mix(times, eps) stop test every round)")
     p.add_argument("--no-graph", action="store_true", help="c3/c5: eager launches, no hipGraph")
     p.add_argument("--streams", type=int, default=8, help="c5: HIP streams the agents share")
     p.add_argument("--c3-layout", default="rows", choices=["rows", "tiled"],
@@ -749,18 +751,37 @@ def run_gossip(args, dev, rank, world):
         log(f"c2-gossip: LDS slot order, bank conflicts {c0} -> {c1}")
     eng = engine.GossipEngine(csr, P, device=dev, X=torch.randn(n, P, device=dev, generator=g),
                               order=order)
-    plan = engine.rounds_plan(eng.W, eng.X, eng.Y, deviation=True, tiled=(eng.P, eng.T))
-    if plan is None:
-        raise SystemExit("c2-gossip: the multi-round kernel does not fit this graph")
     stream = torch.cuda.current_stream(dev)
     evs = event_pairs(args.steps, 2)
+    if args.trace:
+        # Mixer.mix(times, eps) as the drop-in runs it for X too large for one workgroup: one
+        # traced pass of K rounds + one readback of the K per-round max deviations per step
+        kmax = eng.trace_max_rounds()
+        if kmax < 1:
+            raise SystemExit("c2-gossip --trace: the traced kernel does not fit this graph")
+        K = min(K, kmax)
+        plan = {"kernel": "mix_trace_kernel", "max_rounds_per_pass": kmax}
+        trace = torch.empty(K, dtype=torch.float32, device=dev)
+        last = []
 
-    def step(i):
-        if i is not None:
-            evs[i][0].record(stream)
-        eng.rounds(K, deviation=True)
-        if i is not None:
-            evs[i][1].record(stream)
+        def step(i):
+            if i is not None:
+                evs[i][0].record(stream)
+            eng.rounds_traced(K, trace)
+            if i is not None:
+                evs[i][1].record(stream)
+            last[:] = trace.tolist()     # the host stop test reads the K values every pass
+    else:
+        plan = engine.rounds_plan(eng.W, eng.X, eng.Y, deviation=True, tiled=(eng.P, eng.T))
+        if plan is None:
+            raise SystemExit("c2-gossip: the multi-round kernel does not fit this graph")
+
+        def step(i):
+            if i is not None:
+                evs[i][0].record(stream)
+            eng.rounds(K, deviation=True)
+            if i is not None:
+                evs[i][1].record(stream)
 
     elapsed = timed_loop(step, args, world, dev)
     launch_ms = max_over_ranks(float(np.mean([a.elapsed_time(b) for a, b in evs])), world, dev)
@@ -800,8 +821,11 @@ def run_gossip(args, dev, rank, world):
         "dtype": "f32",
         "data": "synthetic (X ~ N(0,1) resident in HBM; networkx random_regular_graph(4, 1024, "
                 "seed=0))",
-        "config": {"workload": f"c2-gossip: Mixer.mix(times={K}) eps=None as one dl_mix_rounds "
-                               "pass + final deviation",
+        "config": {"workload": (f"c2-gossip --trace: Mixer.mix(times, eps) passes of {K} rounds "
+                                "(dl_mix_rounds_trace: one HBM pass + the per-round max "
+                                "deviations, read back every pass)" if args.trace else
+                                f"c2-gossip: Mixer.mix(times={K}) eps=None as one dl_mix_rounds "
+                                "pass + final deviation"),
                    "agents": n, "params_per_gpu": P, "rounds_per_step": K,
                    "graph": {"rr4": "random 4-regular", "circ4": "circulant a+-1, a+-2",
                              "torus": "2-D periodic torus"}[args.graph], "weights": f"best-constant {wconst:.6f}",
@@ -811,13 +835,14 @@ def run_gossip(args, dev, rank, world):
                      "peak": LDS_PEAK_GBS, "unit": "GB/s",
                      "frac": lds_bytes / (launch_ms / 1e3) / 1e9 / LDS_PEAK_GBS,
                      "traffic": None,
-                     "kernel": "mix_multi_kernel (+dev_reduce) per-step HIP-event time",
+                     "kernel": ("mix_trace_kernel (+trace_reduce)" if args.trace else
+                                "mix_multi_kernel (+dev_reduce)") + " per-step HIP-event time",
                      "bytes_per_launch": lds_bytes, "launch_ms": launch_ms,
                      "hbm_bytes_per_launch": hbm_bytes,
                      "hbm_GBs": hbm_bytes / (launch_ms / 1e3) / 1e9,
                      "round_equivalent_hbm_GBs": K * hbm_bytes / (launch_ms / 1e3) / 1e9},
         "cpu_baseline": cpu,
-        "final_max_deviation": float(eng.dev_max.item()),
+        "final_max_deviation": (float(last[-1]) if args.trace else float(eng.dev_max.item())),
     }
     print(json.dumps(rec), flush=True)
 

@@ -96,6 +96,9 @@ SIGNATURES = {
     "dl_mix_round": (_i32, [ctypes.POINTER(DlMixArgs), _vp, _sz, _vp]),
     "dl_mix_rounds_plan": (_i32, [ctypes.POINTER(DlMixArgs), ctypes.POINTER(DlMixPlan)]),
     "dl_mix_rounds": (_i32, [ctypes.POINTER(DlMixArgs), _i32, _vp, _sz, _vp]),
+    "dl_mix_trace_plan": (_i32, [ctypes.POINTER(DlMixArgs), ctypes.POINTER(_i32)]),
+    "dl_mix_trace_workspace_bytes": (_sz, [_i32, _i32]),
+    "dl_mix_rounds_trace": (_i32, [ctypes.POINTER(DlMixArgs), _i32, _vp, _vp, _sz, _vp]),
     "dl_mix_until_fits": (_i32, [_i32, _i64, _i32]),
     "dl_mix_until": (_i32, [ctypes.POINTER(DlMixUntilArgs), _vp]),
     "dl_consensus_gd": (_i32, [ctypes.POINTER(DlConsensusGdArgs), _i32, _vp]),

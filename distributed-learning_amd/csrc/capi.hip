@@ -406,11 +406,113 @@ int plan_rounds(const dl_mix_args *a, Plan *pl) {
     return DL_OK;
 }
 
+// dl_mix_rounds_trace configuration: one agent per thread, one float4 column chunk per step.
+struct TracePlan {
+    int32_t max_rounds;  // rounds whose [rounds][n_rows] trace fits LDS beside the images
+    int32_t grid;
+    uint32_t csr_off, scratch_off, trace_off, fixed_lds;
+};
+
+int plan_trace(const dl_mix_args *a, TracePlan *tp) {
+    const int32_t N = a->W.n_rows;
+    if (a->n_halo > 0)
+        return fail(DL_ERR_UNSUPPORTED, "dl_mix_rounds_trace: halo rows need one exchange per "
+                                        "round");
+    if (!a->W.doubly_stochastic)
+        return fail(DL_ERR_UNSUPPORTED, "dl_mix_rounds_trace: the per-round deviation needs a "
+                                        "doubly stochastic W (mean(W x) = mean(x))");
+    if (a->g)
+        return fail(DL_ERR_UNSUPPORTED, "dl_mix_rounds_trace: no local step (g must be NULL)");
+    if (N < 2 || N > dl::kTileThreads)
+        return fail(DL_ERR_UNSUPPORTED, "dl_mix_rounds_trace: needs 2..%d agents (one per "
+                                        "thread), got %d", dl::kTileThreads, N);
+    if (a->n_params % 4)
+        return fail(DL_ERR_UNSUPPORTED, "dl_mix_rounds_trace: n_params must be a multiple of 4");
+    const int reg = a->W.uniform_row_nnz > 0 ? 1 : 0;
+    const int32_t n_w = (reg && a->W.shared_row_weights) ? a->W.uniform_row_nnz : a->W.nnz;
+    const bool in_regs = a->W.uniform_row_nnz == 5 && n_w == 5;
+    const uint32_t csr = in_regs ? 0u : dl::csr_lds_bytes(N, a->W.nnz, reg, n_w);
+    if (!in_regs && csr == 0)
+        return fail(DL_ERR_UNSUPPORTED, "dl_mix_rounds_trace: CSR too large");
+    const uint32_t img = 2u * (uint32_t)N * 16u;
+    tp->csr_off = img;
+    tp->scratch_off = (uint32_t)align_up(img + csr);
+    tp->trace_off = tp->scratch_off + (dl::kTileThreads / 64) * 16u;
+    tp->fixed_lds = tp->trace_off;
+    const int64_t k = ((int64_t)dl::kLdsBytes - tp->fixed_lds) / (4 * (int64_t)N);
+    if (k < 1) return fail(DL_ERR_UNSUPPORTED, "dl_mix_rounds_trace: no LDS left for a trace");
+    tp->max_rounds = (int32_t)(k < 1024 ? k : 1024);
+    const int64_t nq = a->n_params / 4;
+    tp->grid = (int32_t)balanced_grid(nq, device_cus());
+    return DL_OK;
+}
+
 }  // namespace
 
 extern "C" {
 
 int dl_abi_version(void) { return DLAMD_ABI_VERSION; }
+
+int dl_mix_trace_plan(const dl_mix_args *args, int32_t *max_rounds) {
+    g_err.clear();
+    if (!max_rounds) return fail(DL_ERR_INVALID, "dl_mix_trace_plan: max_rounds is NULL");
+    int rc = check_mix_args(args);
+    if (rc) return rc;
+    TracePlan tp;
+    rc = plan_trace(args, &tp);
+    if (rc) return rc;
+    *max_rounds = tp.max_rounds;
+    return DL_OK;
+}
+
+size_t dl_mix_trace_workspace_bytes(int32_t n_rows, int32_t rounds) {
+    if (n_rows <= 0 || rounds <= 0) return 0;
+    return align_up((size_t)device_cus() * (size_t)rounds * (size_t)n_rows * 4) + kAlign;
+}
+
+int dl_mix_rounds_trace(const dl_mix_args *args, int32_t rounds, float *trace, void *workspace,
+                        size_t ws_bytes, dl_stream_t stream) {
+    g_err.clear();
+    int rc = check_mix_args(args);
+    if (rc) return rc;
+    if (!trace) return fail(DL_ERR_INVALID, "dl_mix_rounds_trace: trace is NULL");
+    TracePlan tp;
+    rc = plan_trace(args, &tp);
+    if (rc) return rc;
+    if (rounds < 1 || rounds > tp.max_rounds)
+        return fail(DL_ERR_INVALID, "dl_mix_rounds_trace: rounds must be in [1, %d] (the LDS "
+                                    "trace), got %d", tp.max_rounds, rounds);
+    dl::TileArgs t = tile_args(args);
+    if (!t.vec)
+        return fail(DL_ERR_UNSUPPORTED, "dl_mix_rounds_trace: operands must be 16-byte aligned "
+                                        "float4 rows");
+    const int32_t N = args->W.n_rows;
+    if (t.tiled) {
+        const int64_t T = args->tile_cols;
+        t.lchunks = (int32_t)(T / 4);
+        t.xts = t.yts = (int64_t)N * T * 4;
+        t.xrs = t.yrs = (uint32_t)(T * 4);
+    } else {
+        t.lchunks = 1;
+        t.xts = t.yts = 16;
+        t.xrs = (uint32_t)(args->ldx * 4);
+        t.yrs = (uint32_t)(args->ldy * 4);
+    }
+    t.n_tiles = (int32_t)(args->n_params / 4);
+    t.csr_off = tp.csr_off;
+    t.scratch_off = tp.scratch_off;
+    t.trace_off = tp.trace_off;
+    const size_t need = align_up((size_t)tp.grid * rounds * N * 4);
+    char *ws = static_cast<char *>(workspace);
+    if (!ws || (reinterpret_cast<uintptr_t>(ws) & 15u) || ws_bytes < need)
+        return fail(DL_ERR_WORKSPACE, "dl_mix_rounds_trace: needs a 16-byte aligned workspace "
+                                      "of %zu bytes (dl_mix_trace_workspace_bytes)", need);
+    t.dev_partial = reinterpret_cast<float *>(ws);
+    const int lds = (int)(tp.fixed_lds + 4u * (uint32_t)rounds * (uint32_t)N);
+    hipError_t e = dl::launch_mix_trace(t, rounds, tp.grid, lds, trace,
+                                        static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? DL_OK : hip_fail(e, "mix_trace_kernel launch");
+}
 
 int dl_mix_rounds_plan(const dl_mix_args *args, dl_mix_plan *plan) {
     g_err.clear();

@@ -188,6 +188,35 @@ def mix_rounds(W: DeviceCsr, X, Y, rounds, G=None, lr=0.0, dev_sq=None, dev_max=
     return True
 
 
+def trace_max_rounds(W: DeviceCsr, X, Y, tiled=None):
+    """dl_mix_trace_plan: the most rounds one traced pass can run, or 0 when the traced kernel
+    does not fit this graph/layout (then the caller loops ``mix_round``)."""
+    lib = _lib.load()
+    args = (mix_args_tiled(W, tiled[0], tiled[1], X, Y) if tiled is not None
+            else mix_args(W, X, Y))
+    k = ctypes.c_int32(0)
+    rc = lib.dl_mix_trace_plan(ctypes.byref(args), ctypes.byref(k))
+    if rc == _lib.DL_ERR_UNSUPPORTED:
+        return 0
+    _lib.check(rc, "dl_mix_trace_plan")
+    return int(k.value)
+
+
+def mix_rounds_trace(W: DeviceCsr, X, Y, rounds, trace, workspace: Workspace = None,
+                     tiled=None):
+    """dl_mix_rounds_trace: Y = W^rounds X in one HBM pass and trace[r] = the max deviation
+    after round r + 1 (device float32[rounds]).  X is left unmodified."""
+    lib = _lib.load()
+    args = (mix_args_tiled(W, tiled[0], tiled[1], X, Y) if tiled is not None
+            else mix_args(W, X, Y))
+    if trace.dtype != torch.float32 or trace.device != W.device or trace.numel() < rounds:
+        raise ValueError("trace must be a float32 device tensor of at least `rounds` entries")
+    workspace = workspace or Workspace(W.device)
+    wp, wn = workspace.ptr_size(lib.dl_mix_trace_workspace_bytes(W.n_rows, int(rounds)))
+    _lib.check(lib.dl_mix_rounds_trace(ctypes.byref(args), int(rounds), _lib.ptr(trace), wp, wn,
+                                       _lib.stream_handle(W.device)), "dl_mix_rounds_trace")
+
+
 def rounds_plan(W: DeviceCsr, X, Y, deviation=False, tiled=None):
     """dl_mix_rounds_plan: the multi-round configuration, or None when it does not fit."""
     lib = _lib.load()
@@ -450,6 +479,18 @@ class GossipEngine:
                   dev_sq=self.dev_sq if deviation else None,
                   dev_max=self.dev_max if deviation else None, mean=mean, workspace=self.ws,
                   tiled=(self.P, self.T) if self.layout == "tiled" else None)
+        self.X, self.Y = self.Y, self.X
+
+    def trace_max_rounds(self):
+        """Most rounds one traced pass (``rounds_traced``) can run; 0 = not supported."""
+        return trace_max_rounds(self.W, self.X, self.Y,
+                                tiled=(self.P, self.T) if self.layout == "tiled" else None)
+
+    def rounds_traced(self, k, trace):
+        """k rounds X <- W^k X in one HBM pass; trace[r] = max deviation after round r + 1
+        (device float32[k]; what Mixer.mix(times, eps) tests after every round)."""
+        mix_rounds_trace(self.W, self.X, self.Y, int(k), trace, workspace=self.ws,
+                         tiled=(self.P, self.T) if self.layout == "tiled" else None)
         self.X, self.Y = self.Y, self.X
 
     def rounds(self, k, G=None, lr=0.0, deviation=False, mean=None):

@@ -9,7 +9,10 @@ of the round count; the reference's per-evaluation debug log is replayed from th
 trace of max deviations.  Otherwise each round is one
 ``dl_mix_round`` launch (the reference's ``_mix_params_once`` fold, :43-49, bit-identical in
 fp32), and when ``eps`` is given the same launch also produces the per-agent deviation
-(:51-66) so the stop test costs one 4-byte readback per round.  With ``eps=None`` the ``times``
+(:51-66) so the stop test costs one 4-byte readback per round -- or, when the graph fits the
+traced multi-round kernel (<= 1024 agents, doubly stochastic W), K rounds run in one HBM pass
+that also returns their K per-round max deviations (``dl_mix_rounds_trace``), and the stop
+round is found on the host.  With ``eps=None`` the ``times``
 rounds have nothing in between, so they run as ONE ``dl_mix_rounds`` pass (every round on
 LDS-resident column tiles, bit-identical to ``times`` single rounds).  The results are written
 back into the models once at the end (:34-35, 71-76).
@@ -71,6 +74,8 @@ class Mixer(object):
             dev_max = torch.empty(1, dtype=torch.float32, device=X.device)
 
             stopping_criterion = self._update_stopping_criterion(X, times_done, times, eps)
+            if not stopping_criterion and fused_dev:
+                X, times_done, stopping_criterion = self._mix_traced(W, X, times, eps)
             if not stopping_criterion and eps is None:
                 # times rounds, no stop test in between: one pass over HBM (rows padded with
                 # zero columns to whole tiles; zeros mix to zeros)
@@ -131,6 +136,47 @@ class Mixer(object):
             first = False
             if stopped:
                 return done
+
+    _TRACE_MIN_ROUNDS = 4     # below this many rounds per traced pass the round loop is as good
+    _TRACE_MAX_ROUNDS = 256   # rounds per traced pass (LDS permitting)
+
+    def _mix_traced(self, W, X, times, eps):
+        """mixer.py:27-32 with eps set, in passes of K rounds (dl_mix_rounds_trace): each pass
+        runs K rounds in one HBM pass and returns the K per-round max deviations, which are
+        logged and tested in order exactly as the reference evaluates them after every round.
+        When the stop round falls inside a pass, that many rounds are re-run from the pass's
+        input (left intact).  Returns (X, times_done, stopped); stopped is False, with nothing
+        done, when the traced kernel does not fit (the caller's round loop takes over)."""
+        P = X.shape[1]
+        Pp = -(-P // 64) * 64
+        cur = torch.nn.functional.pad(X, (0, Pp - P)) if Pp != P else X
+        nxt = torch.empty_like(cur)
+        K = min(_engine.trace_max_rounds(W, cur, nxt), self._TRACE_MAX_ROUNDS)
+        if K < min(self._TRACE_MIN_ROUNDS, self._TRACE_MAX_ROUNDS):
+            return X, 0, False
+        trace = torch.empty(K, dtype=torch.float32, device=X.device)
+        ws = self._wspace()
+        done = 0
+        while True:
+            _engine.mix_rounds_trace(W, cur, nxt, K, trace, workspace=ws)
+            stop_at = None
+            for i, d in enumerate(trace.tolist()):
+                max_dev = np.float32(d)
+                self.logger.debug('Mixer calculate max deviation= {}'.format(max_dev))
+                if max_dev < eps and done + i + 1 >= times:
+                    stop_at = i + 1
+                    break
+            if stop_at is None:
+                cur, nxt = nxt, cur
+                done += K
+                continue
+            if stop_at < K:   # the same rounds again from the pass's input (bit-identical)
+                if not _engine.mix_rounds(W, cur, nxt, stop_at, workspace=ws):
+                    for _ in range(stop_at):
+                        _engine.mix_round(W, cur, nxt, workspace=ws)
+                        cur, nxt = nxt, cur
+                    nxt = cur
+            return nxt[:, :P], done + stop_at, True
 
     def _update_stopping_criterion(self, X, times_done, max_times, eps, fused=None):
         """mixer.py:40-41; the deviation is only evaluated when eps is set (short circuit)."""

@@ -15,6 +15,8 @@
  *                          replaces the per-neighbour value messages of consensus_asyncio.py:236-284
  *   dl_column_sum       <- the np.mean numerator of mixer.py:61 (multi-GPU global mean)
  *   dl_mix_rounds       <- Mixer.mix(times=K) with eps=None: K rounds in one HBM pass  mixer.py:18-38
+ *   dl_mix_rounds_trace <- Mixer.mix(times, eps) when X does not fit one workgroup: K rounds in
+ *                          one HBM pass plus the K per-round max deviations  mixer.py:18-41, 51-66
  *   dl_mix_until        <- Mixer.mix(times, eps): loop, deviation and stop rule in one launch
  *                          mixer.py:18-41
  *   dl_consensus_gd     <- the Titanic notebook's consensus GD run (local logreg steps,
@@ -140,6 +142,22 @@ int dl_mix_round(const dl_mix_args *args, void *workspace, size_t ws_bytes, dl_s
 int dl_mix_rounds_plan(const dl_mix_args *args, dl_mix_plan *plan);
 int dl_mix_rounds(const dl_mix_args *args, int32_t rounds, void *workspace, size_t ws_bytes,
                   dl_stream_t stream);
+
+/* `rounds` mixing rounds in one HBM pass, y = W^rounds x, with the per-round disagreement
+ * trace[r] = max_a ||x_a^(r+1) - mean(x)||_2 (device float[rounds]) for r < rounds -- what
+ * Mixer.mix(times, eps) (mixer.py:18-41) evaluates after every round (_get_max_deviation,
+ * :51-55, 57-66).  The caller finds the first round whose value is below eps (and >= times); if
+ * it lies inside the pass it re-runs that many rounds from x with dl_mix_rounds (x is not
+ * modified).  Rounds are the dl_mix_round fold (bit-identical).  The mean is the column mean of
+ * x: W must be doubly stochastic (mean(W x) = mean(x)).  One agent per thread: 2 <= n_rows <=
+ * 1024; no halo rows; g must be NULL; n_params % 4 == 0; 16-byte aligned operands, row-major
+ * or column-tiled (tile_cols).  dl_mix_trace_plan gives the most rounds one pass can trace (the
+ * [rounds][n_rows] fp32 trace lives in LDS beside two column images) or DL_ERR_UNSUPPORTED.
+ * Workspace: dl_mix_trace_workspace_bytes(n_rows, rounds). */
+int dl_mix_trace_plan(const dl_mix_args *args, int32_t *max_rounds);
+size_t dl_mix_trace_workspace_bytes(int32_t n_rows, int32_t rounds);
+int dl_mix_rounds_trace(const dl_mix_args *args, int32_t rounds, float *trace, void *workspace,
+                        size_t ws_bytes, dl_stream_t stream);
 
 /* Mixer.mix(times, eps) (utils/consensus_simple/mixer.py:18-41) as ONE launch: the loop
  *     stop = (!use_eps || max_a ||x_a - mean|| < eps) && done >= times

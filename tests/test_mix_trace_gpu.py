@@ -1,0 +1,161 @@
+"""GPU parity of the traced multi-round pass (dl_mix_rounds_trace: K rounds in one HBM pass plus
+the K per-round max deviations) and of the Mixer.mix(times, eps) path built on it, against the
+oracle's restatement of the reference loop (oracle/mixer_ref: mix_once, deviation, mixer_mix;
+utils/consensus_simple/mixer.py:18-66).  Iterates bit-exact, round counts equal, deviations
+within 1e-5 relative or the mean-rounding noise floor 8 sqrt(P) eps32 max|mean| (the kernel
+takes the column mean of the pass input, exact for doubly stochastic W; numpy re-sums it)."""
+import logging
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import mixer_ref as M
+from test_mix_gpu import bits
+
+pytestmark = pytest.mark.gpu
+
+
+def E():
+    from distributed_learning_amd import engine
+    return engine
+
+
+def rr_csr(n, seed):
+    from distributed_learning_amd.graph import (best_constant_weight, from_edge_weights,
+                                                random_regular_edges)
+    edges = random_regular_edges(4, n, seed=seed)
+    w = best_constant_weight(edges, list(range(n)))
+    return from_edge_weights(edges, [w] * len(edges), list(range(n)))
+
+
+def metropolis_csr(n, p, seed):
+    """Erdos-Renyi graph (plus a ring, connected) with Metropolis weights: irregular, symmetric,
+    doubly stochastic -- the CSR-in-LDS path of the kernel."""
+    from distributed_learning_amd.graph import from_edge_weights
+    rng = np.random.default_rng(seed)
+    es = {(i, (i + 1) % n) for i in range(n)}
+    for i in range(n):
+        for j in range(i + 1, n):
+            if rng.random() < p:
+                es.add((i, j))
+    edges = sorted((min(a, b), max(a, b)) for a, b in es)
+    deg = np.zeros(n, int)
+    for a, b in edges:
+        deg[a] += 1
+        deg[b] += 1
+    w = [1.0 / (1 + max(deg[a], deg[b])) for a, b in edges]
+    return from_edge_weights(edges, w, list(range(n)))
+
+
+def noise_floor(X):
+    return 8 * np.sqrt(X.shape[1]) * np.finfo(np.float32).eps * np.abs(X.mean(axis=0)).max()
+
+
+CASES = [("rr4", 64, 4096, 0), ("rr4", 1024, 256, 1), ("metro", 50, 1000, 2),
+         ("metro", 7, 4, 3), ("rr4", 16, 65536, 4)]
+
+
+def make(kind, n, seed):
+    return rr_csr(n, seed) if kind == "rr4" else metropolis_csr(n, 0.1, seed)
+
+
+@pytest.mark.parametrize("kind,n,P,seed", CASES)
+@pytest.mark.parametrize("layout", ["rows", "tiled"])
+def test_trace_pass_matches_round_by_round(cuda, kind, n, P, seed, layout):
+    e = E()
+    csr = make(kind, n, seed)
+    assert csr.doubly_stochastic
+    rng = np.random.default_rng(seed)
+    X = rng.standard_normal((n, P), dtype=np.float32)
+    W = e.DeviceCsr(csr, cuda)
+    Xd = torch.from_numpy(X).to(cuda)
+    tiled = None
+    if layout == "tiled":
+        T = 16
+        if P % T:
+            pytest.skip("tiled layout needs whole tiles here")
+        Xd = e.to_tiled(Xd, T)
+        tiled = (P, T)
+    Yd = torch.full_like(Xd, float("nan"))
+    kmax = e.trace_max_rounds(W, Xd, Yd, tiled=tiled)
+    assert kmax >= 4
+    K = min(kmax, 23)
+    trace = torch.full((K,), -1.0, device=cuda)
+    X0 = Xd.clone()
+    e.mix_rounds_trace(W, Xd, Yd, K, trace, tiled=tiled)
+    assert torch.equal(Xd, X0)                     # the pass input is left intact
+    got = (e.from_tiled(Yd, P) if tiled else Yd).cpu().numpy()
+    Z, ref = X, []
+    for _ in range(K):
+        Z = M.mix_once(Z, csr.rowptr, csr.col, csr.w)
+        ref.append(M.deviation(Z).max())
+    assert np.array_equal(bits(got), bits(Z))
+    np.testing.assert_allclose(trace.cpu().numpy(), ref, rtol=1e-5, atol=noise_floor(X))
+
+
+def test_trace_plan_rejects_unsupported(cuda):
+    from test_mix_gpu import graph_csr
+    e = E()
+    X = torch.randn(8, 64, device=cuda)
+    Y = torch.empty_like(X)
+    # random directed neighbours: not doubly stochastic -> the round loop takes over
+    assert e.trace_max_rounds(e.DeviceCsr(graph_csr(8, 3, seed=0), cuda), X, Y) == 0
+    big = torch.randn(2048, 64, device=cuda)
+    assert e.trace_max_rounds(e.DeviceCsr(rr_csr(2048, 0), cuda), big, torch.empty_like(big)) == 0
+    W = e.DeviceCsr(rr_csr(8, 0), cuda)
+    k = e.trace_max_rounds(W, X, Y)
+    with pytest.raises(ValueError, match="rounds must be"):
+        e.mix_rounds_trace(W, X, Y, k + 1, torch.empty(k + 1, device=cuda))
+
+
+class _Rec(logging.Handler):
+    def __init__(self):
+        super().__init__()
+        self.lines = []
+
+    def emit(self, record):
+        self.lines.append(record.getMessage())
+
+
+@pytest.mark.parametrize("times,eps,kmax", [(1, 1e-2, 256), (1, 1e-2, 5), (40, 1e-1, 7),
+                                             (3, 5e-1, 4), (1, 1e-4, 64)])
+def test_mixer_traced_path_matches_reference_loop(cuda, monkeypatch, times, eps, kmax):
+    """Mixer.mix(times, eps) on models too large for the one-workgroup loop goes through the
+    traced passes: same round count, same bits, one debug line per evaluation."""
+    from distributed_learning_amd import engine
+    from distributed_learning_amd.networks import ANNModel
+    from distributed_learning_amd.utils.consensus_simple import Mixer
+    from distributed_learning_amd.utils.consensus_simple import mixer as mixer_mod
+    calls = []
+    real = engine.mix_rounds_trace
+    monkeypatch.setattr(engine, "mix_rounds_trace",
+                        lambda *a, **k: (calls.append(a[3]), real(*a, **k))[1])
+    monkeypatch.setattr(mixer_mod.Mixer, "_TRACE_MAX_ROUNDS", kmax)
+    log = logging.getLogger("traced")
+    log.setLevel(logging.DEBUG)
+    h = _Rec()
+    log.addHandler(h)
+    torch.manual_seed(1)
+    n = 24
+    keys = [f"agent{i}" for i in range(n)]
+    csr = rr_csr(n, 5)
+    topo = {}
+    for i, k in enumerate(keys):
+        row = range(csr.rowptr[i], csr.rowptr[i + 1])
+        topo[k] = {keys[csr.col[e]]: float(csr.w[e]) for e in row}
+    models = {k: ANNModel(60, 40, 10).to(cuda) for k in keys}
+    X0 = np.stack([torch.cat([p.data.reshape(-1) for p in models[k].parameters()]).cpu().numpy()
+                   for k in keys])
+    assert not engine.until_fits(engine.DeviceCsr(csr, cuda), X0.shape[1])
+    rp, cl, w = M.topology_to_csr(topo)
+    want, want_n = M.mixer_mix(X0, rp, cl, w, times=times, eps=eps)
+    mixer = Mixer(models, topo, log)
+    assert mixer.mix(times=times, eps=eps) == want_n
+    assert calls, "the traced pass was not used"
+    got = np.stack([torch.cat([p.data.reshape(-1) for p in models[k].parameters()]).cpu().numpy()
+                    for k in keys])
+    assert np.array_equal(bits(got), bits(want))
+    devs = [ln for ln in h.lines if ln.startswith("Mixer calculate max deviation")]
+    assert len(devs) == want_n + 1
+    log.removeHandler(h)

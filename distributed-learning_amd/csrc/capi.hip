@@ -406,11 +406,12 @@ int plan_rounds(const dl_mix_args *a, Plan *pl) {
     return DL_OK;
 }
 
-// dl_mix_rounds_trace configuration: one agent per thread, one float4 column chunk per step.
+// dl_mix_rounds_trace configuration: one agent per thread, C float4 column chunks per step.
 struct TracePlan {
-    int32_t max_rounds;  // rounds whose [rounds][n_rows] trace fits LDS beside the images
-    int32_t grid;
-    uint32_t csr_off, scratch_off, trace_off, fixed_lds;
+    int32_t max_rounds;  // rounds per traced pass (the per-round deviations live in VGPRs)
+    int32_t grid, chunks;
+    int64_t n_steps;
+    uint32_t csr_off, scratch_off, lds;
 };
 
 int plan_trace(const dl_mix_args *a, TracePlan *tp) {
@@ -434,16 +435,29 @@ int plan_trace(const dl_mix_args *a, TracePlan *tp) {
     const uint32_t csr = in_regs ? 0u : dl::csr_lds_bytes(N, a->W.nnz, reg, n_w);
     if (!in_regs && csr == 0)
         return fail(DL_ERR_UNSUPPORTED, "dl_mix_rounds_trace: CSR too large");
-    const uint32_t img = 2u * (uint32_t)N * 16u;
-    tp->csr_off = img;
-    tp->scratch_off = (uint32_t)align_up(img + csr);
-    tp->trace_off = tp->scratch_off + (dl::kTileThreads / 64) * 16u;
-    tp->fixed_lds = tp->trace_off;
-    const int64_t k = ((int64_t)dl::kLdsBytes - tp->fixed_lds) / (4 * (int64_t)N);
-    if (k < 1) return fail(DL_ERR_UNSUPPORTED, "dl_mix_rounds_trace: no LDS left for a trace");
-    tp->max_rounds = (int32_t)(k < 1024 ? k : 1024);
     const int64_t nq = a->n_params / 4;
-    tp->grid = (int32_t)balanced_grid(nq, device_cus());
+    const int64_t lc = a->tile_cols > 0 ? a->tile_cols / 4 : 0;   // 0: row-major
+    // widest chunk count whose two images fit LDS (a round then does C outputs per thread)
+    tp->chunks = 0;
+    for (int c = 4; c >= 1; c >>= 1) {
+        const uint32_t img = 2u * (uint32_t)N * 16u * (uint32_t)c;
+        const uint32_t scr = (uint32_t)align_up(img + csr);
+        const uint32_t lds = scr + (dl::kTileThreads / 64) * 16u * (uint32_t)c;
+        // a step's chunks must be whole (nq % c) and lie in one operand tile (lc % c)
+        if (lds <= (uint32_t)dl::kLdsBytes && nq % c == 0 && (lc == 0 || lc % c == 0)) {
+            tp->chunks = c;
+            tp->csr_off = img;
+            tp->scratch_off = scr;
+            tp->lds = lds;
+            break;
+        }
+    }
+    if (tp->chunks == 0)
+        return fail(DL_ERR_UNSUPPORTED, "dl_mix_rounds_trace: two column images of %d agents "
+                                        "do not fit LDS", N);
+    tp->max_rounds = dl::kTraceRounds;
+    tp->n_steps = nq / tp->chunks;
+    tp->grid = (int32_t)balanced_grid(tp->n_steps, device_cus());
     return DL_OK;
 }
 
@@ -480,8 +494,8 @@ int dl_mix_rounds_trace(const dl_mix_args *args, int32_t rounds, float *trace, v
     rc = plan_trace(args, &tp);
     if (rc) return rc;
     if (rounds < 1 || rounds > tp.max_rounds)
-        return fail(DL_ERR_INVALID, "dl_mix_rounds_trace: rounds must be in [1, %d] (the LDS "
-                                    "trace), got %d", tp.max_rounds, rounds);
+        return fail(DL_ERR_INVALID, "dl_mix_rounds_trace: rounds must be in [1, %d] (one "
+                                    "traced pass), got %d", tp.max_rounds, rounds);
     dl::TileArgs t = tile_args(args);
     if (!t.vec)
         return fail(DL_ERR_UNSUPPORTED, "dl_mix_rounds_trace: operands must be 16-byte aligned "
@@ -498,18 +512,16 @@ int dl_mix_rounds_trace(const dl_mix_args *args, int32_t rounds, float *trace, v
         t.xrs = (uint32_t)(args->ldx * 4);
         t.yrs = (uint32_t)(args->ldy * 4);
     }
-    t.n_tiles = (int32_t)(args->n_params / 4);
+    t.n_tiles = (int32_t)tp.n_steps;
     t.csr_off = tp.csr_off;
     t.scratch_off = tp.scratch_off;
-    t.trace_off = tp.trace_off;
     const size_t need = align_up((size_t)tp.grid * rounds * N * 4);
     char *ws = static_cast<char *>(workspace);
     if (!ws || (reinterpret_cast<uintptr_t>(ws) & 15u) || ws_bytes < need)
         return fail(DL_ERR_WORKSPACE, "dl_mix_rounds_trace: needs a 16-byte aligned workspace "
                                       "of %zu bytes (dl_mix_trace_workspace_bytes)", need);
     t.dev_partial = reinterpret_cast<float *>(ws);
-    const int lds = (int)(tp.fixed_lds + 4u * (uint32_t)rounds * (uint32_t)N);
-    hipError_t e = dl::launch_mix_trace(t, rounds, tp.grid, lds, trace,
+    hipError_t e = dl::launch_mix_trace(t, tp.chunks, rounds, tp.grid, (int)tp.lds, trace,
                                         static_cast<hipStream_t>(stream));
     return e == hipSuccess ? DL_OK : hip_fail(e, "mix_trace_kernel launch");
 }

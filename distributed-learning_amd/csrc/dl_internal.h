@@ -44,7 +44,6 @@ struct TileArgs {
     int64_t xts, gts, yts;
     uint32_t xrs, grs, yrs;
     uint32_t hrs;     // halo row stride in bytes (ldh*4)
-    uint32_t trace_off;  // mix_trace_kernel: byte offset of the [rounds][n_rows] LDS trace
     int32_t lchunks;     // mix_trace_kernel: float4 chunks per operand tile (1 = row-major)
     float *dev_partial;  // [gridDim.x][n_rows] per-workgroup partial ||y_a - mean||^2
     float *mean;         // [n_params] nullable
@@ -71,8 +70,9 @@ hipError_t launch_mix_multi(const TileArgs &a, int chunks, int rounds, bool sgd,
                             int grid, int lds, hipStream_t s);
 // K rounds on LDS-resident column chunks with the per-round max deviation trace
 // (mix_trace.hip): mix_trace_kernel + trace_reduce into trace_out[rounds]
-hipError_t launch_mix_trace(const TileArgs &a, int rounds, int grid, int lds, float *trace_out,
-                            hipStream_t s);
+constexpr int kTraceRounds = 32;   // rounds per traced pass (per-round deviations in VGPRs)
+hipError_t launch_mix_trace(const TileArgs &a, int chunks, int rounds, int grid, int lds,
+                            float *trace_out, hipStream_t s);
 // max_zeroed: an earlier launch on the stream already zeroed dev_max (TileArgs::dev_max_zero)
 hipError_t launch_dev_reduce(const float *partial, int nparts, int n_rows, float *dev_sq,
                              float *dev_max, hipStream_t s, bool max_zeroed = false);

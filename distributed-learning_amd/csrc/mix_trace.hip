@@ -4,17 +4,18 @@
 // whose value is below eps.  mix_multi_kernel already runs K rounds on LDS-resident column tiles
 // (mixing is column-independent); the stop test is what kept eps-loops on one HBM-bound launch
 // per round.  Here every workgroup also accumulates, for each of the K rounds, every agent's
-// squared deviation over its own columns in an LDS trace [K][N]; one reduce launch turns the
-// per-workgroup traces into the K per-round max deviations.  The host then finds the stop round
+// squared deviation over its own columns; one reduce launch turns the per-workgroup traces
+// [grid][K][N] into the K per-round max deviations.  The host then finds the stop round
 // and, if it lies inside the pass, re-runs that many rounds from the pass's input (still intact:
 // X -> Y).  The rounds are the same CSR-order fp32 fold as the one-round kernel, so the iterates
 // are bit-identical to round-by-round mixing.
 //
-// Geometry: one agent per thread (N <= 1024), one float4 column chunk per tile step, so a
-// thread's trace slot is a single LDS word it alone updates (no shuffles, no atomics).  LDS:
-// two chunk images 2 x N x 16 B, the trace K x N x 4 B, the CSR (unless register-cached), a
-// 16-float4 mean scratch.  W must be doubly stochastic: the column mean of every round equals
-// the mean of the pass's input chunk (mean(W t) = mean(t)), as in the fused one-round deviation.
+// Geometry: one agent per thread (N <= 1024), C float4 column chunks per step (the widest of
+// 4, 2, 1 whose two images fit LDS), the per-round squared deviations in registers, so nothing
+// is shuffled or atomically added per round.  LDS: two images 2 x N x C x 16 B, the CSR (unless
+// register-cached), a 16 x C float4 mean scratch.  W must be doubly stochastic: the column mean of every
+// round equals the mean of the pass's input chunk (mean(W t) = mean(t)), as in the fused
+// one-round deviation.
 #include "dl_internal.h"
 
 namespace dl {
@@ -33,24 +34,30 @@ __device__ __forceinline__ void tr_store4(float4 v, char *p) {
 }
 
 // RE > 0: regular graph of RE entries per row sharing row 0's weights, CSR in registers.
-template <int RE>
+// C: float4 column chunks per agent per step (T = 4C columns): a round does C outputs per thread
+// between barriers.  The per-round deviations live in registers (dacc[r], the round loop
+// unrolled up to kTraceRounds; 118 VGPRs at C = 4, no spills).  Measured against an LDS trace
+// [rounds][N] (rolled loop, which leaves room for two images only at C <= 2 for 1024 agents):
+// 1218 rounds/s at C = 2 vs 1589 at C = 4 here (c2 sizes, profiles/r05/trace_bench.log).
+template <int RE, int C>
 __global__ void __launch_bounds__(kTileThreads) mix_trace_kernel(TileArgs a, int rounds) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int KR = kTraceRounds;
     const int tid = threadIdx.x;
     const int N = a.n_rows;
     const bool mine = tid < N;
+    // images chunk-major [C][N]: lanes (consecutive agents) reading random neighbours of one
+    // chunk plane hit 16-byte slots spread over all banks; agent-major [N][C] rows (64 B at C = 4)
+    // put every neighbour of a chunk on the same quarter of the banks (890 vs 1589 rounds/s at c2)
     float4 *img0 = reinterpret_cast<float4 *>(smem);
-    float4 *img1 = img0 + N;
-    float *trace = reinterpret_cast<float *>(smem + a.trace_off);
-    float4 *scratch = reinterpret_cast<float4 *>(smem + a.scratch_off);
+    float4 *img1 = img0 + N * C;
+    float4 *scratch = reinterpret_cast<float4 *>(smem + a.scratch_off);   // [16][C]
     float *lw = reinterpret_cast<float *>(smem + a.csr_off);
     uint16_t *lcol = reinterpret_cast<uint16_t *>(smem + a.csr_off + 4u * (uint32_t)a.n_w);
     uint16_t *lrp = lcol + a.nnz;
     const int reg = a.regular;
     const bool wshared = a.n_w != a.nnz;
 
-    if (mine)
-        for (int r = 0; r < rounds; ++r) trace[r * N + tid] = 0.f;
     if constexpr (RE == 0) {
         for (int i = tid; i < a.n_w; i += kTileThreads) lw[i] = a.w[i];
         for (int i = tid; i < a.nnz; i += kTileThreads) lcol[i] = (uint16_t)a.col[i];
@@ -67,11 +74,11 @@ __global__ void __launch_bounds__(kTileThreads) mix_trace_kernel(TileArgs a, int
             wreg[e] = a.w[e];
         }
     }
-    // agent tid's output chunk: left fold in CSR order from +0.0 (mixer.py:47)
-    auto mix = [&](const float4 *src) {
+    // agent tid's output chunk c: left fold in CSR order from +0.0 (mixer.py:47)
+    auto mix = [&](const float4 *src, int c) {
         float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
         if constexpr (RE > 0) {
-            const char *base = reinterpret_cast<const char *>(src);
+            const char *base = reinterpret_cast<const char *>(src + c * N);
 #pragma unroll
             for (int e = 0; e < RE; ++e) {
                 const float4 v = *reinterpret_cast<const float4 *>(base + coff[e]);
@@ -93,7 +100,7 @@ __global__ void __launch_bounds__(kTileThreads) mix_trace_kernel(TileArgs a, int
             const float *wr = wshared ? lw - e0 : lw;
             for (int e = e0; e < e1; ++e) {
                 const float w = wr[e];
-                const float4 v = src[lcol[e]];
+                const float4 v = src[c * N + lcol[e]];
                 acc.x = acc.x + w * v.x;
                 acc.y = acc.y + w * v.y;
                 acc.z = acc.z + w * v.z;
@@ -102,67 +109,96 @@ __global__ void __launch_bounds__(kTileThreads) mix_trace_kernel(TileArgs a, int
         }
         return acc;
     };
-    // byte offset of (agent tid, chunk q) in an operand laid out in lc-chunk tiles
-    const int64_t lc = a.lchunks;
-    auto off = [&](int64_t ts, uint32_t rs, int64_t q) {
-        return (q / lc) * ts + (int64_t)tid * rs + (q % lc) * 16;
+    // byte offset of (agent tid, chunk q) in an operand laid out in lc-chunk tiles (lc a power
+    // of two; the step index is wave-uniform, so the tile part is scalar arithmetic)
+    const int lsh = __builtin_ctz((unsigned)a.lchunks);
+    const int64_t lmask = (int64_t)a.lchunks - 1;
+    const int64_t xrow = (int64_t)tid * a.xrs, yrow = (int64_t)tid * a.yrs;
+    auto off = [&](int64_t ts, int64_t row, int64_t q) {
+        return (q >> lsh) * ts + row + (q & lmask) * 16;
     };
     const char *xb = reinterpret_cast<const char *>(a.x);
     char *yb = reinterpret_cast<char *>(a.y);
-    const int64_t nq = a.n_tiles;   // float4 column chunks
-    float4 px = make_float4(0.f, 0.f, 0.f, 0.f);
-    int64_t q = blockIdx.x;
-    if (q < nq && mine) px = tr_load4(xb + off(a.xts, a.xrs, q));
-    __syncthreads();   // CSR and trace initialised
-    for (; q < nq; q += gridDim.x) {
-        if (mine) img0[tid] = px;
-        float4 cs = mine ? px : make_float4(0.f, 0.f, 0.f, 0.f);
+    const int64_t nsteps = a.n_tiles;   // steps of C float4 column chunks
+    float dacc[KR];   // this agent's squared deviation after each round (registers)
 #pragma unroll
-        for (int m = 1; m < 64; m <<= 1) {
-            cs.x += __shfl_xor(cs.x, m);
-            cs.y += __shfl_xor(cs.y, m);
-            cs.z += __shfl_xor(cs.z, m);
-            cs.w += __shfl_xor(cs.w, m);
+    for (int r = 0; r < KR; ++r) dacc[r] = 0.f;
+    float4 px[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) px[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+    int64_t q = blockIdx.x;
+    if (q < nsteps && mine) {
+#pragma unroll
+        for (int c = 0; c < C; ++c) px[c] = tr_load4(xb + off(a.xts, xrow, q * C + c));
+    }
+    __syncthreads();   // CSR staged
+    for (; q < nsteps; q += gridDim.x) {
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            if (mine) img0[c * N + tid] = px[c];
+            float4 cs = mine ? px[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int m = 1; m < 64; m <<= 1) {
+                cs.x += __shfl_xor(cs.x, m);
+                cs.y += __shfl_xor(cs.y, m);
+                cs.z += __shfl_xor(cs.z, m);
+                cs.w += __shfl_xor(cs.w, m);
+            }
+            if ((tid & 63) == 0) scratch[(tid >> 6) * C + c] = cs;
         }
-        if ((tid & 63) == 0) scratch[tid >> 6] = cs;
         __syncthreads();
-        float4 mean = make_float4(0.f, 0.f, 0.f, 0.f);
-        for (int wv = 0; wv < kTileThreads / 64; ++wv) {
-            const float4 p = scratch[wv];
-            mean.x += p.x;
-            mean.y += p.y;
-            mean.z += p.z;
-            mean.w += p.w;
-        }
+        float4 mean[C];
         const float n = (float)N;
-        mean.x = mean.x / n;
-        mean.y = mean.y / n;
-        mean.z = mean.z / n;
-        mean.w = mean.w / n;
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            float4 m4 = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 2   // (fully unrolled, the 16 reads are hoisted: 64 VGPRs at once, spills)
+            for (int wv = 0; wv < kTileThreads / 64; ++wv) {
+                const float4 p = scratch[wv * C + c];
+                m4.x += p.x;
+                m4.y += p.y;
+                m4.z += p.z;
+                m4.w += p.w;
+            }
+            mean[c] = make_float4(m4.x / n, m4.y / n, m4.z / n, m4.w / n);
+        }
         const int64_t qn = q + gridDim.x;
-        if (qn < nq && mine) px = tr_load4(xb + off(a.xts, a.xrs, qn));   // lands during the rounds
+        if (qn < nsteps && mine) {   // lands during the rounds
+#pragma unroll
+            for (int c = 0; c < C; ++c) px[c] = tr_load4(xb + off(a.xts, xrow, qn * C + c));
+        }
         const float4 *src = img0;
         float4 *dst = img1;
-        for (int r = 0; r < rounds; ++r) {
-            if (mine) {
-                const float4 y = mix(src);
-                if (r + 1 < rounds)
-                    dst[tid] = y;
-                else
-                    tr_store4(y, yb + off(a.yts, a.yrs, q));
-                const float dx = y.x - mean.x, dy = y.y - mean.y;
-                const float dz = y.z - mean.z, dw = y.w - mean.w;
-                trace[r * N + tid] += (dx * dx + dy * dy) + (dz * dz + dw * dw);
+#pragma unroll
+        for (int r = 0; r < KR; ++r) {
+            if (r < rounds) {
+                if (mine) {
+                    float d = 0.f;
+#pragma unroll
+                    for (int c = 0; c < C; ++c) {
+                        const float4 y = mix(src, c);
+                        if (r + 1 < rounds)
+                            dst[c * N + tid] = y;
+                        else
+                            tr_store4(y, yb + off(a.yts, yrow, q * C + c));
+                        const float dx = y.x - mean[c].x, dy = y.y - mean[c].y;
+                        const float dz = y.z - mean[c].z, dw = y.w - mean[c].w;
+                        d += (dx * dx + dy * dy) + (dz * dz + dw * dw);
+                    }
+                    dacc[r] += d;
+                }
+                __syncthreads();   // dst complete before it is read; img0/scratch reuse
+                const float4 *t = src;
+                src = dst;
+                dst = const_cast<float4 *>(t);
             }
-            __syncthreads();   // dst complete before it is read; img0/scratch reuse next chunk
-            const float4 *t = src;
-            src = dst;
-            dst = const_cast<float4 *>(t);
         }
     }
-    if (mine)
-        for (int r = 0; r < rounds; ++r)
-            a.dev_partial[((int64_t)blockIdx.x * rounds + r) * N + tid] = trace[r * N + tid];
+    if (mine) {
+#pragma unroll
+        for (int r = 0; r < KR; ++r)
+            if (r < rounds) a.dev_partial[((int64_t)blockIdx.x * rounds + r) * N + tid] = dacc[r];
+    }
 }
 
 // out[r] = max_a sqrt(sum_b partial[b][r][a]) (fp64 sum in workgroup order, then float, as
@@ -189,22 +225,35 @@ __global__ void __launch_bounds__(1024) trace_reduce_kernel(const float *__restr
     }
 }
 
-template <int RE>
-hipError_t launch_re(const TileArgs &a, int rounds, int grid, int lds, hipStream_t s) {
-    const void *k = reinterpret_cast<const void *>(mix_trace_kernel<RE>);
+template <int RE, int C>
+hipError_t launch_rc(const TileArgs &a, int rounds, int grid, int lds, hipStream_t s) {
+    const void *k = reinterpret_cast<const void *>(mix_trace_kernel<RE, C>);
     hipError_t e = allow_full_lds(k);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(mix_trace_kernel<RE>, dim3(grid), dim3(kTileThreads), lds, s, a, rounds);
+    hipLaunchKernelGGL((mix_trace_kernel<RE, C>), dim3(grid), dim3(kTileThreads), lds, s, a,
+                       rounds);
     return hipGetLastError();
+}
+
+template <int RE>
+hipError_t launch_re(const TileArgs &a, int chunks, int rounds, int grid, int lds,
+                     hipStream_t s) {
+    switch (chunks) {
+        case 1: return launch_rc<RE, 1>(a, rounds, grid, lds, s);
+        case 2: return launch_rc<RE, 2>(a, rounds, grid, lds, s);
+        case 4: return launch_rc<RE, 4>(a, rounds, grid, lds, s);
+        default: return hipErrorInvalidValue;
+    }
 }
 
 }  // namespace
 
-hipError_t launch_mix_trace(const TileArgs &a, int rounds, int grid, int lds, float *trace_out,
-                            hipStream_t s) {
+hipError_t launch_mix_trace(const TileArgs &a, int chunks, int rounds, int grid, int lds,
+                            float *trace_out, hipStream_t s) {
+    if (rounds < 1 || rounds > kTraceRounds) return hipErrorInvalidValue;
     const bool in_regs = a.regular == 5 && a.n_w == 5;
-    hipError_t e = in_regs ? launch_re<5>(a, rounds, grid, lds, s)
-                           : launch_re<0>(a, rounds, grid, lds, s);
+    hipError_t e = in_regs ? launch_re<5>(a, chunks, rounds, grid, lds, s)
+                           : launch_re<0>(a, chunks, rounds, grid, lds, s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(trace_reduce_kernel, dim3(rounds), dim3(1024), 0, s, a.dev_partial, grid,
                        rounds, a.n_rows, trace_out);

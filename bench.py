@@ -25,7 +25,8 @@ Other BASELINE configs (not the headline line; run on request):
       is the synchronous numpy restatement.  Latency-bound by design (7 params per agent).
   c2-gossip  pure gossip averaging as Mixer.mix(times=K) (eps=None): K rounds per HBM pass on
       LDS-resident column tiles (dl_mix_rounds); rounds/s counts every round.  N>1: column
-      stripes, no exchange.
+      stripes, no exchange.  --trace: Mixer.mix(times, eps) as passes of K <= 32 rounds that
+      also return the K per-round max deviations (dl_mix_rounds_trace), read back every pass.
   c5  Wide-ResNet-16-4 consensus SGD, 64 agents x 2,751,146 params, B=64 synthetic CIFAR-shaped
       batches: per-agent PyTorch-ROCm (MIOpen) forward/backward into G's rows, dl_sgd_step
       (SGD momentum 0.9, wd 5e-4) and the fused round, one hipGraph per step.
@@ -113,8 +114,8 @@ def build_graph(n, kind="rr4"):
 def copy_ceiling(dev, nbytes=4 << 30, reps=10):
     """Measured HBM ceilings (libdlamd dl_stream_copy) over 4 GiB streams: float4 copies
     (variants 0-3, read + write bytes) and the triad y = x - lr g (variants 4-6: two reads, one
-    write -- the fused round's own traffic, 12 B per element; 6 in the round's access shape).  Returns (best copy GB/s, best
-    triad GB/s, per-variant GB/s)."""
+    write -- the fused round's own traffic, 12 B per element; 6 in the round's access shape).
+    Returns (best copy GB/s, best triad GB/s, per-variant GB/s)."""
     from distributed_learning_amd import _lib
     lib = _lib.load()
     a = torch.zeros(2 * nbytes // 4, dtype=torch.float32, device=dev)
@@ -433,7 +434,7 @@ def run_c4(args, dev, rank, world):
         shard = sharding.HaloShard(rp, P, dev, sharding.dist_transport(), chunk_cols=P // 8,
                                    n_agents_total=n)
         shard.X.normal_(generator=gen)
-        G = torch.randn(rp.n_local, P, device=dev, generator=gen)
+        G = engine.staggered_zeros((rp.n_local, P), 2, dev).normal_(generator=gen)
         halo_rows = rp.n_halo
         plan = {"path": "halo", "n_local": rp.n_local, "n_halo": rp.n_halo,
                 "peers": sorted(rp.halo_from)}

@@ -349,8 +349,10 @@ class HaloShard:
         self.chunk = int(chunk_cols or self.P)
         self.send_rows = {q: torch.as_tensor(rows.astype(np.int32), device=self.device)
                           for q, rows in plan.send_to.items()}
-        self.X = torch.zeros(plan.n_local, self.P, device=self.device)
-        self.Y = torch.empty_like(self.X)
+        # X, Y (and the caller's G) stream together: staggered so they do not alias in HBM
+        from .engine import staggered_zeros
+        self.X = staggered_zeros((plan.n_local, self.P), 0, self.device)
+        self.Y = staggered_zeros((plan.n_local, self.P), 1, self.device)
         self._bufs = {}
 
     def _buffers(self, slot, width):

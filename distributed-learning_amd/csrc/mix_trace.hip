@@ -28,9 +28,12 @@ __device__ __forceinline__ float4 tr_load4(const char *p) {
     return make_float4(v.x, v.y, v.z, v.w);
 }
 
+// Plain (write-back) stores: a lane writes its agent's C chunks with C instructions, each one
+// 16 B per lane at the agent stride, so every instruction covers only part of each line.
+// Through L2 the C partial writes of a line merge before it is written back; non-temporal
+// stores sent them to HBM as partial-line writes (WRITE_SIZE 2.8x the bytes, profiles/r05/trace).
 __device__ __forceinline__ void tr_store4(float4 v, char *p) {
-    f32x4 x = {v.x, v.y, v.z, v.w};
-    __builtin_nontemporal_store(x, reinterpret_cast<f32x4 *>(p));
+    *reinterpret_cast<float4 *>(p) = v;
 }
 
 // RE > 0: regular graph of RE entries per row sharing row 0's weights, CSR in registers.

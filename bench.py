@@ -744,10 +744,13 @@ def run_gossip(args, dev, rank, world):
     order, conflicts = None, None
     if args.relabel > 0:
         from distributed_learning_amd.graph import lds_slot_order
-        T = engine.plan_shape(engine.DeviceCsr(csr, dev), P, deviation=True,
-                              tile_cols=-1)["tile_cols"]
+        # the bank slot of a neighbour read depends on the image layout: mix_multi_kernel keeps
+        # agent-major rows of T/4 chunks (lane = row * chunks + chunk), mix_trace_kernel
+        # chunk-major planes with one agent per lane (the slot order of chunks = 1)
+        chunks = 1 if args.trace else engine.plan_shape(
+            engine.DeviceCsr(csr, dev), P, deviation=True, tile_cols=-1)["tile_cols"] // 4
         t0 = time.perf_counter()
-        order, c0, c1 = lds_slot_order(csr, T // 4, moves=args.relabel)
+        order, c0, c1 = lds_slot_order(csr, chunks, moves=args.relabel)
         conflicts = {"before": c0, "after": c1, "search_s": time.perf_counter() - t0}
         log(f"c2-gossip: LDS slot order, bank conflicts {c0} -> {c1}")
     eng = engine.GossipEngine(csr, P, device=dev, X=torch.randn(n, P, device=dev, generator=g),

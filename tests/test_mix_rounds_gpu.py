@@ -168,3 +168,31 @@ def test_lds_slot_order_is_transparent(cuda):
     torch.cuda.synchronize()
     assert torch.equal(a.rows(), b.rows())
     torch.testing.assert_close(a.agent_dev_sq(), b.agent_dev_sq(), rtol=1e-5, atol=0)
+
+
+def test_lds_slot_order_traced_is_transparent(cuda):
+    """The traced pass (chunk-major images, one agent per lane) under its own slot order
+    (lds_slot_order with chunks = 1): same bits per agent as the agent-order engine, and the
+    same per-round max deviations up to the mean's summation order."""
+    from distributed_learning_amd.graph import (best_constant_weight, lds_conflicts,
+                                                lds_slot_order, random_regular_edges,
+                                                uniform_weights)
+    E = engine()
+    n, P = 1024, 4096
+    edges = random_regular_edges(4, n, seed=0)
+    csr = uniform_weights(edges, best_constant_weight(edges), list(range(n)))
+    order, c0, c1 = lds_slot_order(csr, 1, moves=20000)
+    assert c1 < c0 and lds_conflicts(csr, 1, order) == c1
+    rng = np.random.default_rng(5)
+    X = torch.from_numpy(rng.standard_normal((n, P), dtype=np.float32)).to(cuda)
+    a = E.GossipEngine(csr, P, device=cuda, X=X)
+    b = E.GossipEngine(csr, P, device=cuda, X=X, order=order)
+    K = min(12, a.trace_max_rounds())
+    assert K >= 1 and b.trace_max_rounds() >= K
+    ta = torch.empty(K, dtype=torch.float32, device=cuda)
+    tb = torch.empty(K, dtype=torch.float32, device=cuda)
+    a.rounds_traced(K, ta)
+    b.rounds_traced(K, tb)
+    torch.cuda.synchronize()
+    assert torch.equal(a.rows(), b.rows())
+    torch.testing.assert_close(ta, tb, rtol=1e-5, atol=1e-6)

@@ -61,7 +61,7 @@ def parse():
     p.add_argument("--graph", default="rr4", choices=["rr4", "circ4", "torus"],
                    help="c2-gossip: agent graph (circ4 = conflict-free control)")
     p.add_argument("--relabel", type=int, default=0,
-                   help="c2-gossip: greedy slot-swap moves of graph.lds_slot_order (0 = agent "
+                   help="c2-gossip: greedy slot-swap moves of graph.lds_slot_order_native (0 = agent "
                         "order); spreads each ds_read_b128 lane group over distinct banks")
     p.add_argument("--rounds", type=int, default=64,
                    help="c2-gossip: rounds per Mixer.mix(times=K) call (one HBM pass)")
@@ -743,14 +743,14 @@ def run_gossip(args, dev, rank, world):
     g = torch.Generator(device=dev).manual_seed(1000 + rank)
     order, conflicts = None, None
     if args.relabel > 0:
-        from distributed_learning_amd.graph import lds_slot_order
+        from distributed_learning_amd.graph import lds_slot_order_native
         # the bank slot of a neighbour read depends on the image layout: mix_multi_kernel keeps
         # agent-major rows of T/4 chunks (lane = row * chunks + chunk), mix_trace_kernel
         # chunk-major planes with one agent per lane (the slot order of chunks = 1)
         chunks = 1 if args.trace else engine.plan_shape(
             engine.DeviceCsr(csr, dev), P, deviation=True, tile_cols=-1)["tile_cols"] // 4
         t0 = time.perf_counter()
-        order, c0, c1 = lds_slot_order(csr, chunks, moves=args.relabel)
+        order, c0, c1 = lds_slot_order_native(csr, chunks, moves=args.relabel)
         conflicts = {"before": c0, "after": c1, "search_s": time.perf_counter() - t0}
         log(f"c2-gossip: LDS slot order, bank conflicts {c0} -> {c1}")
     eng = engine.GossipEngine(csr, P, device=dev, X=torch.randn(n, P, device=dev, generator=g),

@@ -117,6 +117,7 @@ SIGNATURES = {
     "dl_xent_grad": (_i32, [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i32, _i32, _i32, _vp]),
     "dl_perron_workspace_bytes": (_sz, [_i32, _i32, _i64]),
     "dl_perron_round": (_i32, [ctypes.POINTER(DlPerronArgs), _vp, _sz, _vp]),
+    "dl_lds_slot_order": (_i32, [_i32, _i32, _vp, _i32, _i64, ctypes.c_uint64, _vp, _vp]),
 }
 
 ABI_VERSION = 2

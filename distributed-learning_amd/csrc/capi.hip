@@ -463,6 +463,10 @@ int plan_trace(const dl_mix_args *a, TracePlan *tp) {
 
 }  // namespace
 
+namespace dl {
+int fail_msg(int code, const char *msg) { return fail(code, "%s", msg); }
+}  // namespace dl
+
 extern "C" {
 
 int dl_abi_version(void) { return DLAMD_ABI_VERSION; }

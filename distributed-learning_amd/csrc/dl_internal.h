@@ -208,4 +208,8 @@ hipError_t launch_mlp_fused(const float *X, int64_t ldx, const float *data, int6
                             float *loss, int n_agents, int din, int dh, int dout, int tile_cols,
                             hipStream_t s);
 
+// sets dl_last_error()'s message (capi.hip) and returns code: for host-only entry points
+// defined outside capi.hip
+int fail_msg(int code, const char *msg);
+
 }  // namespace dl

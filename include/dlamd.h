@@ -252,6 +252,19 @@ int dl_column_sum(const float *x, int64_t ldx, int32_t n_rows, int64_t n_params,
 int dl_max_column_std(const float *x, int64_t ldx, int32_t n_rows, int64_t n_params, float *out,
                       dl_stream_t stream);
 
+/* Host-only (no device work): agent -> LDS image row-slot order for the multi-round kernels'
+ * neighbour gathers.  col: [n_rows][degree] neighbour agent ids in CSR entry order (the
+ * reference's topology dict order, mixer.py:43-49); chunks: float4 chunks per image row and lane
+ * (4 = dl_mix_rounds' agent-major rows at 16 columns, 1 = dl_mix_rounds_trace's chunk-major
+ * planes).  A greedy random-swap search over `moves` moves (seeded) that lowers the number of
+ * ds_read_b128 16-lane groups' repeated 16-byte bank slots; order[slot] = agent (out, n_rows);
+ * conflicts[0] / [1] = extra LDS cycles per round before / after.  Relabelling keeps every row's
+ * entry order, so the iterates are bit-identical per agent.  Same objective and move rule as
+ * graph.lds_slot_order (Python), with incremental counts.  Not in the reference: it has no
+ * device layout to order. */
+int dl_lds_slot_order(int32_t n_rows, int32_t degree, const int32_t *col, int32_t chunks,
+                      int64_t moves, uint64_t seed, int32_t *order, int64_t *conflicts);
+
 /* out[i, :] = x[rows[i], :] - lr * g[rows[i], :]  (g nullable: plain copy).  Packs the boundary
  * rows a GPU sends to its neighbours in the multi-GPU halo exchange. */
 int dl_step_rows(const float *x, int64_t ldx, const float *g, int64_t ldg, float lr,

@@ -129,3 +129,27 @@ def test_lds_slot_order_permutation_and_csr():
     # neighbours at fixed slot offsets: conflict-free except where agent 0 lists its ring
     # neighbours in the opposite order (edge-list order, agent.py:204-207 restated)
     assert graph.lds_conflicts(ring, 4) <= 2
+
+
+def test_lds_slot_order_native_matches_objective():
+    """dl_lds_slot_order (host C++, no GPU): a permutation whose reported conflicts are
+    graph.lds_conflicts' count for both image layouts, lower than the identity's and at most
+    the Python search's at equal moves; bad arguments raise through dl_last_error."""
+    from distributed_learning_amd import _lib, graph
+    n = 256
+    edges = graph.random_regular_edges(4, n, seed=0)
+    csr = graph.uniform_weights(edges, graph.best_constant_weight(edges), list(range(n)))
+    for chunks in (1, 4):
+        order, c0, c1 = graph.lds_slot_order_native(csr, chunks, moves=200000, seed=3)
+        assert sorted(order.tolist()) == list(range(n))
+        assert c0 == graph.lds_conflicts(csr, chunks)
+        assert c1 == graph.lds_conflicts(csr, chunks, order) and c1 < c0
+        _, p0, p1 = graph.lds_slot_order(csr, chunks, moves=5000, seed=1)
+        assert p0 == c0 and c1 <= p1
+    lib = _lib.load()
+    col = np.zeros(8, np.int32)
+    out = np.empty(2, np.int32)
+    conf = np.zeros(2, np.int64)
+    with pytest.raises(ValueError, match="chunks"):
+        _lib.check(lib.dl_lds_slot_order(2, 4, col.ctypes.data, 3, 10, 0, out.ctypes.data,
+                                         conf.ctypes.data), "dl_lds_slot_order")

@@ -745,9 +745,10 @@ def run_gossip(args, dev, rank, world):
     if args.relabel > 0:
         from distributed_learning_amd.graph import lds_slot_order_native
         # the bank slot of a neighbour read depends on the image layout: mix_multi_kernel keeps
-        # agent-major rows of T/4 chunks (lane = row * chunks + chunk), mix_trace_kernel
-        # chunk-major planes with one agent per lane (the slot order of chunks = 1)
-        chunks = 1 if args.trace else engine.plan_shape(
+        # agent-major rows of T/4 chunks (lane = row * chunks + chunk), as does
+        # mix_trace_rows_kernel; mix_trace_kernel (DLAMD_TRACE_PLANES=1) chunk-major planes with
+        # one agent per lane (the slot order of chunks = 1)
+        chunks = 1 if args.trace and os.environ.get("DLAMD_TRACE_PLANES") else engine.plan_shape(
             engine.DeviceCsr(csr, dev), P, deviation=True, tile_cols=-1)["tile_cols"] // 4
         t0 = time.perf_counter()
         order, c0, c1 = lds_slot_order_native(csr, chunks, moves=args.relabel)

@@ -455,7 +455,7 @@ int plan_trace(const dl_mix_args *a, TracePlan *tp) {
     if (tp->chunks == 0)
         return fail(DL_ERR_UNSUPPORTED, "dl_mix_rounds_trace: two column images of %d agents "
                                         "do not fit LDS", N);
-    tp->max_rounds = dl::kTraceRounds;
+    tp->max_rounds = dl::trace_max_rounds(N, in_regs, tp->chunks);
     tp->n_steps = nq / tp->chunks;
     tp->grid = (int32_t)balanced_grid(tp->n_steps, device_cus());
     return DL_OK;

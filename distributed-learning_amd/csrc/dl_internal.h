@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
+
 namespace dl {
 
 constexpr int kTileThreads = 1024;      // 16 waves: one workgroup per CU owns a column tile
@@ -71,6 +73,19 @@ hipError_t launch_mix_multi(const TileArgs &a, int chunks, int rounds, bool sgd,
 // K rounds on LDS-resident column chunks with the per-round max deviation trace
 // (mix_trace.hip): mix_trace_kernel + trace_reduce into trace_out[rounds]
 constexpr int kTraceRounds = 32;   // rounds per traced pass (per-round deviations in VGPRs)
+// mix_trace_rows_kernel at 4 agents per thread keeps 4 agents' CSR offsets and prefetch
+// registers: its trace depth is capped so the per-round deviations fit VGPRs (122, no spills)
+constexpr int kRowsTraceRounds = 24;
+// the agent-major traced kernel serves register-cached regular graphs at C = 4;
+// DLAMD_TRACE_PLANES=1 keeps the chunk-major planes kernel (comparison runs)
+inline bool trace_uses_rows(int n_rows, bool in_regs, int chunks) {
+    return in_regs && chunks == 4 && n_rows <= kTileThreads &&
+           std::getenv("DLAMD_TRACE_PLANES") == nullptr;
+}
+inline int trace_max_rounds(int n_rows, bool in_regs, int chunks) {
+    return trace_uses_rows(n_rows, in_regs, chunks) && n_rows > kTileThreads / 2 ? kRowsTraceRounds
+                                                                                  : kTraceRounds;
+}
 hipError_t launch_mix_trace(const TileArgs &a, int chunks, int rounds, int grid, int lds,
                             float *trace_out, hipStream_t s);
 // max_zeroed: an earlier launch on the stream already zeroed dev_max (TileArgs::dev_max_zero)

@@ -18,6 +18,8 @@
 // one-round deviation.
 #include "dl_internal.h"
 
+#include <cstdlib>
+
 namespace dl {
 namespace {
 
@@ -34,6 +36,16 @@ __device__ __forceinline__ float4 tr_load4(const char *p) {
 // stores sent them to HBM as partial-line writes (WRITE_SIZE 2.8x the bytes, profiles/r05/trace).
 __device__ __forceinline__ void tr_store4(float4 v, char *p) {
     *reinterpret_cast<float4 *>(p) = v;
+}
+
+// Lane exchange inside a quad as a DPP modifier on a VALU move (quad_perm [1,0,3,2] /
+// [2,3,0,1]): __shfl_xor compiles to ds_bpermute_b32, an LDS instruction, and the traced rows
+// kernel would issue 8 of them per thread per round next to its 24 image accesses.
+__device__ __forceinline__ float quad_xor1(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float quad_xor2(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));
 }
 
 // RE > 0: regular graph of RE entries per row sharing row 0's weights, CSR in registers.
@@ -204,6 +216,146 @@ __global__ void __launch_bounds__(kTileThreads) mix_trace_kernel(TileArgs a, int
     }
 }
 
+// Agent-major variant for register-cached regular graphs (RE = 5) at C = 4: the images are rows
+// [N][4] float4 (64 B per agent, all 16 columns of the step) and lane = (row, chunk) as in
+// mix_multi_kernel: thread (s, c) produces chunk c of agents s + k * 256, k < KV.  A 16-lane
+// ds_read_b128 group then reads 4 neighbour rows x 4 chunks, so it is conflict-free when those
+// 4 rows sit on distinct slots mod 4 (graph.lds_slot_order with chunks = 4: a random 4-regular
+// graph of 1024 agents reaches 51 extra cycles per round-tile, against 335 x 4 planes for the
+// chunk-major images at their best order).  Per round the 4 chunk lanes of an agent add their
+// squared deviations with two quad shuffles; lane c keeps agent s + c * 256's trace in dacc.
+template <int KV, int KR>
+__global__ void __launch_bounds__(kTileThreads) mix_trace_rows_kernel(TileArgs a, int rounds) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int C = 4, RE = 5;
+    constexpr int SLOTS = kTileThreads / C;
+    const int tid = threadIdx.x;
+    const int c = tid & (C - 1);
+    const int s = tid / C;
+    const int N = a.n_rows;
+    float4 *img0 = reinterpret_cast<float4 *>(smem);
+    float4 *img1 = img0 + N * C;
+    float4 *scratch = reinterpret_cast<float4 *>(smem + a.scratch_off);   // [16][C]
+    uint32_t coff[KV][RE];
+    float wreg[RE];
+#pragma unroll
+    for (int e = 0; e < RE; ++e) wreg[e] = a.w[e];
+#pragma unroll
+    for (int k = 0; k < KV; ++k) {
+        const int ag = s + k * SLOTS < N ? s + k * SLOTS : 0;
+#pragma unroll
+        for (int e = 0; e < RE; ++e) coff[k][e] = ((uint32_t)a.col[ag * RE + e] * C + c) * 16u;
+    }
+    auto mix = [&](const float4 *src, int k) {
+        const char *base = reinterpret_cast<const char *>(src);
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int e = 0; e < RE; ++e) {
+            const float4 v = *reinterpret_cast<const float4 *>(base + coff[k][e]);
+            const float w = wreg[e];
+            acc.x = acc.x + w * v.x;
+            acc.y = acc.y + w * v.y;
+            acc.z = acc.z + w * v.z;
+            acc.w = acc.w + w * v.w;
+        }
+        return acc;
+    };
+    const int lsh = __builtin_ctz((unsigned)a.lchunks);
+    const int64_t lmask = (int64_t)a.lchunks - 1;
+    auto off = [&](int64_t ts, int64_t row, int64_t q) {
+        return (q >> lsh) * ts + row + (q & lmask) * 16;
+    };
+    const char *xb = reinterpret_cast<const char *>(a.x);
+    char *yb = reinterpret_cast<char *>(a.y);
+    const int64_t nsteps = a.n_tiles;
+    float dacc[KR];
+#pragma unroll
+    for (int r = 0; r < KR; ++r) dacc[r] = 0.f;
+    float4 px[KV];
+    auto prefetch = [&](int64_t q) {
+#pragma unroll
+        for (int k = 0; k < KV; ++k) {
+            const int ag = s + k * SLOTS < N ? s + k * SLOTS : 0;   // ragged: re-read row 0
+            px[k] = tr_load4(xb + off(a.xts, (int64_t)ag * a.xrs, q * C + c));
+        }
+    };
+    int64_t q = blockIdx.x;
+    if (q < nsteps) prefetch(q);
+    for (; q < nsteps; q += gridDim.x) {
+        float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int k = 0; k < KV; ++k) {
+            const int ag = s + k * SLOTS;
+            if (ag < N) {
+                img0[ag * C + c] = px[k];
+                cs.x += px[k].x;
+                cs.y += px[k].y;
+                cs.z += px[k].z;
+                cs.w += px[k].w;
+            }
+        }
+#pragma unroll
+        for (int m = C; m < 64; m <<= 1) {
+            cs.x += __shfl_xor(cs.x, m);
+            cs.y += __shfl_xor(cs.y, m);
+            cs.z += __shfl_xor(cs.z, m);
+            cs.w += __shfl_xor(cs.w, m);
+        }
+        if ((tid & 63) < C) scratch[(tid >> 6) * C + (tid & 63)] = cs;
+        __syncthreads();
+        float4 mean = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 2
+        for (int wv = 0; wv < kTileThreads / 64; ++wv) {
+            const float4 p = scratch[wv * C + c];
+            mean.x += p.x;
+            mean.y += p.y;
+            mean.z += p.z;
+            mean.w += p.w;
+        }
+        const float n = (float)N;
+        mean = make_float4(mean.x / n, mean.y / n, mean.z / n, mean.w / n);
+        if (q + gridDim.x < nsteps) prefetch(q + gridDim.x);   // lands during the rounds
+        const float4 *src = img0;
+        float4 *dst = img1;
+#pragma unroll
+        for (int r = 0; r < KR; ++r) {
+            if (r < rounds) {
+                float own = 0.f;
+#pragma unroll
+                for (int k = 0; k < KV; ++k) {
+                    const int ag = s + k * SLOTS;
+                    float v = 0.f;
+                    if (ag < N) {
+                        const float4 y = mix(src, k);
+                        if (r + 1 < rounds)
+                            dst[ag * C + c] = y;
+                        else
+                            tr_store4(y, yb + off(a.yts, (int64_t)ag * a.yrs, q * C + c));
+                        const float dx = y.x - mean.x, dy = y.y - mean.y;
+                        const float dz = y.z - mean.z, dw = y.w - mean.w;
+                        v = (dx * dx + dy * dy) + (dz * dz + dw * dw);
+                    }
+                    v += quad_xor1(v);   // the agent's 4 chunk lanes (whole wave active)
+                    v += quad_xor2(v);
+                    own += k == c ? v : 0.f;
+                    __builtin_amdgcn_sched_barrier(0);   // one output row at a time (VGPRs)
+                }
+                dacc[r] += own;
+                __syncthreads();   // dst complete before it is read; img0/scratch reuse
+                const float4 *t = src;
+                src = dst;
+                dst = const_cast<float4 *>(t);
+            }
+        }
+    }
+    const int mine_ag = s + c * SLOTS;
+    if (c < KV && mine_ag < N) {
+#pragma unroll
+        for (int r = 0; r < KR; ++r)
+            if (r < rounds) a.dev_partial[((int64_t)blockIdx.x * rounds + r) * N + mine_ag] = dacc[r];
+    }
+}
+
 // out[r] = max_a sqrt(sum_b partial[b][r][a]) (fp64 sum in workgroup order, then float, as
 // dev_reduce's dev_sq); one workgroup per round.
 __global__ void __launch_bounds__(1024) trace_reduce_kernel(const float *__restrict__ partial,
@@ -253,10 +405,29 @@ hipError_t launch_re(const TileArgs &a, int chunks, int rounds, int grid, int ld
 
 hipError_t launch_mix_trace(const TileArgs &a, int chunks, int rounds, int grid, int lds,
                             float *trace_out, hipStream_t s) {
-    if (rounds < 1 || rounds > kTraceRounds) return hipErrorInvalidValue;
     const bool in_regs = a.regular == 5 && a.n_w == 5;
-    hipError_t e = in_regs ? launch_re<5>(a, chunks, rounds, grid, lds, s)
-                           : launch_re<0>(a, chunks, rounds, grid, lds, s);
+    if (rounds < 1 || rounds > trace_max_rounds(a.n_rows, in_regs, chunks))
+        return hipErrorInvalidValue;
+    hipError_t e;
+    if (trace_uses_rows(a.n_rows, in_regs, chunks)) {
+        // agent-major rows (mix_trace_rows_kernel); DLAMD_TRACE_PLANES=1 keeps the chunk-major
+        // planes for comparison
+        const void *k = a.n_rows <= 256   ? reinterpret_cast<const void *>(mix_trace_rows_kernel<1, kTraceRounds>)
+                        : a.n_rows <= 512 ? reinterpret_cast<const void *>(mix_trace_rows_kernel<2, kTraceRounds>)
+                                          : reinterpret_cast<const void *>(mix_trace_rows_kernel<4, kRowsTraceRounds>);
+        e = allow_full_lds(k);
+        if (e != hipSuccess) return e;
+        if (a.n_rows <= 256)
+            hipLaunchKernelGGL((mix_trace_rows_kernel<1, kTraceRounds>), dim3(grid), dim3(kTileThreads), lds, s, a, rounds);
+        else if (a.n_rows <= 512)
+            hipLaunchKernelGGL((mix_trace_rows_kernel<2, kTraceRounds>), dim3(grid), dim3(kTileThreads), lds, s, a, rounds);
+        else
+            hipLaunchKernelGGL((mix_trace_rows_kernel<4, kRowsTraceRounds>), dim3(grid), dim3(kTileThreads), lds, s, a, rounds);
+        e = hipGetLastError();
+    } else {
+        e = in_regs ? launch_re<5>(a, chunks, rounds, grid, lds, s)
+                    : launch_re<0>(a, chunks, rounds, grid, lds, s);
+    }
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(trace_reduce_kernel, dim3(rounds), dim3(1024), 0, s, a.dev_partial, grid,
                        rounds, a.n_rows, trace_out);

@@ -52,8 +52,10 @@ def noise_floor(X):
     return 8 * np.sqrt(X.shape[1]) * np.finfo(np.float32).eps * np.abs(X.mean(axis=0)).max()
 
 
+# rr4 rows run mix_trace_rows_kernel (4 / 2 / 1 agents per thread at 1024 / 300 / 64 agents,
+# ragged at 300); metropolis rows (irregular) the chunk-major planes kernel
 CASES = [("rr4", 64, 4096, 0), ("rr4", 1024, 256, 1), ("metro", 50, 1000, 2),
-         ("metro", 7, 4, 3), ("rr4", 16, 65536, 4)]
+         ("metro", 7, 4, 3), ("rr4", 16, 65536, 4), ("rr4", 300, 512, 5), ("rr4", 1000, 128, 6)]
 
 
 def make(kind, n, seed):
@@ -92,6 +94,27 @@ def test_trace_pass_matches_round_by_round(cuda, kind, n, P, seed, layout):
         ref.append(M.deviation(Z).max())
     assert np.array_equal(bits(got), bits(Z))
     np.testing.assert_allclose(trace.cpu().numpy(), ref, rtol=1e-5, atol=noise_floor(X))
+
+
+@pytest.mark.parametrize("n", [1024, 300])
+def test_trace_rows_and_planes_kernels_agree(cuda, monkeypatch, n):
+    """The agent-major kernel (default for register-cached regular graphs) and the chunk-major
+    planes kernel (DLAMD_TRACE_PLANES=1) give the same bits and traces within rounding."""
+    e = E()
+    csr = rr_csr(n, 7)
+    X = torch.from_numpy(np.random.default_rng(7).standard_normal((n, 1024), dtype=np.float32)).to(cuda)
+    W = e.DeviceCsr(csr, cuda)
+    out = {}
+    for planes in (False, True):
+        if planes:
+            monkeypatch.setenv("DLAMD_TRACE_PLANES", "1")
+        Y = torch.full_like(X, float("nan"))
+        K = min(e.trace_max_rounds(W, X, Y), 20)
+        tr = torch.empty(K, device=cuda)
+        e.mix_rounds_trace(W, X, Y, K, tr)
+        out[planes] = (Y.cpu(), tr.cpu())
+    assert torch.equal(out[False][0], out[True][0])
+    torch.testing.assert_close(out[False][1], out[True][1], rtol=1e-5, atol=1e-6)
 
 
 def test_trace_plan_rejects_unsupported(cuda):

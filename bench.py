@@ -60,9 +60,10 @@ def parse():
                    choices=["c1", "c2", "c2-mix", "c2-gossip", "c3", "c4", "c5"])
     p.add_argument("--graph", default="rr4", choices=["rr4", "circ4", "torus"],
                    help="c2-gossip: agent graph (circ4 = conflict-free control)")
-    p.add_argument("--relabel", type=int, default=0,
+    p.add_argument("--relabel", type=int, default=2_000_000,
                    help="c2-gossip: greedy slot-swap moves of graph.lds_slot_order_native (0 = agent "
-                        "order); spreads each ds_read_b128 lane group over distinct banks")
+                        "order; the default takes ~0.5 s on the host); spreads each ds_read_b128 "
+                        "lane group over distinct banks")
     p.add_argument("--rounds", type=int, default=64,
                    help="c2-gossip: rounds per Mixer.mix(times=K) call (one HBM pass)")
     p.add_argument("--agents", type=int, default=1024)

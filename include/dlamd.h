@@ -151,8 +151,9 @@ int dl_mix_rounds(const dl_mix_args *args, int32_t rounds, void *workspace, size
  * modified).  Rounds are the dl_mix_round fold (bit-identical).  The mean is the column mean of
  * x: W must be doubly stochastic (mean(W x) = mean(x)).  One agent per thread: 2 <= n_rows <=
  * 1024; no halo rows; g must be NULL; n_params % 4 == 0; 16-byte aligned operands, row-major
- * or column-tiled (tile_cols).  dl_mix_trace_plan gives the most rounds one pass can trace (32:
- * each thread keeps its agent's per-round deviations in registers) or DL_ERR_UNSUPPORTED (two
+ * or column-tiled (tile_cols).  dl_mix_trace_plan gives the most rounds one pass can trace (32,
+ * or 24 for > 512 agents of a register-cached regular graph: the per-round deviations live in
+ * registers) or DL_ERR_UNSUPPORTED (two
  * column images of all agents must fit LDS).
  * Workspace: dl_mix_trace_workspace_bytes(n_rows, rounds). */
 int dl_mix_trace_plan(const dl_mix_args *args, int32_t *max_rounds);

@@ -338,7 +338,6 @@ __global__ void __launch_bounds__(kTileThreads) mix_trace_rows_kernel(TileArgs a
                     v += quad_xor1(v);   // the agent's 4 chunk lanes (whole wave active)
                     v += quad_xor2(v);
                     own += k == c ? v : 0.f;
-                    __builtin_amdgcn_sched_barrier(0);   // one output row at a time (VGPRs)
                 }
                 dacc[r] += own;
                 __syncthreads();   // dst complete before it is read; img0/scratch reuse

@@ -23,7 +23,7 @@ import numpy as np
 import torch
 
 from ... import engine as _engine
-from ...graph import from_topology
+from ...graph import from_topology, lds_slot_order_native, permuted
 
 __all__ = ["Mixer", "basic_deviation_metric"]
 
@@ -51,6 +51,7 @@ class Mixer(object):
         self._device = torch.device(device) if device is not None else None
         self._ws = None
         self._csr = None   # (host Csr, DeviceCsr) of the last topology seen
+        self._ordered = None   # (host Csr, DeviceCsr in LDS slot order, agents in slot order)
 
     # ------------------------------------------------------------------ public API (:18-38)
     def mix(self, times=1, eps=None):
@@ -62,7 +63,14 @@ class Mixer(object):
         with torch.no_grad():
             times_done = 0
             W = self._device_csr()
-            X = self._flatten_all()
+            agents = None
+            if eps is None and times >= 1 and not (
+                    not self._custom_metric and _engine.until_fits(W, self._n_params())):
+                # mix(times) with no stop test on a large X: the rows go into the device matrix
+                # in an LDS slot order (every agent keeps its CSR entry order, so its bits are
+                # the same; the multi-round pass gathers neighbours with fewer bank conflicts)
+                W, agents = self._ordered_csr()
+            X = self._flatten_all(agents)
             if not self._custom_metric and _engine.until_fits(W, X.shape[1]):
                 times_done = self._mix_resident(W, X, times, eps)
                 self._write_back(X)
@@ -94,7 +102,7 @@ class Mixer(object):
                 stopping_criterion = self._update_stopping_criterion(
                     X, times_done, times, eps, fused=(dev_max if fused_dev else None))
 
-            self._write_back(X)
+            self._write_back(X, agents)
 
         self.logger.debug('Mixer finished with {} times'.format(times_done))
         return times_done
@@ -221,6 +229,25 @@ class Mixer(object):
         self._csr = (csr, _engine.DeviceCsr(csr, self._dev()))
         return self._csr[1]
 
+    _SLOT_MOVES_PER_AGENT = 2000   # slot-order search moves (1024 agents: ~0.5 s, once)
+
+    def _ordered_csr(self):
+        """(DeviceCsr, agents) with the rows in dl_lds_slot_order's order for the multi-round
+        kernel's agent-major images (4 chunks per row), recomputed only when the topology
+        changes; agents[slot] is the topology key of row slot."""
+        self._device_csr()
+        csr = self._csr[0]
+        if self._ordered is None or self._ordered[0] is not csr:
+            keys = list(self.topology)
+            order, _, _ = lds_slot_order_native(csr, 4,
+                                                moves=self._SLOT_MOVES_PER_AGENT * csr.n_rows)
+            self._ordered = (csr, _engine.DeviceCsr(permuted(csr, order), self._dev()),
+                             [keys[a] for a in order])
+        return self._ordered[1], self._ordered[2]
+
+    def _n_params(self):
+        return sum(p.numel() for p in self.models[next(iter(self.topology))].parameters())
+
     def _dev(self):
         if self._device is None:
             self._device = _default_device()
@@ -231,12 +258,12 @@ class Mixer(object):
             self._ws = _engine.Workspace(self._dev())
         return self._ws
 
-    def _flatten_all(self):
-        """X[N, P], rows in topology order: one concatenation of every parameter of every
-        model (mixer.py:26/68-69)."""
+    def _flatten_all(self, agents=None):
+        """X[N, P], rows in topology order (or in ``agents`` order): one concatenation of every
+        parameter of every model (mixer.py:26/68-69)."""
         dev = self._dev()
         parts, sizes = [], []
-        for agent in self.topology:
+        for agent in (self.topology if agents is None else agents):
             n = 0
             for p in self.models[agent].parameters():
                 parts.append(p.data.to(device=dev, dtype=torch.float32).view(-1))
@@ -260,10 +287,11 @@ class Mixer(object):
             p.data.copy_(params[used_params:used_params + cnt_params].view(p.shape).to(p.dtype))
             used_params += cnt_params
 
-    def _write_back(self, X):
-        """mixer.py:34-35 / 71-76 for every model, as one fused multi-tensor copy."""
+    def _write_back(self, X, agents=None):
+        """mixer.py:34-35 / 71-76 for every model, as one fused multi-tensor copy (row i belongs
+        to agents[i], topology order by default)."""
         dst, src = [], []
-        for i, agent in enumerate(self.topology):
+        for i, agent in enumerate(self.topology if agents is None else agents):
             used = 0
             for p in self.models[agent].parameters():
                 n = p.numel()

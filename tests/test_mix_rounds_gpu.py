@@ -196,3 +196,38 @@ def test_lds_slot_order_traced_is_transparent(cuda):
     torch.cuda.synchronize()
     assert torch.equal(a.rows(), b.rows())
     torch.testing.assert_close(ta, tb, rtol=1e-5, atol=1e-6)
+
+
+def test_mixer_times_slot_order_bits(cuda):
+    """Mixer.mix(times=K), eps=None, on 64 agents of a random 4-regular graph: the rows go to
+    the device in dl_lds_slot_order's order (not the identity here) and every model ends with
+    the reference fold's bits; a second call reuses the cached order."""
+    import logging
+
+    from test_mix_trace_gpu import rr_csr
+
+    from distributed_learning_amd.networks import ANNModel
+    from distributed_learning_amd.utils.consensus_simple import Mixer
+    torch.manual_seed(2)
+    n = 64
+    keys = [f"agent{i}" for i in range(n)]
+    csr = rr_csr(n, 9)
+    topo = {}
+    for i, k in enumerate(keys):
+        topo[k] = {keys[csr.col[e]]: float(csr.w[e]) for e in range(csr.rowptr[i], csr.rowptr[i + 1])}
+    models = {k: ANNModel(60, 40, 10).to(cuda) for k in keys}
+    X0 = np.stack([torch.cat([p.data.reshape(-1) for p in models[k].parameters()]).cpu().numpy()
+                   for k in keys])
+    rp, cl, w = M.topology_to_csr(topo)
+    want = X0
+    for _ in range(7 + 3):
+        want = M.mix_once(want, rp, cl, w)
+    mixer = Mixer(models, topo, logging.getLogger("t"))
+    assert mixer.mix(times=7) == 7
+    ordered = mixer._ordered
+    assert ordered is not None and ordered[2] != keys
+    assert mixer.mix(times=3) == 3
+    assert mixer._ordered is ordered
+    got = np.stack([torch.cat([p.data.reshape(-1) for p in models[k].parameters()]).cpu().numpy()
+                    for k in keys])
+    assert np.array_equal(bits(got), bits(want))

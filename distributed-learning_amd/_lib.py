@@ -58,6 +58,21 @@ class DlPerronArgs(ctypes.Structure):
                 ("conv_eps_rows", _vp)]
 
 
+DL_ASYNC_MAX_NBRS = 64
+
+
+class DlAsyncLoadArgs(ctypes.Structure):
+    _fields_ = [("arena", _vp), ("ld", _i64), ("n_params", _i64), ("slot", _i32), ("mode", _i32),
+                ("src", _vp), ("weight", _f64), ("mean_weight", _f64)]
+
+
+class DlAsyncUpdateArgs(ctypes.Structure):
+    _fields_ = [("arena", _vp), ("ld", _i64), ("n_params", _i64), ("self_slot", _i32),
+                ("out_slot", _i32), ("n_nbrs", _i32), ("nbr_slots", _i32 * DL_ASYNC_MAX_NBRS),
+                ("sum_f32", _i32), ("keep", _f64), ("eps", _f64), ("conv_eps", _f64),
+                ("flags", _vp), ("parity", _i32)]
+
+
 class DlBgemmArgs(ctypes.Structure):
     _fields_ = [("batch", _i32), ("M", _i32), ("N", _i32), ("K", _i32),
                 ("A", _vp), ("lda", _i64), ("sA", _i64), ("ta", _i32),
@@ -117,10 +132,13 @@ SIGNATURES = {
     "dl_xent_grad": (_i32, [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i32, _i32, _i32, _vp]),
     "dl_perron_workspace_bytes": (_sz, [_i32, _i32, _i64]),
     "dl_perron_round": (_i32, [ctypes.POINTER(DlPerronArgs), _vp, _sz, _vp]),
+    "dl_async_load": (_i32, [ctypes.POINTER(DlAsyncLoadArgs), _vp]),
+    "dl_async_update": (_i32, [ctypes.POINTER(DlAsyncUpdateArgs), ctypes.POINTER(_i32), _vp]),
+    "dl_async_read": (_i32, [_vp, _i64, _i32, _i64, _vp, _vp]),
     "dl_lds_slot_order": (_i32, [_i32, _i32, _vp, _i32, _i64, ctypes.c_uint64, _vp, _vp]),
 }
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 _lib = None
 
 

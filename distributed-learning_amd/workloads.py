@@ -38,17 +38,21 @@ async def _learning_instance(X, y, agent, iterations, alpha, tau, schedule):
 
 
 async def consensus_gd(topology, X, y, iterations, alpha=1e-1, tau=1e-4, convergence_eps=1e-10,
-                       schedule="sqrt", device=None):
-    """``run`` of the notebook (cell 14) without plots.  Returns {token: final w}."""
+                       schedule="sqrt", device=None, consensus="reference"):
+    """``run`` of the notebook (cell 14) without plots: the learning tasks are created first and
+    the master's ``serve`` after them, as the notebook does.  ``consensus`` picks the façade's
+    schedule ("reference": the reference's own message interleaving, each agent step on the
+    device; "synchronous": one Jacobi launch per round).  Returns {token: final w}."""
     shutdown = asyncio.Queue()
-    net = ca.ConsensusNetwork(topology, shutdown, device=device)
+    net = ca.ConsensusNetwork(topology, shutdown, device=device, schedule=consensus)
     agents = [ca.ConsensusAgent(t, convergence_eps=convergence_eps) for t in net.tokens]
     for a in agents:
         net.register_agent(a)
     shards = split_data(X, y, net.tokens)
+    tasks = [asyncio.create_task(_learning_instance(*shards[a.token], a, iterations, alpha, tau,
+                                                    schedule)) for a in agents]
     serve = asyncio.create_task(net.serve())
-    res = await asyncio.gather(*[_learning_instance(*shards[a.token], a, iterations, alpha, tau,
-                                                    schedule) for a in agents])
+    res = await asyncio.gather(*tasks)
     await shutdown.put(ca.SHUTDOWN)
     await serve
     return {a.token: w for a, w in zip(agents, res)}

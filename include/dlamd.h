@@ -11,6 +11,10 @@
  *   dl_deviation        <- Mixer._get_deviation_dict / _get_max_deviation   mixer.py:51-66
  *   dl_max_column_std   <- Mixer.get_max_parameters_std                     mixer.py:82-84
  *   dl_perron_round     <- ConsensusAgent.run_round mixing loop             consensus_asyncio.py:231-310
+ *                          (synchronous Jacobi form: every agent at the same iteration)
+ *   dl_async_load / dl_async_update / dl_async_read
+ *                       <- ConsensusAgent.run_round's per-agent arithmetic under the reference's
+ *                          own message schedule: pre-scale :231, step :295, verdict :297
  *   dl_step_rows        <- (multi-GPU) boundary rows x - lr*g packed for the halo exchange that
  *                          replaces the per-neighbour value messages of consensus_asyncio.py:236-284
  *   dl_column_sum       <- the np.mean numerator of mixer.py:61 (multi-GPU global mean)
@@ -43,7 +47,7 @@
 extern "C" {
 #endif
 
-#define DLAMD_ABI_VERSION 2
+#define DLAMD_ABI_VERSION 3
 
 typedef void *dl_stream_t; /* hipStream_t; NULL = the legacy default stream */
 
@@ -337,6 +341,66 @@ typedef struct dl_perron_args {
 size_t dl_perron_workspace_bytes(int32_t dtype, int32_t n_rows, int64_t n_params);
 int dl_perron_round(const dl_perron_args *args, void *workspace, size_t ws_bytes,
                     dl_stream_t stream);
+
+/* ---------------------------------------------------------------- asyncio message schedule
+ * The reference's asyncio round is NOT synchronous Jacobi after the first round: each agent
+ * answers REQUEST_VALUE with whatever iterate it holds when the request is served, drops
+ * other-round messages (consensus_asyncio.py:276-278) and sees DONE only between exchanges
+ * (:241-252, :260-265), so an agent may mix a neighbour's iterate t+1 or t-2 into its own step
+ * t, and agents stop at different iteration counts.  The host façade
+ * (utils/consensus_asyncio.py) replays that message protocol on asyncio exactly and sends every
+ * arithmetic step here.  Iterates live in a caller-owned device arena of fp64 slots
+ * ([n_slots][ld]); a message carries a slot index, as the reference's carries its numpy array.
+ *
+ * dl_async_load: y0 = v * weight / mean_weight (:231) into `slot`.  `src` is HOST memory holding
+ *   n_params doubles (the caller converts fp32/int values exactly).  mode 0: numpy computes in
+ *   fp64 (fp64 values, or a strong fp64/int64 weight); mode 1: in fp32 (fp32 values with Python
+ *   scalar weights, NEP 50) -- weight and mean_weight already rounded to fp32 by the caller.
+ *   Stream-ordered; the pageable host copy is consumed before return.
+ * dl_async_update: one agent step (:295, :297)
+ *     y' = y * keep + eps * S,  S = np.sum([v_0 .. v_{d-1}], axis=0) in arrival order,
+ *     converged = all_j all_p ((y' - v_j) <= conv_eps)
+ *   keep = 1 - eps*deg (np.float64, computed by the caller), each product and sum rounded
+ *   separately.  S follows numpy's reduction exactly: a left fold from +0.0 when n_params > 1;
+ *   for n_params == 1 numpy's pairwise sum (8 accumulators once d >= 8); in fp32 when every v_j
+ *   is an fp32 pre-scaled value (sum_f32 = 1), else in fp64.  `flags` is a device int32[2]
+ *   (zeroed once by the caller): the launch ORs violations into flags[parity] and zeroes
+ *   flags[parity ^ 1] for the next launch.  converged_host (nullable): when set, the call copies
+ *   the verdict there and SYNCHRONISES the stream (the protocol needs it before the agent's next
+ *   message, :301-310).
+ * dl_async_read: copies n_params doubles of `slot` to host memory and synchronises the stream. */
+#define DL_ASYNC_MAX_NBRS 64
+typedef struct dl_async_load_args {
+    double *arena;            /* [n_slots][ld] */
+    int64_t ld;
+    int64_t n_params;
+    int32_t slot;
+    int32_t mode;             /* 0 = fp64, 1 = fp32 */
+    const double *src;        /* host [n_params] */
+    double weight;
+    double mean_weight;
+} dl_async_load_args;
+int dl_async_load(const dl_async_load_args *args, dl_stream_t stream);
+
+typedef struct dl_async_update_args {
+    double *arena;            /* [n_slots][ld] */
+    int64_t ld;
+    int64_t n_params;
+    int32_t self_slot;        /* the agent's current iterate y */
+    int32_t out_slot;         /* receives y' (must differ from every input slot) */
+    int32_t n_nbrs;           /* <= DL_ASYNC_MAX_NBRS, in arrival order */
+    int32_t nbr_slots[DL_ASYNC_MAX_NBRS];
+    int32_t sum_f32;
+    double keep;
+    double eps;
+    double conv_eps;
+    int32_t *flags;           /* device int32[2] */
+    int32_t parity;
+} dl_async_update_args;
+int dl_async_update(const dl_async_update_args *args, int32_t *converged_host,
+                    dl_stream_t stream);
+int dl_async_read(const double *arena, int64_t ld, int32_t slot, int64_t n_params,
+                  double *host_out, dl_stream_t stream);
 
 /* ---------------------------------------------------------------- batched per-agent GEMMs
  * BASELINE config c3: every agent trains its own ANNModel (networks/ann_model.py:4-45) on its own

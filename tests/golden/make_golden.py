@@ -17,11 +17,17 @@ What is produced (see SURVEY.md §8c for the list this follows):
 * ``asyncio_graphs.npz`` -- ``ConsensusAgent.run_round`` (utils/consensus_asyncio.py:209-312)
   over K4 / ring8 / cycle3 / grid5 / RR4-16 at several convergence eps, plus the mixing
   iteration count k recovered by matching the synchronous Jacobi iterate.
+* ``asyncio_rounds.npz`` -- CONSECUTIVE ``run_round`` calls, where the reference stops being
+  synchronous (stale-round drops :276-278, DONE seen between exchanges :241-265): 6 graphs x
+  4 convergence eps x 4 rounds, vector / scalar / fp32 values, two drivers (new tasks per round;
+  one task per agent looping over rounds with a local update in between, as the notebook's
+  ``learning_instance`` does), plus notebook-style Titanic consensus GD runs at inexact eps.
 * ``titanic.npz``        -- preprocessed Titanic data (notebook cells 2-4), centralised GD
   (cell 5) and ring-8 asyncio consensus GD for 4000 steps at eps=10 (cells 12-14).
 * ``notebook_outputs.json`` -- values the reference notebooks themselves recorded.
 
-Run:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+Run:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [fixture ...]
+(no argument: all fixtures; e.g. ``asyncio_rounds`` regenerates only that file)
 """
 import asyncio
 import hashlib
@@ -266,6 +272,146 @@ def make_asyncio():
     np.savez_compressed(os.path.join(OUT, "asyncio_graphs.npz"), **out)
 
 
+async def _async_multi(topology, values_per_round, weights, conv_eps, driver):
+    """Consecutive rounds under one of two drivers.  'gather': new run_round tasks per round,
+    gathered (make_asyncio's driver).  'loop': one task per agent running every round, feeding
+    round r the value ``0.5 * previous_result + values[r]`` (a local step between rounds, the
+    shape of the notebook's learning_instance)."""
+    shutdown = asyncio.Queue()
+    net = ref_async.ConsensusNetwork(topology, shutdown)
+    agents = [ref_async.ConsensusAgent(t, convergence_eps=conv_eps) for t in net.tokens]
+    for a in agents:
+        net.register_agent(a)
+    if driver == "gather":
+        serve = asyncio.create_task(net.serve())
+        results = []
+        for values in values_per_round:
+            tasks = [asyncio.create_task(a.run_round(values[a.token], weights[a.token]))
+                     for a in agents]
+            res = await asyncio.gather(*tasks)
+            results.append({a.token: r for a, r in zip(agents, res)})
+    else:
+        async def instance(a):
+            outs, w = [], values_per_round[0][a.token]
+            for r in range(len(values_per_round)):
+                w = await a.run_round(w * 0.5 + values_per_round[r][a.token], weights[a.token])
+                outs.append(w)
+            return outs
+        tasks = [asyncio.create_task(instance(a)) for a in agents]
+        serve = asyncio.create_task(net.serve())
+        outs = await asyncio.gather(*tasks)
+        results = [{a.token: outs[i][r] for i, a in enumerate(agents)}
+                   for r in range(len(values_per_round))]
+    await shutdown.put(ref_async.SHUTDOWN)
+    await serve
+    return [int(t) for t in net.tokens], results
+
+
+ASYNC_GRAPHS = {
+    "ring8": [(i, (i + 1) % 8) for i in range(8)],
+    "k4": [(0, 1), (0, 2), (0, 3), (1, 2), (1, 3), (2, 3)],
+    "grid5": [(2, 1), (2, 3), (2, 0), (2, 4), (1, 0), (0, 3), (3, 4), (1, 4)],
+    "star9": [(0, i) for i in range(1, 10)],
+    "path5": [(0, 1), (1, 2), (2, 3), (3, 4)],
+}
+
+
+def make_asyncio_rounds():
+    graphs = dict(ASYNC_GRAPHS)
+    graphs["rr4_16"] = [(int(u), int(v)) for u, v in nx.random_regular_graph(4, 16, seed=0).edges()]
+    rng = np.random.default_rng(11)
+    out, rounds = {}, 4
+    names = []
+    for name, topo in graphs.items():
+        toks = sorted(set(np.array(topo).flatten().tolist()))
+        for ce in (1e-1, 1e-2, 1e-4, 1e-8):
+            for kind in ("vec", "scalar", "f32"):
+                for driver in ("gather", "loop"):
+                    if kind == "f32" and (driver == "loop" or ce < 1e-4):
+                        continue
+                    if kind == "vec":
+                        vals = [{t: rng.standard_normal(7) for t in toks} for _ in range(rounds)]
+                    elif kind == "f32":
+                        vals = [{t: rng.standard_normal(5).astype(np.float32) for t in toks}
+                                for _ in range(rounds)]
+                    else:
+                        vals = [{t: float(rng.standard_normal()) for t in toks}
+                                for _ in range(rounds)]
+                    wts = {t: int(rng.integers(1, 10)) for t in toks}
+                    tokens, res = asyncio.run(_async_multi(topo, vals, wts, ce, driver))
+                    key = f"{name}_{ce:g}_{kind}_{driver}"
+                    names.append(key)
+                    out[key + "_edges"] = np.asarray(topo, np.int64)
+                    out[key + "_conv_eps"] = np.float64(ce)
+                    out[key + "_tokens"] = np.asarray(tokens)
+                    out[key + "_weights"] = np.asarray([wts[t] for t in tokens], np.int64)
+                    out[key + "_values"] = np.stack([np.stack([np.asarray(vals[r][t]) for t in tokens])
+                                                     for r in range(rounds)])
+                    out[key + "_out"] = np.stack([np.stack([np.asarray(res[r][t]) for t in tokens])
+                                                  for r in range(rounds)])
+                    out[key + "_out_is_scalar"] = np.int64(
+                        all(np.ndim(res[r][t]) == 0 for r in range(rounds) for t in tokens))
+    out["cases"] = np.asarray(names)
+    print("asyncio_rounds:", len(names), "cases")
+    out.update(_titanic_async_runs())
+    np.savez_compressed(os.path.join(OUT, "asyncio_rounds.npz"), **out)
+
+
+def _titanic_async_runs(steps=300):
+    """Notebook-style consensus GD (cells 12-14, 22) through the reference agents at inexact
+    convergence eps, where the per-round schedule is asynchronous: final W of every agent."""
+    Xall, yall = _prepare_titanic()
+    nt = Xall.shape[0] // 10
+    X, y = Xall[nt:], yall[nt:]
+    runs = {"tit_grid5_1e-2_sqrt": (ASYNC_GRAPHS["grid5"], 1e-2, "sqrt"),
+            "tit_grid5_1e-4_old": (ASYNC_GRAPHS["grid5"], 1e-4, "old"),
+            "tit_ring8_1e-1_sqrt": (ASYNC_GRAPHS["ring8"], 1e-1, "sqrt")}
+    out = {}
+    for key, (topo, ce, algo) in runs.items():
+        tokens = list(set(np.array(topo).flatten()))
+        shards, tmpX, tmpy = {}, X.copy(), y.copy()
+        for i in range(len(tokens)):
+            ln = len(tmpX) // (len(tokens) - i)
+            shards[tokens[i]] = (tmpX[:ln], tmpy[:ln])
+            tmpX, tmpy = tmpX[ln:], tmpy[ln:]
+
+        async def learning_instance(Xs, ys, agent):
+            alpha, tau = (1e-1, 1e-4) if algo == "sqrt" else (5e-4, 1e-4)
+            w = np.zeros(Xs.shape[1])
+            for it in range(steps):
+                g = _grad(Xs, ys, w, tau)
+                if algo == "sqrt":
+                    w -= alpha * np.power(it + 1, -0.5) * g
+                else:
+                    w -= alpha * g
+                w = await agent.run_round(w, Xs.shape[0])
+                if algo == "old" and it % 2000 == 0:
+                    alpha *= 0.99
+            return w
+
+        async def main():
+            shutdown = asyncio.Queue()
+            net = ref_async.ConsensusNetwork(topo, shutdown)
+            agents = [ref_async.ConsensusAgent(t, convergence_eps=ce) for t in net.tokens]
+            for a in agents:
+                net.register_agent(a)
+            tasks = [asyncio.create_task(learning_instance(*shards[a.token], a)) for a in agents]
+            asyncio.create_task(net.serve())
+            res = await asyncio.gather(*tasks)
+            await shutdown.put(ref_async.SHUTDOWN)
+            return [int(a.token) for a in agents], res
+
+        toks, ws = asyncio.run(main())
+        out[key + "_edges"] = np.asarray(topo, np.int64)
+        out[key + "_tokens"] = np.asarray(toks)
+        out[key + "_conv_eps"] = np.float64(ce)
+        out[key + "_steps"] = np.int64(steps)
+        out[key + "_w"] = np.stack(ws)
+        print(key, "agent0", ws[0])
+    out["titanic_runs"] = np.asarray(list(runs))
+    return out
+
+
 # ---------------------------------------------------------------- Titanic (config 1)
 def _prepare_titanic():
     import pandas as pd
@@ -378,12 +524,11 @@ def make_notebook_outputs():
 
 
 if __name__ == "__main__":
-    make_notebook_outputs()
-    make_mix_rr4()
-    make_ring8_fa()
-    make_mixer_ann()
-    make_asyncio()
-    make_titanic()
+    makers = {"notebook_outputs": make_notebook_outputs, "mix_rr4": make_mix_rr4,
+              "ring8_fa": make_ring8_fa, "mixer_ann": make_mixer_ann, "asyncio": make_asyncio,
+              "asyncio_rounds": make_asyncio_rounds, "titanic": make_titanic}
+    for name in (sys.argv[1:] or list(makers)):
+        makers[name]()
     for fn in sorted(os.listdir(OUT)):
         p = os.path.join(OUT, fn)
         if fn.endswith((".npz", ".json")):

@@ -44,10 +44,61 @@ def test_optimality_certificate(seed):
     np.testing.assert_allclose(W.sum(1), 1, atol=1e-12)
 
 
-def test_vertex_order_self_loops_and_large_fallback():
+def test_vertex_order_self_loops_and_explicit_methods():
     edges = [("b", "a"), ("a", "c"), ("c", "c"), ("c", "b")]
     w, g = find_optimal_weights(edges)
     assert w[2] == 0.0 and g < 1
     ring = [(i, (i + 1) % 500) for i in range(500)]
-    w, g = find_optimal_weights(ring, max_dense=400)          # best-constant fallback
-    assert np.allclose(w, w[0]) and g < 1
+    info = {}
+    w, g = find_optimal_weights(ring, method="best_constant", info=info)
+    assert info["method"] == "best_constant"             # asked for, and recorded
+    assert np.allclose(w, w[0]) and g == pytest.approx(info["gamma_best_constant"], abs=1e-12)
+    with pytest.raises(ValueError):
+        find_optimal_weights(ring, method="cvxpy")
+
+
+def test_auto_switches_to_subgradient_and_says_so():
+    """Above max_sdp the Lanczos subgradient method runs (never a silent best-constant): it never
+    returns worse than the best-constant weights and lands near the SDP optimum."""
+    edges = list(nx.connected_watts_strogatz_graph(40, 4, 0.5, seed=3).edges)
+    info_sg, info_sdp = {}, {}
+    w, g = find_optimal_weights(edges, max_sdp=16, info=info_sg)
+    assert info_sg["method"] == "subgradient"
+    assert g == pytest.approx(spectral_gamma(edges, w), abs=1e-10)
+    assert g <= info_sg["gamma_best_constant"] + 1e-12
+    _, g_sdp = find_optimal_weights(edges, info=info_sdp)
+    assert info_sdp["method"] == "sdp" and g_sdp <= g + 1e-9
+    assert g - g_sdp < 0.5 * (info_sg["gamma_best_constant"] - g_sdp) + 1e-6
+
+
+def test_edge_transitive_torus_best_constant_is_optimal():
+    """On an edge-transitive graph (8 x 8 torus) the SDP optimum is the uniform best-constant
+    weight: what makes ``best_constant`` exact for config c4's torus."""
+    from distributed_learning_amd.graph import torus_edges
+    edges = torus_edges(8, 8)
+    info = {}
+    w, g = find_optimal_weights(edges, info=info)
+    assert info["method"] == "sdp"
+    assert g == pytest.approx(info["gamma_best_constant"], abs=1e-7)
+    np.testing.assert_allclose(w, info["best_constant_weight"], atol=1e-4)
+
+
+@pytest.mark.parametrize("name", ["rr4_1024", "torus64"])
+def test_committed_config_weights(golden, name):
+    """The committed FDLA weights of the BASELINE graphs (scripts/make_fdla_fixture.py): c2's
+    random 4-regular 1024-agent graph (barrier SDP) and c4's 64 x 64 torus.  gamma is recomputed
+    here from the weights, the c2 weights beat the best constant, and W = I - L(w) is doubly
+    stochastic and symmetric."""
+    d = golden(f"fdla_{name}.npz")
+    edges = [tuple(int(x) for x in e) for e in d["edges"]]
+    w = d["w"]
+    if name == "rr4_1024":
+        assert str(d["method"]) == "sdp"
+        assert spectral_gamma(edges, w) == pytest.approx(float(d["gamma"]), abs=1e-9)
+        assert float(d["gamma"]) < float(d["gamma_best_constant"]) - 0.015
+        assert not np.allclose(w, w[0])                    # genuinely per-edge weights
+    else:
+        assert float(d["gamma"]) == pytest.approx(float(d["gamma_best_constant"]), abs=1e-12)
+    W = from_edge_weights(edges, w).dense()
+    np.testing.assert_allclose(W.sum(0), 1, atol=1e-12)
+    np.testing.assert_allclose(W, W.T, atol=0)

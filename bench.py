@@ -84,6 +84,11 @@ def parse():
     p.add_argument("--no-halo-probe", action="store_true",
                    help="N>1: skip the c4 agent-partition (RCCL halo exchange) probe that the "
                         "c2 line carries as its 'c4_halo' object")
+    p.add_argument("--weights", default="best-constant", choices=["best-constant", "fdla"],
+                   help="c2/c2-mix: mixing weights of the headline loop (fdla: the committed "
+                        "per-edge FDLA SDP weights of the c2 graph, tests/golden/fdla_rr4_1024.npz)")
+    p.add_argument("--no-fdla-probe", action="store_true",
+                   help="c2 at N=1: skip the second measurement with per-edge FDLA weights")
     p.add_argument("--dist-backend", default="nccl",
                    help="nccl (= RCCL, default) or gloo (multi-rank rehearsal on one GPU)")
     return p.parse_args()
@@ -110,6 +115,56 @@ def build_graph(n, kind="rr4"):
     verts = sorted(first_appearance_vertices(edges))
     w = best_constant_weight(edges, verts)
     return from_edge_weights(edges, [w] * len(edges), verts), w
+
+
+FDLA_FIXTURE = os.path.join(ROOT, "tests", "golden", "fdla_rr4_1024.npz")
+
+
+def build_fdla_graph(n):
+    """The c2 graph with its per-edge FDLA weights (utils/fast_averaging.py's SDP, solved on the
+    host by scripts/make_fdla_fixture.py and committed): W = I - L(w), every row its own weights
+    (shared_row_weights = 0, so the kernel stages all n*(d+1) weights)."""
+    from distributed_learning_amd.graph import first_appearance_vertices, from_edge_weights
+    d = np.load(FDLA_FIXTURE)
+    edges = [tuple(int(x) for x in e) for e in d["edges"]]
+    if len(first_appearance_vertices(edges)) != n:
+        raise ValueError(f"the FDLA fixture is for {len(first_appearance_vertices(edges))} agents")
+    verts = sorted(first_appearance_vertices(edges))
+    info = {"gamma": float(d["gamma"]), "gamma_best_constant": float(d["gamma_best_constant"]),
+            "method": str(d["method"]), "source": os.path.relpath(FDLA_FIXTURE, ROOT)}
+    return from_edge_weights(edges, d["w"], verts), info
+
+
+def fdla_probe(dev, n, P, lr, steps=20, warmup=3):
+    """The headline round (fused local step + mix + deviation, tiled layout) with the per-edge
+    FDLA weights instead of the uniform best-constant ones: HIP-event time per launch."""
+    from distributed_learning_amd import engine
+    csr, info = build_fdla_graph(n)
+    g = torch.Generator(device=dev).manual_seed(77)
+    eng = engine.GossipEngine(csr, P, device=dev, X=torch.randn(n, P, device=dev, generator=g))
+    G = eng.layout_like(torch.randn(n, P, device=dev, generator=g))
+    plan = eng.plan(deviation=True)
+    for _ in range(warmup):
+        eng.round(G=G, lr=lr, deviation=True)
+    stream = torch.cuda.current_stream(dev)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(steps)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for a, b in evs:
+        a.record(stream)
+        eng.round(G=G, lr=lr, deviation=True)
+        b.record(stream)
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / steps
+    launch_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    achieved = 12 * n * P / (launch_ms / 1e3) / 1e9
+    del eng, G
+    torch.cuda.empty_cache()
+    return {"weights": "per-edge FDLA (SDP)", **info, "shared_row_weights": int(csr.shared_row_weights),
+            "rounds_per_s": 1.0 / wall, "ms_per_step": wall * 1e3, "launch_ms": launch_ms,
+            "achieved_GBs": achieved, "frac": achieved / HBM_PEAK_GBS, "plan": plan,
+            "kernel_instance": kernel_name(plan, True, True, n)}
 
 
 def copy_ceiling(dev, nbytes=4 << 30, reps=10):
@@ -924,7 +979,12 @@ def main():
     n, P = args.agents, args.params
     sgd = args.workload == "c2"
     lr = 1e-3
-    csr, wconst = build_graph(n)
+    if args.weights == "fdla":
+        csr, finfo = build_fdla_graph(n)
+        weights_desc = f"per-edge FDLA (SDP gamma {finfo['gamma']:.6f})"
+    else:
+        csr, wconst = build_graph(n)
+        weights_desc = f"best-constant {wconst:.6f}"
     g = torch.Generator(device=dev).manual_seed(1000 + rank)
     X = torch.randn(n, P, device=dev, generator=g)
     G = torch.randn(n, P, device=dev, generator=g) if sgd else None
@@ -975,6 +1035,12 @@ def main():
     value = n_gpus * args.steps / elapsed                 # 1024 x 2^20-equivalent rounds / s
     achieved = bytes_per_round / (launch_ms / 1e3) / 1e9  # GB/s of the fused round launch
 
+    fdla = None
+    if rank == 0 and world == 1 and sgd and args.weights == "best-constant" and \
+            not args.no_fdla_probe:
+        del eng, G
+        torch.cuda.empty_cache()
+        fdla = fdla_probe(dev, n, P, lr)
     if rank == 0:
         kname = kernel_name(plan, sgd, True, n)
         traffic, traffic_src = traffic_from_profile(kname)
@@ -1007,7 +1073,7 @@ def main():
             "config": {"workload": "c2: pure gossip consensus round, fused local step + mix + "
                                    "deviation" if sgd else "c2-mix: mix + deviation",
                        "agents": n, "params_per_gpu": P, "graph": "random 4-regular",
-                       "weights": f"best-constant {wconst:.6f}", "parallelism":
+                       "weights": weights_desc, "parallelism":
                            f"column stripes x{n_gpus}, deviation all-reduce" if n_gpus > 1
                            else "single GPU",
                        "plan": plan},
@@ -1022,6 +1088,7 @@ def main():
                          "stream_variants_GBs": ceiling_variants},
             "cpu_baseline": cpu,
             "final_max_deviation": dev_max,
+            "fdla_weights": fdla,
         }
     if world > 1:
         dist.barrier()

@@ -16,9 +16,9 @@ import torch
 from . import mixer_ref
 
 
-def flatten(model):
-    """mixer.py:68-69"""
-    return torch.cat([p.data.to(torch.float32).view(-1) for p in model.parameters()]).numpy()
+def flatten(model, dtype=torch.float32):
+    """mixer.py:68-69 (dtype=float64 only for the tests' fp64 truth runs)"""
+    return torch.cat([p.data.to(dtype).view(-1) for p in model.parameters()]).numpy()
 
 
 def load_flat(model, vec):
@@ -30,19 +30,21 @@ def load_flat(model, vec):
         off += n
 
 
-def consensus_sgd_steps(models, optimizers, data, labels, rowptr, cols, w, steps):
+def consensus_sgd_steps(models, optimizers, data, labels, rowptr, cols, w, steps,
+                        dtype=torch.float32):
     """``steps`` rounds of (local SGD step per agent, one Mixer round).  Returns the per-agent
-    losses of every step ([steps][N])."""
+    losses of every step ([steps][N]).  dtype=float64 (models, data and the mix in fp64) is the
+    tests' accuracy yardstick, not a reference behaviour."""
     losses = []
     for _ in range(steps):
         ls = []
         for a, (m, opt) in enumerate(zip(models, optimizers)):
             opt.zero_grad()
-            loss = torch.nn.functional.cross_entropy(m(data[a]), labels[a])
+            loss = torch.nn.functional.cross_entropy(m(data[a].to(dtype)), labels[a])
             loss.backward()
             opt.step()
             ls.append(float(loss.detach()))
-        X = np.stack([flatten(m) for m in models])
+        X = np.stack([flatten(m, dtype) for m in models])
         Y = mixer_ref.mix_once(X, rowptr, cols, w)
         for m, y in zip(models, Y):
             load_flat(m, y)

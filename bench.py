@@ -57,7 +57,7 @@ def parse():
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--workload", default="c2",
-                   choices=["c1", "c2", "c2-mix", "c2-gossip", "c3", "c4", "c5"])
+                   choices=["c1", "c2", "c2-mix", "c2-gossip", "c3", "c4", "c4-gather", "c5"])
     p.add_argument("--graph", default="rr4", choices=["rr4", "circ4", "torus"],
                    help="c2-gossip: agent graph (circ4 = conflict-free control)")
     p.add_argument("--relabel", type=int, default=2_000_000,
@@ -451,6 +451,99 @@ def run_c3(args, dev, rank, world):
         "mean_loss_first_last": [float(v.item()) for v in losses],
     }
     print(json.dumps(rec), flush=True)
+
+
+def per_edge_torus(rows, cols, seed=0):
+    """The c4 torus with genuinely per-edge symmetric weights (best constant x (1 +- 10 %)):
+    W = I - L(w) stays doubly stochastic, but with 4096 agents the per-entry CSR (120 KiB) no
+    longer fits LDS beside a column tile of every agent, so dl_mix_round takes the general
+    gather path."""
+    import math
+    from distributed_learning_amd import graph
+    n = rows * cols
+    edges = graph.torus_edges(rows, cols)
+    wc = 2.0 / (2.0 - 2.0 * math.cos(2 * math.pi / cols) + 8.0)
+    u = np.random.default_rng(seed).random(len(edges))
+    return graph.from_edge_weights(edges, list(wc * (0.9 + 0.2 * u)), list(range(n))), n
+
+
+def run_gather(args, dev, rank, world):
+    """c4 with per-edge weights (``per_edge_torus``): 4096 agents x 2^18 params, one fused round
+    (local step + mix + deviation) per step.  The per-entry CSR does not fit LDS beside a column
+    tile of every agent, so the product path is the register-CSR tile kernel (plan path 4,
+    column-tiled layout, fused deviation) -- ``value`` and ``roofline``.  The general gather
+    kernel (path 2: neighbour rows from L2/MALL, two-pass deviation), which irregular graphs of
+    this size still take, is timed on the same graph as ``gather`` (forced).  N>1: replicas."""
+    from distributed_learning_amd import engine
+    csr, n = per_edge_torus(64, 64)
+    P, lr = 1 << 18, 1e-3
+    gen = torch.Generator(device=dev).manual_seed(1000 + rank)
+    stream = torch.cuda.current_stream(dev)
+
+    def timed(round_fn):
+        evs = event_pairs(args.steps, 2)
+
+        def step(i):
+            if i is not None:
+                evs[i][0].record(stream)
+            round_fn()
+            if i is not None:
+                evs[i][1].record(stream)
+        elapsed = timed_loop(step, args, world, dev)
+        return elapsed, float(np.mean([a.elapsed_time(b) for a, b, *_ in evs]))
+
+    # product path: register-CSR tile kernel, tiled layout, fused deviation
+    eng = engine.GossipEngine(csr, P, device=dev, X=torch.randn(n, P, device=dev, generator=gen))
+    G = eng.layout_like(torch.randn(n, P, device=dev, generator=gen))
+    plan = eng.plan(deviation=True)
+    elapsed, launch_ms = timed(lambda: eng.round(G=G, lr=lr, deviation=True))
+    del eng, G
+    torch.cuda.empty_cache()
+    # the general gather kernel on the same graph (row-major operands, forced)
+    os.environ["DLAMD_FORCE_GATHER"] = "1"
+    W = engine.DeviceCsr(csr, dev)
+    X = engine.staggered_zeros((n, P), 0, dev).normal_(generator=gen)
+    Gr = engine.staggered_zeros((n, P), 1, dev).normal_(generator=gen)
+    Y = engine.staggered_zeros((n, P), 2, dev)
+    dsq, dmax = torch.empty(n, device=dev), torch.empty(1, device=dev)
+    ws = engine.Workspace(dev)
+    gplan = engine.plan_shape(W, P, deviation=True)
+    g_round = timed(lambda: engine.mix_round(W, X, Y, G=Gr, lr=lr, dev_sq=dsq, dev_max=dmax,
+                                             workspace=ws))
+    g_mix = timed(lambda: engine.mix_round(W, X, Y, G=Gr, lr=lr, workspace=ws))
+    del os.environ["DLAMD_FORCE_GATHER"]
+    bytes_per_round = 12 * n * P
+    prof = os.path.join(ROOT, "profiles", "r07", "peredge", "summary.json")
+    traffic, src = traffic_from_profile("mix_tile_kernel<1, 4, true, true, true, false, true, 5>",
+                                        prof)
+    g_traffic, g_src = traffic_from_profile("mix_gather_kernel", prof)
+    achieved = bytes_per_round / (launch_ms / 1e3) / 1e9
+    g_achieved = bytes_per_round / (g_mix[1] / 1e3) / 1e9
+    if rank == 0:
+        print(json.dumps({
+            "metric": "consensus rounds/sec, 4096 agents x 2^18 fp32 params, per-edge weights",
+            "value": world * args.steps / elapsed, "unit": "rounds/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic X, G ~ N(0,1) resident in HBM",
+            "config": {"workload": "c4-gather: 64x64 torus, per-edge weights (best constant "
+                                   "x U[0.9, 1.1]), fused local step + mix + deviation",
+                       "agents": n, "params": P, "plan": plan,
+                       "parallelism": f"{world} independent replicas" if world > 1
+                       else "single GPU"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_source": src,
+                         "kernel": "mix_tile_kernel register-CSR (+dev_reduce), HIP-event time",
+                         "bytes_per_launch": bytes_per_round, "launch_ms": launch_ms},
+            "gather": {"plan": gplan, "rounds_per_s_with_deviation": 1e3 / g_round[1],
+                       "round_ms_with_deviation": g_round[1], "mix_launch_ms": g_mix[1],
+                       "achieved": g_achieved, "frac": g_achieved / HBM_PEAK_GBS,
+                       "traffic": g_traffic, "traffic_source": g_src,
+                       "read_amplification": (g_traffic / bytes_per_round) if g_traffic else None,
+                       "grid_order": os.environ.get("DLAMD_GATHER_ORDER", "agents")},
+        }), flush=True)
 
 
 def run_c4(args, dev, rank, world):
@@ -967,9 +1060,9 @@ def main():
         else:
             dist.init_process_group(args.dist_backend)
 
-    if args.workload in ("c1", "c2-gossip", "c3", "c4", "c5"):
+    if args.workload in ("c1", "c2-gossip", "c3", "c4", "c4-gather", "c5"):
         {"c1": run_c1, "c2-gossip": run_gossip, "c3": run_c3, "c4": run_c4,
-         "c5": run_c5}[args.workload](args, dev, rank, world)
+         "c4-gather": run_gather, "c5": run_c5}[args.workload](args, dev, rank, world)
         if world > 1:
             dist.destroy_process_group()
         return

@@ -110,6 +110,8 @@ SIGNATURES = {
                                  ctypes.POINTER(DlMixPlan)]),
     "dl_mix_round": (_i32, [ctypes.POINTER(DlMixArgs), _vp, _sz, _vp]),
     "dl_mix_rounds_plan": (_i32, [ctypes.POINTER(DlMixArgs), ctypes.POINTER(DlMixPlan)]),
+    "dl_mix_rounds_plan_shape": (_i32, [_i32, _i64, _i32, _i32, _i32, _i32, _i32, _i32,
+                                        ctypes.POINTER(DlMixPlan)]),
     "dl_mix_rounds": (_i32, [ctypes.POINTER(DlMixArgs), _i32, _vp, _sz, _vp]),
     "dl_mix_trace_plan": (_i32, [ctypes.POINTER(DlMixArgs), ctypes.POINTER(_i32)]),
     "dl_mix_trace_workspace_bytes": (_sz, [_i32, _i32]),

@@ -115,7 +115,7 @@ int next_pow2_chunks(int64_t n_params) {
 // of all R rows is <= 64 KiB and fits LDS beside the CSR.  Measured on MI355X:
 // 64-KiB tiles stream at 5.7-5.85 TB/s for N = 256..1024, 128-KiB tiles at 5.0-5.6 TB/s
 // depending on the box.  0 = no tiled configuration fits.
-int choose_tiled_chunks(int32_t R, uint32_t csr, bool want_dev) {
+int choose_tiled_chunks(int32_t R, uint32_t csr, bool want_dev, int32_t regular = 0) {
     if (csr == 0 || R > 65535) return 0;
     for (int c = dl::kMaxChunks; c >= 1; c >>= 1) {
         if ((int64_t)R * c > (int64_t)dl::kRowsPerThread * dl::kTileThreads) continue;
@@ -124,7 +124,40 @@ int choose_tiled_chunks(int32_t R, uint32_t csr, bool want_dev) {
         const int64_t scratch = want_dev ? (int64_t)(dl::kTileThreads / 64) * c * 16 : 0;
         if (tile + csr + scratch <= dl::kLdsBytes) return c;
     }
+    // the CSR does not fit beside any tile: the register-CSR kernel needs LDS for the tile only
+    for (int c = 1; c >= 1; c >>= 1) {
+        const int64_t tile = (int64_t)R * c * 16;
+        const int64_t scratch = want_dev ? (int64_t)(dl::kTileThreads / 64) * c * 16 : 0;
+        if (dl::reg_csr_supported(c, R, regular, 0) && tile <= 65536 &&
+            tile + scratch <= dl::kLdsBytes)
+            return c;
+    }
     return 0;
+}
+
+// Register-CSR plan (path 4) for c chunks, or false when it does not apply.
+bool plan_reg(const dl_mix_args *a, int c, bool want_dev, Plan *pl) {
+    const int32_t R = a->W.n_rows;
+    if (a->n_halo > 0 || !dl::reg_csr_supported(c, R, a->W.uniform_row_nnz, 0)) return false;
+    const int64_t tile = (int64_t)R * c * 16;
+    const int64_t scratch = want_dev ? (int64_t)(dl::kTileThreads / 64) * c * 16 : 0;
+    if (tile + scratch > dl::kLdsBytes) return false;
+    const int64_t T = 4 * c;
+    const int64_t n_tiles = (a->n_params + T - 1) / T;
+    if (n_tiles > 0x7fffffff) return false;
+    int bpc = (int)(dl::kLdsBytes / (tile + scratch));
+    if (bpc > wg_per_cu_cap()) bpc = wg_per_cu_cap();
+    pl->pub.path = 4;
+    pl->pub.tile_cols = (int32_t)T;
+    pl->pub.grid = (int32_t)balanced_grid(
+        n_tiles, (int64_t)device_cus() * bpc * (a->tile_cols > 0 ? grid_mult() : 1));
+    pl->pub.lds_bytes = (int32_t)(tile + scratch);
+    pl->pub.n_tiles = (int32_t)n_tiles;
+    pl->pub.regular = 1;
+    pl->chunks = c;
+    pl->csr_off = (uint32_t)tile;
+    pl->scratch_off = (uint32_t)tile;
+    return true;
 }
 
 // Pick the kernel configuration for a mix round.
@@ -151,6 +184,8 @@ int plan_mix(const dl_mix_args *a, Plan *pl) {
         const int64_t tile = (int64_t)R * c * 16;
         const int64_t scratch = want_dev ? (int64_t)(dl::kTileThreads / 64) * c * 16 : 0;
         const int64_t lds = tile + csr + scratch;
+        if ((csr == 0 || lds > dl::kLdsBytes) && R <= 65535 && plan_reg(a, c, want_dev, pl))
+            return DL_OK;
         if (csr == 0 || R > 65535 || (int64_t)R * c > (int64_t)dl::kRowsPerThread * dl::kTileThreads ||
             lds > dl::kLdsBytes)
             return fail(DL_ERR_INVALID, "dl_mix_round: tile_cols %d does not fit this graph "
@@ -201,6 +236,9 @@ int plan_mix(const dl_mix_args *a, Plan *pl) {
             pl->scratch_off = (uint32_t)(tile + csr);
             return DL_OK;
         }
+    }
+    if (R <= 65535 && !force_gather) {
+        if (a->n_params % 4 == 0 && plan_reg(a, 1, want_dev, pl)) return DL_OK;
     }
     if (a->W.n_rows > 4 * 65535)
         return fail(DL_ERR_UNSUPPORTED, "dl_mix_round: %d rows exceed the gather path limit",
@@ -706,6 +744,30 @@ int dl_mix_plan_query(const dl_mix_args *args, dl_mix_plan *plan) {
     return DL_OK;
 }
 
+int dl_mix_rounds_plan_shape(int32_t n_rows, int64_t n_params, int32_t nnz,
+                             int32_t uniform_row_nnz, int32_t shared_row_weights,
+                             int32_t doubly_stochastic, int32_t deviation, int32_t tile_cols,
+                             dl_mix_plan *plan) {
+    g_err.clear();
+    if (!plan || n_rows <= 0 || n_params <= 0 || nnz < 0 || tile_cols < 0)
+        return fail(DL_ERR_INVALID, "dl_mix_rounds_plan_shape: bad arguments");
+    dl_mix_args a{};
+    a.W.n_rows = n_rows;
+    a.W.nnz = nnz;
+    a.W.uniform_row_nnz = uniform_row_nnz;
+    a.W.shared_row_weights = uniform_row_nnz > 0 ? shared_row_weights : 0;
+    a.W.doubly_stochastic = doubly_stochastic;
+    a.n_params = n_params;
+    a.tile_cols = tile_cols;
+    float dummy;
+    if (deviation) a.dev_max = &dummy;
+    Plan pl;
+    const int rc = plan_rounds(&a, &pl);
+    if (rc) return rc;
+    *plan = pl.pub;
+    return DL_OK;
+}
+
 int dl_mix_plan_shape(int32_t n_rows, int32_t n_halo, int64_t n_params, int32_t nnz,
                       int32_t uniform_row_nnz, int32_t shared_row_weights, int32_t deviation,
                       int32_t tile_cols, dl_mix_plan *plan) {
@@ -726,7 +788,7 @@ int dl_mix_plan_shape(int32_t n_rows, int32_t n_halo, int64_t n_params, int32_t 
         const int32_t n_w = (reg && a.W.shared_row_weights) ? uniform_row_nnz : nnz;
         const int c = n_halo == 0 ? choose_tiled_chunks(n_rows, dl::csr_lds_bytes(
                                                                     n_rows, nnz, reg, n_w),
-                                                        deviation != 0)
+                                                        deviation != 0, uniform_row_nnz)
                                   : 0;
         if (c == 0) {  // not tileable: report the row-major plan
             tile_cols = 0;
@@ -757,9 +819,13 @@ int dl_mix_round(const dl_mix_args *args, void *workspace, size_t ws_bytes, dl_s
                                       "workspace of dl_mix_workspace_bytes()");
     dl::TileArgs t = tile_args(args);
     const bool sgd = args->g != nullptr;
-    if (pl.pub.path == 1) {
+    if (pl.pub.path == 4 && !t.vec) {   // the register-CSR kernel is FAST-only: gather instead
+        pl.pub.path = 2;
+    }
+    if (pl.pub.path == 1 || pl.pub.path == 4) {
         // full tiles on the branch-free float4 kernel, the ragged tail tile (and unaligned
         // operands) on the guarded one; each launch writes its own deviation partial rows
+        const bool reg_csr = pl.pub.path == 4;
         const int64_t T = pl.pub.tile_cols;
         if (t.tiled) {
             if (!t.vec)
@@ -793,11 +859,14 @@ int dl_mix_round(const dl_mix_args *args, void *workspace, size_t ws_bytes, dl_s
             t.n_tiles = (int32_t)n_full;
             t.col_base = 0;
             t.dev_partial = partial;
-            hipError_t e = dl::launch_mix_tile(t, pl.chunks, sgd, pl.dev, true, grid_full,
-                                               lds, true, s);
+            hipError_t e = reg_csr ? dl::launch_mix_tile_reg(t, pl.chunks, sgd, pl.dev,
+                                                             grid_full, lds, s)
+                                   : dl::launch_mix_tile(t, pl.chunks, sgd, pl.dev, true,
+                                                         grid_full, lds, true, s);
             if (e != hipSuccess) return hip_fail(e, "mix_tile_kernel launch");
         }
         if (grid_tail > 0) {
+            if (reg_csr) return fail(DL_ERR_INVALID, "dl_mix_round: register-CSR plan with a tail");
             t.n_tiles = (int32_t)n_tail;
             t.col_base = n_full * T;
             t.dev_partial = pl.dev ? partial + (size_t)grid_full * Nr : nullptr;

@@ -65,6 +65,11 @@ uint32_t csr_lds_bytes(int32_t n_rows, int32_t nnz, int32_t regular, int32_t n_w
 hipError_t launch_mix_tile(const TileArgs &a, int chunks, bool sgd, bool dev, bool mix, int grid,
                            int lds_bytes, bool fast, hipStream_t s);
 hipError_t launch_mix_gather(const TileArgs &a, bool sgd, hipStream_t s);
+// Tile kernel with the CSR in registers (regular graphs of 5 entries per row whose CSR does not
+// fit LDS beside the tile): FAST path only, no halo, chunks 1, <= 4 rows per thread.
+bool reg_csr_supported(int chunks, int n_rows, int regular, int n_halo);
+hipError_t launch_mix_tile_reg(const TileArgs &a, int chunks, bool sgd, bool dev, int grid,
+                               int lds, hipStream_t s);
 // rows per thread (KV) the FAST tile kernels use for n_src rows at `chunks` float4 per row
 int tile_passes(int chunks, int n_src, bool fast);
 // K rounds of mixing on LDS-resident tiles (mix_multi.hip); FAST tiles only, no halo rows

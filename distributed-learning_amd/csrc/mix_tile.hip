@@ -113,10 +113,14 @@ __device__ __forceinline__ float4 *at(float *base, uint32_t off) {
 // HALO : source rows [n_rows, n_src) come from the halo buffer
 // FAST : every tile is full and every operand 16-byte aligned (float4 path with 32-bit
 //        offsets from a uniform tile base); false = guarded scalar path (tail, unaligned)
+// RD   : 0 = CSR staged in LDS; RD > 0 = regular graph with RD entries per row whose CSR does
+//        not fit LDS beside the tile (per-edge weights on thousands of agents): every thread
+//        keeps its KV rows' weights and LDS row indices in registers (a thread mixes exactly
+//        the rows it stages), loaded once per workgroup.
 // Tiles cover columns [col_base + t*T, ...) for t < n_tiles.  Lanes whose row does not exist
 // (the last, ragged pass) re-read row 0 -- an L1 hit -- and never write LDS or y, so every
 // pass is straight-line code and the loads of the next tile stay in flight during the mix.
-template <int C, int KV, bool SGD, bool DEV, bool MIX, bool HALO, bool FAST>
+template <int C, int KV, bool SGD, bool DEV, bool MIX, bool HALO, bool FAST, int RD = 0>
 __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float4 *tile = reinterpret_cast<float4 *>(smem);
@@ -136,7 +140,26 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
     float *lw = reinterpret_cast<float *>(smem + a.csr_off);
     uint16_t *lcol = reinterpret_cast<uint16_t *>(smem + a.csr_off + 4u * (uint32_t)a.n_w);
     uint16_t *lrp = lcol + nnz;
-    if (MIX) {
+    // register CSR: weights, and the float4 LDS index (col * C + c < 2^16: the host admits
+    // KV <= 4 at C <= 2, i.e. at most 4096 rows) packed two per register
+    constexpr int NRC = RD > 0 ? KV * RD : 1;
+    float rw[NRC];
+    uint32_t ri[(NRC + 1) / 2];
+    if (RD > 0) {
+#pragma unroll
+        for (int i = 0; i < (NRC + 1) / 2; ++i) ri[i] = 0u;
+#pragma unroll
+        for (int k = 0; k < KV; ++k) {
+            const int r = s + k * SLOTS;
+#pragma unroll
+            for (int e = 0; e < RD; ++e) {
+                const int j = k * RD + e;
+                const int idx = (r < Nr ? r : 0) * RD + e;
+                rw[j] = a.w[idx];
+                ri[j >> 1] |= ((uint32_t)a.col[idx] * C + c) << (16 * (j & 1));
+            }
+        }
+    } else if (MIX) {
         for (int i = tid; i < a.n_w; i += NT) lw[i] = a.w[i];
         for (int i = tid; i < nnz; i += NT) lcol[i] = (uint16_t)a.col[i];
         if (!a.regular)
@@ -243,6 +266,26 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
         return acc;
     };
 
+    // the same fold from the register CSR of this thread's pass k: k is a runtime value in the
+    // rolled pass loop, so entry e of pass k is picked by a select chain over the KV passes
+    // (statically indexed registers, no scratch)
+    auto mix_row_reg = [&](int k) {
+        float4 acc = zero4();
+#pragma unroll
+        for (int e = 0; e < (RD > 0 ? RD : 1); ++e) {
+            float w = rw[e];
+            uint32_t idx = ri[e >> 1] >> (16 * (e & 1));
+#pragma unroll
+            for (int kk = 1; kk < KV; ++kk) {
+                const int j = kk * RD + e;
+                w = k == kk ? rw[j] : w;
+                idx = k == kk ? ri[j >> 1] >> (16 * (j & 1)) : idx;
+            }
+            axpy4(acc, w, tile[idx & 0xffffu]);
+        }
+        return acc;
+    };
+
     // column mean of the tile over all agents from per-thread partial sums: thread -> wave
     // (lanes with the same c) -> LDS scratch -> every thread sums the 16 wave partials in order
     auto tile_mean = [&](float4 cs) {
@@ -325,7 +368,7 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
             for (int k = 0; k < KV; ++k) {
                 const int ag = s + k * SLOTS;
                 if (ag < Nr) {
-                    const float4 acc = mix_row(ag);
+                    const float4 acc = RD > 0 ? mix_row_reg(k) : mix_row(ag);
                     if (FAST) {
                         if (a.nt_store)
                             nt_store4(acc, at(yt, oy + (uint32_t)k * sy));
@@ -350,7 +393,7 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
 #pragma unroll 1
                 for (int k = 0; k < KV; ++k) {
                     const int ag = s + k * SLOTS;
-                    if (ag < Nr) dev_add(k, mix_row(ag), mean);
+                    if (ag < Nr) dev_add(k, RD > 0 ? mix_row_reg(k) : mix_row(ag), mean);
                 }
             }
         } else {
@@ -383,14 +426,20 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
 
 // General path (graphs whose tile does not fit LDS): one wave per (agent, 256 columns); the
 // agent index is wave-uniform so CSR reads are scalar loads; neighbour rows come from L2/MALL.
-template <bool SGD>
+// AGENT_FAST: blockIdx.x walks the agent groups of one 256-column chunk before the next chunk
+// (grid.x = agent groups), so the chunk of every row -- X and G, 2 KiB per agent -- is read by all
+// its neighbours while it is still in L2 / MALL; otherwise blockIdx.x walks the columns of one
+// agent group (neighbour rows are re-read from HBM by every agent that gathers them).
+template <bool SGD, bool AGENT_FAST>
 __global__ void __launch_bounds__(256) mix_gather_kernel(TileArgs a) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    const int ag = blockIdx.y * 4 + wave;
+    const int grp = AGENT_FAST ? blockIdx.x : blockIdx.y;
+    const int chunk = AGENT_FAST ? blockIdx.y : blockIdx.x;
+    const int ag = grp * 4 + wave;
     if (ag >= a.n_rows) return;
     const int64_t P = a.n_params;
-    const int64_t c0 = ((int64_t)blockIdx.x * 64 + lane) * 4;
+    const int64_t c0 = ((int64_t)chunk * 64 + lane) * 4;
     if (c0 >= P) return;
     const bool vec = a.vec != 0;
     const int Nr = a.n_rows;
@@ -519,9 +568,9 @@ __global__ void __launch_bounds__(1024) stream_triad_tile_kernel(const float4 *_
     }
 }
 
-template <int C, int KV, bool SGD, bool DEV, bool MIX, bool HALO, bool FAST>
+template <int C, int KV, bool SGD, bool DEV, bool MIX, bool HALO, bool FAST, int RD = 0>
 hipError_t launch_one(const TileArgs &a, int grid, int lds, hipStream_t s) {
-    auto k = mix_tile_kernel<C, KV, SGD, DEV, MIX, HALO, FAST>;
+    auto k = mix_tile_kernel<C, KV, SGD, DEV, MIX, HALO, FAST, RD>;
     hipError_t e = allow_full_lds(reinterpret_cast<const void *>(k));
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k, dim3(grid), dim3(kTileThreads), lds, s, a);
@@ -557,6 +606,30 @@ int tile_passes(int chunks, int n_src, bool fast) {
     const int need = (n_src + slots - 1) / slots;
     if (!fast) return kRowsPerThread;
     return need <= 2 ? 2 : need <= 4 ? 4 : 8;
+}
+
+// Register-CSR tile kernels: regular graphs of 5 entries per row (degree 4 + self), FAST path,
+// no halo rows, C = 1 (T = 4 columns), KV in {2, 4} rows per thread, i.e. up to 4096 agents.
+// (C = 2 at KV = 4 spills; at KV = 2 -- 1024 agents -- the CSR always fits LDS.)
+template <int KV>
+hipError_t launch_reg_kv(const TileArgs &a, bool sgd, bool dev, int grid, int lds, hipStream_t s) {
+    if (sgd)
+        return dev ? launch_one<1, KV, true, true, true, false, true, 5>(a, grid, lds, s)
+                   : launch_one<1, KV, true, false, true, false, true, 5>(a, grid, lds, s);
+    return dev ? launch_one<1, KV, false, true, true, false, true, 5>(a, grid, lds, s)
+               : launch_one<1, KV, false, false, true, false, true, 5>(a, grid, lds, s);
+}
+
+bool reg_csr_supported(int chunks, int n_rows, int regular, int n_halo) {
+    return regular == 5 && n_halo == 0 && chunks == 1 && tile_passes(chunks, n_rows, true) <= 4;
+}
+
+hipError_t launch_mix_tile_reg(const TileArgs &a, int chunks, bool sgd, bool dev, int grid,
+                               int lds, hipStream_t s) {
+    if (!reg_csr_supported(chunks, a.n_rows, a.regular, a.n_src - a.n_rows))
+        return hipErrorInvalidValue;
+    return tile_passes(chunks, a.n_src, true) <= 2 ? launch_reg_kv<2>(a, sgd, dev, grid, lds, s)
+                                                   : launch_reg_kv<4>(a, sgd, dev, grid, lds, s);
 }
 
 hipError_t launch_mix_tile(const TileArgs &a, int chunks, bool sgd, bool dev, bool mix, int grid,
@@ -605,11 +678,24 @@ uint32_t csr_lds_bytes(int32_t n_rows, int32_t nnz, int32_t regular, int32_t n_w
 }
 
 hipError_t launch_mix_gather(const TileArgs &a, bool sgd, hipStream_t s) {
-    dim3 grid((unsigned)((a.n_params + 255) / 256), (unsigned)((a.n_rows + 3) / 4));
-    if (sgd)
-        hipLaunchKernelGGL(mix_gather_kernel<true>, grid, dim3(256), 0, s, a);
-    else
-        hipLaunchKernelGGL(mix_gather_kernel<false>, grid, dim3(256), 0, s, a);
+    const unsigned chunks = (unsigned)((a.n_params + 255) / 256);
+    const unsigned groups = (unsigned)((a.n_rows + 3) / 4);
+    // DLAMD_GATHER_ORDER=columns keeps the column-fastest order (measurement knob)
+    const char *o = getenv("DLAMD_GATHER_ORDER");
+    const bool agent_fast = !(o && o[0] == 'c') && chunks <= 65535;
+    if (agent_fast) {
+        dim3 grid(groups, chunks);
+        if (sgd)
+            hipLaunchKernelGGL((mix_gather_kernel<true, true>), grid, dim3(256), 0, s, a);
+        else
+            hipLaunchKernelGGL((mix_gather_kernel<false, true>), grid, dim3(256), 0, s, a);
+    } else {
+        dim3 grid(chunks, groups);
+        if (sgd)
+            hipLaunchKernelGGL((mix_gather_kernel<true, false>), grid, dim3(256), 0, s, a);
+        else
+            hipLaunchKernelGGL((mix_gather_kernel<false, false>), grid, dim3(256), 0, s, a);
+    }
     return hipGetLastError();
 }
 

@@ -233,6 +233,20 @@ def rounds_plan(W: DeviceCsr, X, Y, deviation=False, tiled=None):
     return {f: getattr(plan, f) for f, _ in plan._fields_}
 
 
+def rounds_plan_shape(W: DeviceCsr, n_params, deviation=False, tile_cols=0):
+    """dl_mix_rounds_plan_shape: the multi-round configuration for row-major (tile_cols 0) or
+    column-tiled operands of these sizes, or None when the multi-round kernel does not fit."""
+    lib = _lib.load()
+    plan = _lib.DlMixPlan()
+    rc = lib.dl_mix_rounds_plan_shape(W.n_rows, int(n_params), W.nnz, W.uniform_row_nnz,
+                                      W.shared_row_weights, W.doubly_stochastic,
+                                      int(bool(deviation)), int(tile_cols), ctypes.byref(plan))
+    if rc == _lib.DL_ERR_UNSUPPORTED:
+        return None
+    _lib.check(rc, "dl_mix_rounds_plan_shape")
+    return {f: getattr(plan, f) for f, _ in plan._fields_}
+
+
 def until_fits(W: DeviceCsr, n_params):
     """True when dl_mix_until holds these agents' whole vectors in one workgroup's LDS."""
     return W.n_src == W.n_rows and bool(_lib.load().dl_mix_until_fits(W.n_rows, int(n_params),
@@ -412,7 +426,7 @@ class GossipEngine:
         self.n, self.P = csr.n_rows, int(n_params)
         plan = plan_shape(self.W, self.P, deviation=True,
                           tile_cols=int(tile_cols) if tile_cols else -1)
-        tiled_ok = plan["path"] == 1 and plan["tile_cols"] >= 4 and self.W.n_src == self.n
+        tiled_ok = plan["path"] in (1, 4) and plan["tile_cols"] >= 4 and self.W.n_src == self.n
         if layout == "auto":
             layout = "tiled" if tiled_ok else "rows"
         if layout == "tiled" and not tiled_ok:

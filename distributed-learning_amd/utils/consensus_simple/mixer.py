@@ -18,6 +18,7 @@ LDS-resident column tiles, bit-identical to ``times`` single rounds).  The resul
 back into the models once at the end (:34-35, 71-76).
 """
 import logging
+import math
 
 import numpy as np
 import torch
@@ -51,7 +52,7 @@ class Mixer(object):
         self._device = torch.device(device) if device is not None else None
         self._ws = None
         self._csr = None   # (host Csr, DeviceCsr) of the last topology seen
-        self._ordered = None   # (host Csr, DeviceCsr in LDS slot order, agents in slot order)
+        self._ordered = None   # (host Csr, n_params, DeviceCsr in slot order or None, agents)
 
     # ------------------------------------------------------------------ public API (:18-38)
     def mix(self, times=1, eps=None):
@@ -66,10 +67,13 @@ class Mixer(object):
             agents = None
             if eps is None and times >= 1 and not (
                     not self._custom_metric and _engine.until_fits(W, self._n_params())):
-                # mix(times) with no stop test on a large X: the rows go into the device matrix
-                # in an LDS slot order (every agent keeps its CSR entry order, so its bits are
-                # the same; the multi-round pass gathers neighbours with fewer bank conflicts)
-                W, agents = self._ordered_csr()
+                # mix(times) with no stop test on a large X: when the multi-round pass will run,
+                # the rows go into the device matrix in an LDS slot order (every agent keeps its
+                # CSR entry order, so its bits are the same; the pass gathers neighbours with
+                # fewer bank conflicts)
+                W_ord, agents = self._ordered_csr(self._n_params())
+                if agents is not None:
+                    W = W_ord
             X = self._flatten_all(agents)
             if not self._custom_metric and _engine.until_fits(W, X.shape[1]):
                 times_done = self._mix_resident(W, X, times, eps)
@@ -91,8 +95,8 @@ class Mixer(object):
                 Pp = -(-P // 64) * 64
                 Xp = torch.nn.functional.pad(X, (0, Pp - P)) if Pp != P else X
                 Yp = torch.empty_like(Xp)
-                if _engine.mix_rounds(W, Xp, Yp, times, workspace=self._wspace()):
-                    X, times_done = Yp[:, :P], int(times)
+                if _engine.mix_rounds(W, Xp, Yp, math.ceil(times), workspace=self._wspace()):
+                    X, times_done = Yp[:, :P], math.ceil(times)
                     stopping_criterion = True
             while not stopping_criterion:
                 _engine.mix_round(W, X, Y, dev_sq=dev_sq if fused_dev else None,
@@ -134,7 +138,7 @@ class Mixer(object):
         log = eps is not None and self.logger.isEnabledFor(logging.DEBUG)
         done, first = 0, True
         while True:
-            _engine.mix_until(W, X, X, max(int(times) - done, 0), eps, self._UNTIL_ROUNDS,
+            _engine.mix_until(W, X, X, max(math.ceil(times) - done, 0), eps, self._UNTIL_ROUNDS,
                               status, trace)
             n, stopped = status.tolist()
             if log:
@@ -230,20 +234,32 @@ class Mixer(object):
         return self._csr[1]
 
     _SLOT_MOVES_PER_AGENT = 2000   # slot-order search moves (1024 agents: ~0.5 s, once)
+    _SLOT_MOVES_MAX = 4_000_000    # cap: the search is host work spent before the first round
+    _SLOT_MIN_AGENTS = 64          # below a few lane groups there is nothing to spread
 
-    def _ordered_csr(self):
+    def _ordered_csr(self, n_params):
         """(DeviceCsr, agents) with the rows in dl_lds_slot_order's order for the multi-round
-        kernel's agent-major images (4 chunks per row), recomputed only when the topology
-        changes; agents[slot] is the topology key of row slot."""
+        kernel's agent-major images, or (None, None) when ordering cannot pay: the multi-round
+        pass does not fit these sizes (dl_mix_rounds_plan_shape), the graph is irregular, or it
+        is small.  The search uses the chunks per row of the plan the pass will run with, its
+        moves are capped, and the result is cached per (topology, n_params);
+        agents[slot] is the topology key of row slot."""
         self._device_csr()
-        csr = self._csr[0]
-        if self._ordered is None or self._ordered[0] is not csr:
+        csr, W = self._csr
+        key = (csr, int(n_params))
+        if self._ordered is not None and self._ordered[0] is key[0] and \
+                self._ordered[1] == key[1]:
+            return self._ordered[2], self._ordered[3]
+        W_ord, agents = None, None
+        plan = _engine.rounds_plan_shape(W, -(-int(n_params) // 64) * 64)
+        if plan is not None and csr.uniform_row_nnz and csr.n_rows >= self._SLOT_MIN_AGENTS:
             keys = list(self.topology)
-            order, _, _ = lds_slot_order_native(csr, 4,
-                                                moves=self._SLOT_MOVES_PER_AGENT * csr.n_rows)
-            self._ordered = (csr, _engine.DeviceCsr(permuted(csr, order), self._dev()),
-                             [keys[a] for a in order])
-        return self._ordered[1], self._ordered[2]
+            moves = min(self._SLOT_MOVES_PER_AGENT * csr.n_rows, self._SLOT_MOVES_MAX)
+            order, _, _ = lds_slot_order_native(csr, plan["tile_cols"] // 4, moves=moves)
+            W_ord = _engine.DeviceCsr(permuted(csr, order), self._dev())
+            agents = [keys[a] for a in order]
+        self._ordered = (key[0], key[1], W_ord, agents)
+        return W_ord, agents
 
     def _n_params(self):
         return sum(p.numel() for p in self.models[next(iter(self.topology))].parameters())

@@ -144,6 +144,13 @@ int dl_mix_round(const dl_mix_args *args, void *workspace, size_t ws_bytes, dl_s
  * dl_mix_workspace_bytes (deviation only).  dl_mix_rounds_plan reports the configuration
  * (path 3) or DL_ERR_UNSUPPORTED. */
 int dl_mix_rounds_plan(const dl_mix_args *args, dl_mix_plan *plan);
+/* The same from sizes alone (no operands): the configuration dl_mix_rounds would use for
+ * row-major (tile_cols 0) or column-tiled operands of n_rows x n_params, or
+ * DL_ERR_UNSUPPORTED.  Lets a caller decide on an LDS slot order before X exists. */
+int dl_mix_rounds_plan_shape(int32_t n_rows, int64_t n_params, int32_t nnz,
+                             int32_t uniform_row_nnz, int32_t shared_row_weights,
+                             int32_t doubly_stochastic, int32_t deviation, int32_t tile_cols,
+                             dl_mix_plan *plan);
 int dl_mix_rounds(const dl_mix_args *args, int32_t rounds, void *workspace, size_t ws_bytes,
                   dl_stream_t stream);
 

@@ -343,13 +343,54 @@ def test_torus_4096_shared_weights_bit_exact(cuda, layout):
     torch.cuda.synchronize()
     assert np.array_equal(bits(eng.rows().cpu().numpy()), bits(want))
     check_dev(want, eng.dev_sq.cpu().numpy(), float(eng.dev_max.item()), mean.cpu().numpy())
-    # the same graph with per-entry weights (no shared flag) -> gather path, same bits
+    # the same graph with per-entry weights (no shared flag): the CSR no longer fits LDS beside
+    # the tile -> the register-CSR tile kernel (path 4), and the gather kernel when forced;
+    # same bits
     W = E.DeviceCsr(csr, cuda)
     W.shared_row_weights = 0
+    assert E.plan_shape(W, P)["path"] == 4
     Y = torch.empty(n, P, device=cuda)
     E.mix_round(W, torch.from_numpy(X).to(cuda), Y, G=torch.from_numpy(G).to(cuda), lr=0.01)
     torch.cuda.synchronize()
     assert np.array_equal(bits(Y.cpu().numpy()), bits(want))
+
+
+def _per_edge_regular(kind, n, seed):
+    """A degree-4 regular graph with genuinely per-edge symmetric weights (doubly stochastic)."""
+    from distributed_learning_amd.graph import from_edge_weights, random_regular_edges, torus_edges
+    edges = torus_edges(64, n // 64) if kind == "torus" else random_regular_edges(4, n, seed=seed)
+    w = np.random.default_rng(seed).uniform(0.12, 0.24, len(edges))
+    return from_edge_weights(edges, list(w), sorted({v for e in edges for v in e}))
+
+
+@pytest.mark.parametrize("kind,n", [("torus", 4096), ("rr4", 4096), ("rr4", 3600)])
+@pytest.mark.parametrize("layout", ["tiled", "rows"])
+def test_register_csr_tile_path(cuda, monkeypatch, kind, n, layout):
+    """Regular graphs of thousands of agents with per-edge weights: the CSR (n * 5 weights + ids)
+    does not fit LDS beside a column tile of every agent, so the tile kernel keeps each thread's
+    rows' CSR in registers (path 4) instead of falling back to the gather kernel.  Fused local
+    step + mix + deviation: bit-exact with the oracle, deviation within 1e-5; the forced gather
+    path gives the same bits."""
+    E = eng_mod()
+    csr = _per_edge_regular(kind, n, seed=n)
+    assert not csr.shared_row_weights and csr.doubly_stochastic
+    P = 2048 + 64
+    rng = np.random.default_rng(n)
+    X = rng.standard_normal((n, P), dtype=np.float32)
+    G = rng.standard_normal((n, P), dtype=np.float32)
+    want = cref.mix_round(X, csr.rowptr, csr.col, csr.w, G=G, lr=0.02)
+    eng = E.GossipEngine(csr, P, device=cuda, X=torch.from_numpy(X).to(cuda), layout=layout)
+    assert eng.plan()["path"] == 4, eng.plan()
+    mean = torch.empty(P, device=cuda)
+    eng.round(G=eng.layout_like(torch.from_numpy(G).to(cuda)), lr=0.02, deviation=True, mean=mean)
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(eng.rows().cpu().numpy()), bits(want))
+    check_dev(want, eng.dev_sq.cpu().numpy(), float(eng.dev_max.item()), mean.cpu().numpy())
+    if layout == "rows":
+        monkeypatch.setenv("DLAMD_FORCE_GATHER", "1")
+        Y, dsq, dmax, mean_g = run_round(csr, X, G=G, lr=0.02, cuda=cuda)
+        assert np.array_equal(bits(Y), bits(want))
+        check_dev(want, dsq, dmax, mean_g)
 
 
 

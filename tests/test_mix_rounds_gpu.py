@@ -198,36 +198,68 @@ def test_lds_slot_order_traced_is_transparent(cuda):
     torch.testing.assert_close(ta, tb, rtol=1e-5, atol=1e-6)
 
 
-def test_mixer_times_slot_order_bits(cuda):
-    """Mixer.mix(times=K), eps=None, on 64 agents of a random 4-regular graph: the rows go to
-    the device in dl_lds_slot_order's order (not the identity here) and every model ends with
-    the reference fold's bits; a second call reuses the cached order."""
+def test_mixer_times_slot_order_bits(cuda, monkeypatch):
+    """Mixer.mix(times=K), eps=None, on 1024 agents of a random 4-regular graph (small models, so
+    the multi-round pass runs 16-column tiles, 4 float4 chunks per row, where bank conflicts
+    matter): the rows go to the device in dl_lds_slot_order's order (not the identity), the
+    multi-round pass really runs on that ordered CSR, and every model ends with the reference
+    fold's bits; a second call reuses the cached order.  A fractional ``times`` runs
+    ceil(times) rounds, as the reference's ``times_done >= times`` loop does."""
     import logging
 
     from test_mix_trace_gpu import rr_csr
 
+    from distributed_learning_amd import engine as E
     from distributed_learning_amd.networks import ANNModel
     from distributed_learning_amd.utils.consensus_simple import Mixer
+    from distributed_learning_amd.utils.consensus_simple import mixer as mixer_mod
     torch.manual_seed(2)
-    n = 64
+    n = 1024
     keys = [f"agent{i}" for i in range(n)]
     csr = rr_csr(n, 9)
     topo = {}
     for i, k in enumerate(keys):
         topo[k] = {keys[csr.col[e]]: float(csr.w[e]) for e in range(csr.rowptr[i], csr.rowptr[i + 1])}
-    models = {k: ANNModel(60, 40, 10).to(cuda) for k in keys}
+    models = {k: ANNModel(8, 4, 2).to(cuda) for k in keys}
     X0 = np.stack([torch.cat([p.data.reshape(-1) for p in models[k].parameters()]).cpu().numpy()
                    for k in keys])
     rp, cl, w = M.topology_to_csr(topo)
     want = X0
     for _ in range(7 + 3):
         want = M.mix_once(want, rp, cl, w)
+    calls = []
+    real = E.mix_rounds
+
+    def spy(W, X, Y, rounds, *a, **kw):
+        calls.append((W, rounds))
+        return real(W, X, Y, rounds, *a, **kw)
+    monkeypatch.setattr(mixer_mod._engine, "mix_rounds", spy)
     mixer = Mixer(models, topo, logging.getLogger("t"))
     assert mixer.mix(times=7) == 7
     ordered = mixer._ordered
-    assert ordered is not None and ordered[2] != keys
-    assert mixer.mix(times=3) == 3
-    assert mixer._ordered is ordered
+    assert ordered is not None and ordered[3] is not None and ordered[3] != keys
+    assert calls and calls[-1] == (ordered[2], 7)          # the pass ran on the ordered CSR
+    assert mixer.mix(times=2.5) == 3                        # ceil, like the reference loop
+    assert mixer._ordered is ordered and calls[-1] == (ordered[2], 3)
     got = np.stack([torch.cat([p.data.reshape(-1) for p in models[k].parameters()]).cpu().numpy()
                     for k in keys])
     assert np.array_equal(bits(got), bits(want))
+
+
+def test_mixer_slot_order_skipped_when_it_cannot_pay(cuda):
+    """No slot-order search when the multi-round pass will not run (an irregular graph) or the
+    graph is small: the Mixer keeps topology order and caches that decision."""
+    import logging
+
+    from distributed_learning_amd.networks import ANNModel
+    from distributed_learning_amd.utils.consensus_simple import Mixer
+    torch.manual_seed(3)
+    keys = [f"a{i}" for i in range(80)]
+    topo = {k: {k: 0.5, keys[(i + 1) % 80]: 0.25, keys[(i - 1) % 80]: 0.25} for i, k in
+            enumerate(keys)}
+    topo[keys[0]] = {keys[0]: 0.4, keys[1]: 0.2, keys[79]: 0.2, keys[40]: 0.2}   # irregular
+    topo[keys[40]] = {keys[40]: 0.3, keys[41]: 0.25, keys[39]: 0.25, keys[0]: 0.2}
+    models = {k: ANNModel(60, 40, 10).to(cuda) for k in keys}
+    mixer = Mixer(models, topo, logging.getLogger("t"))
+    assert mixer.mix(times=4) == 4
+    assert mixer._ordered is not None and mixer._ordered[3] is None

@@ -152,13 +152,22 @@ class Mixer(object):
     _TRACE_MIN_ROUNDS = 4     # below this many rounds per traced pass the round loop is as good
     _TRACE_MAX_ROUNDS = 256   # rounds per traced pass (LDS permitting)
 
+    # The traced deviations take the column mean as a tree sum (and reuse the pass input's mean:
+    # mean(W x) = mean(x)) while the reference takes numpy's row-order mean every round
+    # (mixer.py:61-65): they agree to ~1e-5 relative or the mean-rounding floor.
+    # A traced value that close to eps could flip the integer round count, so that round is
+    # re-evaluated with the row-order two-pass deviation (dl_column_sum, as dl_mix_until does).
+    _TIE_RTOL = 2e-5
+
     def _mix_traced(self, W, X, times, eps):
         """mixer.py:27-32 with eps set, in passes of K rounds (dl_mix_rounds_trace): each pass
         runs K rounds in one HBM pass and returns the K per-round max deviations, which are
-        logged and tested in order exactly as the reference evaluates them after every round.
-        When the stop round falls inside a pass, that many rounds are re-run from the pass's
-        input (left intact).  Returns (X, times_done, stopped); stopped is False, with nothing
-        done, when the traced kernel does not fit (the caller's round loop takes over)."""
+        logged and tested in order exactly as the reference evaluates them after every round;
+        a deviation within rounding of eps is re-evaluated on that round's iterate with the
+        row-order mean (``_TIE_RTOL``).  When the stop round falls inside a pass, that many
+        rounds are re-run from the pass's input (left intact).  Returns (X, times_done,
+        stopped); stopped is False, with nothing done, when the traced kernel does not fit (the
+        caller's round loop takes over)."""
         P = X.shape[1]
         Pp = -(-P // 64) * 64
         cur = torch.nn.functional.pad(X, (0, Pp - P)) if Pp != P else X
@@ -169,11 +178,20 @@ class Mixer(object):
         trace = torch.empty(K, dtype=torch.float32, device=X.device)
         ws = self._wspace()
         done = 0
+        floor = None
         while True:
             _engine.mix_rounds_trace(W, cur, nxt, K, trace, workspace=ws)
             stop_at = None
             for i, d in enumerate(trace.tolist()):
                 max_dev = np.float32(d)
+                gap = abs(float(max_dev) - float(eps))
+                if gap <= 0.1 * abs(float(eps)):
+                    if floor is None:   # mean(W^k x) = mean(x): one column sum per call
+                        mean = _engine.column_sum(cur[:, :P]) / cur.shape[0]
+                        floor = 8.0 * np.sqrt(P) * float(np.finfo(np.float32).eps) * \
+                            float(mean.abs().max().item())
+                    if gap <= self._TIE_RTOL * abs(float(eps)) + floor:
+                        max_dev = self._recheck_deviation(W, cur, i + 1, P)
                 self.logger.debug('Mixer calculate max deviation= {}'.format(max_dev))
                 if max_dev < eps and done + i + 1 >= times:
                     stop_at = i + 1
@@ -183,12 +201,27 @@ class Mixer(object):
                 done += K
                 continue
             if stop_at < K:   # the same rounds again from the pass's input (bit-identical)
-                if not _engine.mix_rounds(W, cur, nxt, stop_at, workspace=ws):
-                    for _ in range(stop_at):
-                        _engine.mix_round(W, cur, nxt, workspace=ws)
-                        cur, nxt = nxt, cur
-                    nxt = cur
+                nxt = self._rounds_from(W, cur, stop_at, ws)
             return nxt[:, :P], done + stop_at, True
+
+    def _rounds_from(self, W, src, k, ws):
+        """The iterate k rounds after ``src`` (bit-identical to k single rounds), src intact."""
+        out = torch.empty_like(src)
+        if _engine.mix_rounds(W, src, out, k, workspace=ws):
+            return out
+        bufs, a = (out, torch.empty_like(src)), src
+        for j in range(k):
+            _engine.mix_round(W, a, bufs[j % 2], workspace=ws)
+            a = bufs[j % 2]
+        return a
+
+    def _recheck_deviation(self, W, src, k, P):
+        """max_a ||x_a - mean|| of the iterate k rounds after src, with numpy's row-order column
+        mean (mixer.py:61: dl_column_sum, then the division in fp32)."""
+        Z = self._rounds_from(W, src, k, self._wspace())[:, :P]
+        mean = _engine.column_sum(Z) / Z.shape[0]
+        _, dmax = _engine.deviation(Z, mean_in=mean, workspace=self._wspace())
+        return np.float32(dmax.item())
 
     def _update_stopping_criterion(self, X, times_done, max_times, eps, fused=None):
         """mixer.py:40-41; the deviation is only evaluated when eps is set (short circuit)."""

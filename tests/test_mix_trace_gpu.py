@@ -182,3 +182,53 @@ def test_mixer_traced_path_matches_reference_loop(cuda, monkeypatch, times, eps,
     devs = [ln for ln in h.lines if ln.startswith("Mixer calculate max deviation")]
     assert len(devs) == want_n + 1
     log.removeHandler(h)
+
+
+def test_mixer_traced_stop_tie_uses_row_order_mean(cuda):
+    """A traced max deviation within rounding of eps is re-evaluated on that round's iterate
+    with the row-order (numpy) column mean, so the integer round count Mixer.mix returns is the
+    reference loop's (mixer.py:40-41).  The test finds rounds where the traced value and numpy's
+    differ by >= 1 ulp while the row-order recheck reproduces numpy's bits, puts eps between the
+    two values, and checks the stop round for each such round."""
+    from distributed_learning_amd import engine
+    from distributed_learning_amd.networks import ANNModel
+    from distributed_learning_amd.utils.consensus_simple import Mixer
+    torch.manual_seed(3)
+    n, K = 24, 24
+    keys = [f"agent{i}" for i in range(n)]
+    csr = rr_csr(n, 7)
+    topo = {k: {keys[csr.col[e]]: float(csr.w[e]) for e in range(csr.rowptr[i], csr.rowptr[i + 1])}
+            for i, k in enumerate(keys)}
+    init = {k: ANNModel(60, 40, 10) for k in keys}
+    X0 = np.stack([torch.cat([p.data.reshape(-1) for p in init[k].parameters()]).numpy()
+                   for k in keys])
+    P = X0.shape[1]
+    rp, cl, w = M.topology_to_csr(topo)
+    ref, Z = [], X0
+    for _ in range(K):
+        Z = M.mix_once(Z, rp, cl, w)
+        ref.append(np.float32(M.deviation(Z).max()))
+    W = engine.DeviceCsr(csr, cuda)
+    Pp = -(-P // 64) * 64
+    Xd = torch.nn.functional.pad(torch.from_numpy(X0).to(cuda), (0, Pp - P))
+    Yd = torch.empty_like(Xd)
+    trace = torch.empty(K, device=cuda)
+    engine.mix_rounds_trace(W, Xd, Yd, K, trace)
+    traced = [np.float32(v) for v in trace.tolist()]
+    m = Mixer({k: init[k].to(cuda) for k in keys}, topo, logging.getLogger("tie"))
+    m._dev()
+    recheck = [m._recheck_deviation(W, Xd, r + 1, P) for r in range(K)]
+    cands = [r for r in range(1, K) if traced[r] != ref[r] and recheck[r] == ref[r]
+             and ref[r - 1] > max(traced[r], ref[r])]
+    assert cands, "no round where the traced value and numpy's differ"
+    for r in cands[:3]:
+        lo = min(traced[r], ref[r])
+        eps = float(np.nextafter(lo, np.float32(np.inf)))   # lo < eps <= the other one
+        _, want_n = M.mixer_mix(X0, rp, cl, w, times=1, eps=eps)
+        if ref[r] < eps:
+            assert want_n == r + 1      # the reference stops exactly at this round
+        models = {k: ANNModel(60, 40, 10).to(cuda) for k in keys}
+        for k in keys:
+            models[k].load_state_dict(init[k].state_dict())
+        got_n = Mixer(models, topo, logging.getLogger("tie")).mix(times=1, eps=eps)
+        assert got_n == want_n, (r, traced[r], ref[r], eps)

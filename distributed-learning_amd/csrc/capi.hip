@@ -165,7 +165,8 @@ int plan_mix(const dl_mix_args *a, Plan *pl) {
     std::memset(pl, 0, sizeof *pl);
     const int32_t R = a->W.n_rows + a->n_halo;
     const int32_t nnz = a->W.nnz;
-    const bool want_dev = a->dev_sq || a->dev_max || a->mean;
+    // the halo round's column sums use the same LDS scratch as the fused deviation
+    const bool want_dev = a->dev_sq || a->dev_max || a->mean || a->colsum_out;
     pl->dev = want_dev;
     const int reg = a->W.uniform_row_nnz > 0 ? 1 : 0;
     const int32_t n_w = (reg && a->W.shared_row_weights) ? a->W.uniform_row_nnz : nnz;
@@ -243,6 +244,9 @@ int plan_mix(const dl_mix_args *a, Plan *pl) {
     if (a->W.n_rows > 4 * 65535)
         return fail(DL_ERR_UNSUPPORTED, "dl_mix_round: %d rows exceed the gather path limit",
                     a->W.n_rows);
+    if (a->mean_prev || a->colsum_out)
+        return fail(DL_ERR_UNSUPPORTED, "dl_mix_round: the lagged halo deviation needs the LDS "
+                                        "tile kernel; this graph takes the gather path");
     pl->pub.path = 2;
     pl->pub.grid = (int32_t)(((a->n_params + 255) / 256) * ((a->W.n_rows + 3) / 4));
     pl->pub.regular = reg;
@@ -276,10 +280,17 @@ int check_mix_args(const dl_mix_args *a) {
         return fail(DL_ERR_INVALID, "dl_mix_round: uniform_row_nnz * n_rows != nnz");
     if (W.shared_row_weights && W.uniform_row_nnz <= 0)
         return fail(DL_ERR_INVALID, "dl_mix_round: shared_row_weights needs uniform_row_nnz > 0");
-    if ((a->dev_sq || a->dev_max || a->mean) && a->n_halo > 0)
+    if ((a->mean_prev || a->colsum_out) && a->n_halo == 0)
+        return fail(DL_ERR_INVALID, "dl_mix_round: mean_prev / colsum_out are for halo rounds "
+                                    "(n_halo > 0); local rounds fuse the exact deviation");
+    if (a->mean && a->n_halo > 0)
+        return fail(DL_ERR_INVALID, "dl_mix_round: the column mean of a halo round is global: "
+                                    "use colsum_out and an all-reduce");
+    if ((a->dev_sq || a->dev_max || a->mean_prev || a->colsum_out) && a->n_halo > 0 &&
+        !(a->mean_prev && a->colsum_out && a->dev_sq))
         return fail(DL_ERR_INVALID,
-                    "dl_mix_round: fused deviation needs every agent local (n_halo == 0); use "
-                    "dl_column_sum + dl_deviation with a global mean");
+                    "dl_mix_round: a halo round's deviation is the lagged one: mean_prev, "
+                    "colsum_out and dev_sq together (or dl_column_sum + dl_deviation after it)");
     const size_t tiled_b = a->tile_cols > 0 ? (size_t)((a->n_params + a->tile_cols - 1) /
                                                        a->tile_cols) * a->tile_cols * W.n_rows * 4
                                             : 0;
@@ -327,6 +338,10 @@ dl::TileArgs tile_args(const dl_mix_args *a) {
     if (a->g) vec = vec && aligned16(a->g) && a->ldg % 4 == 0;
     if (a->halo) vec = vec && aligned16(a->halo) && a->ldh % 4 == 0;
     if (a->mean) vec = vec && aligned16(a->mean);
+    if (a->mean_prev) vec = vec && aligned16(a->mean_prev);
+    if (a->colsum_out) vec = vec && aligned16(a->colsum_out);
+    t.mean_prev = a->mean_prev;
+    t.colsum_out = a->colsum_out;
     // the float4 kernel addresses rows with 32-bit byte offsets from the tile base
     const int64_t lim = (int64_t)1 << 32;
     const int64_t R = a->W.n_rows;
@@ -814,10 +829,13 @@ int dl_mix_round(const dl_mix_args *args, void *workspace, size_t ws_bytes, dl_s
     hipStream_t s = static_cast<hipStream_t>(stream);
     const int32_t Nr = args->W.n_rows;
     char *ws = static_cast<char *>(workspace);
-    if (pl.dev && (!ws || (reinterpret_cast<uintptr_t>(ws) & 15u)))
+    dl::TileArgs t = tile_args(args);
+    // halo rounds with the lagged deviation: partials only when the deviation of x is asked for
+    const bool lag = dl::tile_lag(t);
+    const bool parts = pl.dev;   // a lagged halo round always writes its deviation partials
+    if (parts && (!ws || (reinterpret_cast<uintptr_t>(ws) & 15u)))
         return fail(DL_ERR_WORKSPACE, "dl_mix_round: deviation outputs need a 16-byte aligned "
                                       "workspace of dl_mix_workspace_bytes()");
-    dl::TileArgs t = tile_args(args);
     const bool sgd = args->g != nullptr;
     if (pl.pub.path == 4 && !t.vec) {   // the register-CSR kernel is FAST-only: gather instead
         pl.pub.path = 2;
@@ -844,12 +862,12 @@ int dl_mix_round(const dl_mix_args *args, void *workspace, size_t ws_bytes, dl_s
         int grid_full = (int)(n_full < pl.pub.grid ? n_full : pl.pub.grid);
         int grid_tail = (int)(n_tail < pl.pub.grid ? n_tail : pl.pub.grid);
         const size_t need = align_up((size_t)(grid_full + grid_tail) * Nr * 4);
-        if (pl.dev && ws_bytes < need)
+        if (parts && ws_bytes < need)
             return fail(DL_ERR_WORKSPACE, "dl_mix_round: workspace %zu < %zu bytes", ws_bytes, need);
         t.csr_off = pl.csr_off;
         t.scratch_off = pl.scratch_off;
-        float *partial = pl.dev ? reinterpret_cast<float *>(ws) : nullptr;
-        if (pl.dev) t.dev_max_zero = reinterpret_cast<unsigned int *>(args->dev_max);
+        float *partial = parts ? reinterpret_cast<float *>(ws) : nullptr;
+        if (parts) t.dev_max_zero = reinterpret_cast<unsigned int *>(args->dev_max);
         int lds = pl.pub.lds_bytes;
         if (const char *v = getenv("DLAMD_LDS_MIN")) {  // measurement knob: LDS per workgroup
             const int m = atoi(v);                        // bounds workgroups per CU
@@ -869,13 +887,13 @@ int dl_mix_round(const dl_mix_args *args, void *workspace, size_t ws_bytes, dl_s
             if (reg_csr) return fail(DL_ERR_INVALID, "dl_mix_round: register-CSR plan with a tail");
             t.n_tiles = (int32_t)n_tail;
             t.col_base = n_full * T;
-            t.dev_partial = pl.dev ? partial + (size_t)grid_full * Nr : nullptr;
+            t.dev_partial = parts ? partial + (size_t)grid_full * Nr : nullptr;
             hipError_t e = dl::launch_mix_tile(t, pl.chunks, sgd, pl.dev, true, grid_tail,
                                                lds, false, s);
             if (e != hipSuccess) return hip_fail(e, "mix_tile_kernel (tail) launch");
         }
-        if (pl.dev) {
-            if (Nr <= 1) return zero_deviation(Nr, args->dev_sq, args->dev_max, s);
+        if (parts) {
+            if (Nr <= 1 && !lag) return zero_deviation(Nr, args->dev_sq, args->dev_max, s);
             hipError_t e = dl::launch_dev_reduce(partial, grid_full + grid_tail, Nr, args->dev_sq,
                                                  args->dev_max, s, true);
             if (e != hipSuccess) return hip_fail(e, "dev_reduce launch");

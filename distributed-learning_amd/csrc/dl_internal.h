@@ -51,6 +51,8 @@ struct TileArgs {
     float *mean;         // [n_params] nullable
     unsigned int *dev_max_zero;  // nullable: workgroup 0 zeroes it (dev_reduce's atomicMax target,
                                  // so that launch needs no memset of its own)
+    const float *mean_prev;      // halo rounds: global column mean of x (lagged deviation)
+    float *colsum_out;           // halo rounds: this rank's column sums of y
 };
 
 // LDS bytes the staged CSR needs (0 if it cannot be staged: > 65535 rows/entries).
@@ -64,6 +66,10 @@ uint32_t csr_lds_bytes(int32_t n_rows, int32_t nnz, int32_t regular, int32_t n_w
 
 hipError_t launch_mix_tile(const TileArgs &a, int chunks, bool sgd, bool dev, bool mix, int grid,
                            int lds_bytes, bool fast, hipStream_t s);
+// true when a launch of this plan runs the halo instantiation with the lagged deviation
+inline bool tile_lag(const TileArgs &a) {
+    return a.n_src > a.n_rows && (a.mean_prev != nullptr || a.colsum_out != nullptr);
+}
 hipError_t launch_mix_gather(const TileArgs &a, bool sgd, hipStream_t s);
 // Tile kernel with the CSR in registers (regular graphs of 5 entries per row whose CSR does not
 // fit LDS beside the tile): FAST path only, no halo, chunks 1, <= 4 rows per thread.

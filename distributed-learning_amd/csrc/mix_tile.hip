@@ -120,7 +120,12 @@ __device__ __forceinline__ float4 *at(float *base, uint32_t off) {
 // Tiles cover columns [col_base + t*T, ...) for t < n_tiles.  Lanes whose row does not exist
 // (the last, ragged pass) re-read row 0 -- an L1 hit -- and never write LDS or y, so every
 // pass is straight-line code and the loads of the next tile stay in flight during the mix.
-template <int C, int KV, bool SGD, bool DEV, bool MIX, bool HALO, bool FAST, int RD = 0>
+// LAG  : halo rounds only: ||x_a - mean_prev||^2 of every local input row while it is staged
+//        (the deviation of the previous round's iterate against its all-reduced global mean) and
+//        this rank's column sums of the stepped inputs t into colsum_out -- all-reduced over the
+//        ranks, the numerator of the next mean_prev (sum(W t) = sum(t): W doubly stochastic).
+template <int C, int KV, bool SGD, bool DEV, bool MIX, bool HALO, bool FAST, int RD = 0,
+          bool LAG = false>
 __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float4 *tile = reinterpret_cast<float4 *>(smem);
@@ -183,6 +188,10 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
     float4 *scratch = reinterpret_cast<float4 *>(smem + a.scratch_off);
 
     float4 px[KV], pg[KV];
+    float4 pm = zero4();             // LAG: this lane's chunk of mean_prev, prefetched with px
+    float lacc[LAG ? KV : 1];        // LAG: per-pass partial ||x - mean_prev||^2 of the chunk
+#pragma unroll
+    for (int k = 0; k < (LAG ? KV : 1); ++k) lacc[k] = 0.f;
     // per-agent ||y - mean||^2 accumulators, spread over the C lanes of a row group: lane c keeps
     // the passes k with k % C == c (slot k / C), so ceil(KV / C) registers instead of KV.
     constexpr int ND = KV <= C ? 1 : KV / C;
@@ -192,6 +201,9 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
 
     auto prefetch = [&](int tile_id) {
         const int64_t col0 = a.col_base + (int64_t)tile_id * T;
+        if (LAG)
+            pm = FAST ? *reinterpret_cast<const float4 *>(a.mean_prev + col0 + 4 * c)
+                      : ld4(a.mean_prev, col0 + 4 * c, P, false);
         if (FAST && HALO) {
             // local rows from x/g (32-bit offsets), halo rows from the halo buffer (row-major,
             // ldh); the per-lane base select keeps every pass straight-line code
@@ -330,25 +342,36 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
             for (int k = 0; k < KV; ++k) {
                 const int r = s + k * SLOTS;
                 float4 t = px[k];
+                // lagged deviation of the input, local rows only: this lane's chunk of
+                // ||x_r - mean_prev||^2, summed over the row group's lanes once, at the end
+                if (LAG && r < Nr) {
+                    const float dx = t.x - pm.x, dy = t.y - pm.y;
+                    const float dz = t.z - pm.z, dw = t.w - pm.w;
+                    lacc[k] += (dx * dx + dy * dy) + (dz * dz + dw * dw);
+                }
                 if (SGD && (!HALO || r < Nr)) t = local_step(t, pg[k], a.lr);
                 if (r < R) {
                     tile[r * C + c] = t;
-                    if (DEV) add4(cst, t);
+                    if (DEV || (LAG && r < Nr)) add4(cst, t);
                 }
             }
             // mean(W t) = mean(t) when W is doubly stochastic: reduce the column sums of the
-            // inputs under the staging barrier instead of re-mixing the tile afterwards
+            // inputs under the staging barrier instead of re-mixing the tile afterwards.  A halo
+            // round (LAG) publishes its local rows' sums of t: all-reduced over the ranks they are
+            // the sum of the whole (doubly stochastic) round's output
             const bool mfi = DEV && a.mean_from_inputs;
-            if (mfi) {
+            constexpr bool lsum = LAG;
+            if (mfi || lsum) {
 #pragma unroll
                 for (int m = C; m < 64; m <<= 1) cst = shfl_xor4(cst, m);
                 if ((tid & 63) < C) scratch[(tid >> 6) * C + (tid & 63)] = cst;
             }
             __syncthreads();
             float4 mean_t = zero4();
-            if (mfi) {
+            if (mfi || lsum) {
 #pragma unroll
                 for (int wv = 0; wv < NT / 64; ++wv) add4(mean_t, scratch[wv * C + c]);
+                if (lsum && s == 0) st4(a.colsum_out, col0 + 4 * c, P, FAST, mean_t);
                 const float n = (float)Nr;
                 mean_t.x = mean_t.x / n;
                 mean_t.y = mean_t.y / n;
@@ -412,6 +435,17 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
                 if (s + k * SLOTS < Nr) dev_add(k, cur[k], mean);
         }
         __syncthreads();  // tile and scratch are rewritten by the next iteration
+    }
+    if (LAG) {
+#pragma unroll
+        for (int k = 0; k < (LAG ? KV : 1); ++k) {
+            float v = lacc[k];
+#pragma unroll
+            for (int m = 1; m < C; m <<= 1) v += __shfl_xor(v, m);   // over the row group
+            const int ag = s + k * SLOTS;
+            if (c == 0 && ag < Nr) a.dev_partial[(int64_t)blockIdx.x * Nr + ag] = v;
+        }
+        if (a.dev_max_zero != nullptr && blockIdx.x == 0 && tid == 0) *a.dev_max_zero = 0u;
     }
     if (DEV) {
 #pragma unroll
@@ -568,9 +602,10 @@ __global__ void __launch_bounds__(1024) stream_triad_tile_kernel(const float4 *_
     }
 }
 
-template <int C, int KV, bool SGD, bool DEV, bool MIX, bool HALO, bool FAST, int RD = 0>
+template <int C, int KV, bool SGD, bool DEV, bool MIX, bool HALO, bool FAST, int RD = 0,
+          bool LAG = false>
 hipError_t launch_one(const TileArgs &a, int grid, int lds, hipStream_t s) {
-    auto k = mix_tile_kernel<C, KV, SGD, DEV, MIX, HALO, FAST, RD>;
+    auto k = mix_tile_kernel<C, KV, SGD, DEV, MIX, HALO, FAST, RD, LAG>;
     hipError_t e = allow_full_lds(reinterpret_cast<const void *>(k));
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k, dim3(grid), dim3(kTileThreads), lds, s, a);
@@ -581,9 +616,13 @@ template <int C, int KV, bool FAST>
 hipError_t launch_mode(const TileArgs &a, bool sgd, bool dev, bool mix, int grid, int lds,
                        hipStream_t s) {
     if (!mix) return launch_one<C, KV, false, true, false, false, FAST>(a, grid, lds, s);
-    if (a.n_src > a.n_rows)  // halo rows: no fused deviation (needs the global mean)
+    if (a.n_src > a.n_rows) {  // halo rows: the exact deviation needs the global mean
+        if (tile_lag(a))        // lagged: previous iterate vs mean_prev, colsum_out for the next
+            return sgd ? launch_one<C, KV, true, false, true, true, FAST, 0, true>(a, grid, lds, s)
+                       : launch_one<C, KV, false, false, true, true, FAST, 0, true>(a, grid, lds, s);
         return sgd ? launch_one<C, KV, true, false, true, true, FAST>(a, grid, lds, s)
                    : launch_one<C, KV, false, false, true, true, FAST>(a, grid, lds, s);
+    }
     if (sgd) return dev ? launch_one<C, KV, true, true, true, false, FAST>(a, grid, lds, s)
                         : launch_one<C, KV, true, false, true, false, FAST>(a, grid, lds, s);
     return dev ? launch_one<C, KV, false, true, true, false, FAST>(a, grid, lds, s)

@@ -88,6 +88,28 @@ __device__ __forceinline__ void pipeline2(int ns, Load load, Store store, Comput
     }
 }
 
+// pipeline2 whose first two slices were issued by the caller (A = slice 0, B = slice 1): a phase
+// whose weights were requested during the previous phase's last MFMAs starts on data that has
+// already landed instead of waiting a full HBM latency with the matrix cores idle.
+template <typename Set, typename Load, typename Store, typename Compute>
+__device__ __forceinline__ void pipeline2_pre(int ns, Set &A, Set &B, Load load, Store store,
+                                              Compute compute) {
+    for (int s = 0; s < ns; s += 2) {
+        store(A);
+        __syncthreads();
+        if (s + 2 < ns) load(A, s + 2);
+        compute(s);
+        __syncthreads();
+        if (s + 1 < ns) {
+            store(B);
+            __syncthreads();
+            if (s + 3 < ns) load(B, s + 3);
+            compute(s + 1);
+            __syncthreads();
+        }
+    }
+}
+
 // Same, with two LDS images: slice s + 1 is written into the other image while the MFMAs read
 // slice s, so each slice costs one barrier and the LDS writes overlap the matrix work.  The
 // register set of slice s + 1 was issued two compute phases before it is stored.
@@ -353,40 +375,58 @@ __device__ __forceinline__ void epi_rows64_t(const f32x4 (&acc)[5], F f) {
 }
 
 // Forward layer on an LDS-resident input: H = act(Hin W^T + b), K = N = dh, W staged by slices.
+// A / B hold W's slices 0 and 1 (issued by the caller, ``prefetch_w``); ``next`` runs after the
+// last MFMAs, before the epilogue -- where the following phase's first slices are requested.
 template <typename M>
+__device__ __forceinline__ void prefetch_w(RowSlice<160> &A, RowSlice<160> &B, const M &W, int dh) {
+    A.load(W, dh, dh, 0);
+    B.load(W, dh, dh, BK);
+}
+template <typename M>
+__device__ __forceinline__ void prefetch_wt(ColSlice &A, ColSlice &B, const M &W, int dk, int dh) {
+    A.load(W, dh, dk, 0);
+    if (dk > BK) B.load(W, dh, dk, BK);
+}
+
+template <typename M, typename Next>
 __device__ __forceinline__ void forward_hidden(const M &W, const M &bias, int dh, const float *Hin,
-                                               float *Hout, float *stage, int layer) {
+                                               float *Hout, float *stage, int layer,
+                                               RowSlice<160> &A, RowSlice<160> &B, Next next) {
     f32x4 acc[5];
     zero(acc);
     float bv[5];
     load_bias5(bias, dh, bv);
-    pipeline2<RowSlice<160>>(
-        (dh + BK - 1) / BK,
+    pipeline2_pre<RowSlice<160>>(
+        (dh + BK - 1) / BK, A, B,
         [&](RowSlice<160> &w, int s) { w.load(W, dh, dh, s * BK); },
         [&](const RowSlice<160> &w) { w.store(stage); },
         [&](int s) {
             const int k0 = s * BK;
             mma_rows64<false>(acc, Hin + k0, LDH, stage);
         });
+    next();
     epi_rows64_t(acc, [&](int m, int n, int t, float v) {
         if (n < dh) Hout[m * LDH + n] = act_fwd(layer, v + bv[t]);
     });
 }
 
-// Backward through a hidden layer: Hio <- (dZ W) * act'(Hio)  (in place), K = dk rows of W.
-template <typename M>
+// Backward through a hidden layer: Hio <- (dZ W) * act'(Hio)  (in place), K = dk rows of W;
+// A / B hold W's slices 0 and 1 (``prefetch_wt``), ``next`` as above.
+template <typename M, typename Next>
 __device__ __forceinline__ void backward_dz(const M &W, int dk, int dh, const float *dZ, int ldz,
-                                            float *Hio, float *stage, int layer) {
+                                            float *Hio, float *stage, int layer, ColSlice &A,
+                                            ColSlice &B, Next next) {
     f32x4 acc[5];
     zero(acc);
-    pipeline2<ColSlice>(
-        (dk + BK - 1) / BK,
+    pipeline2_pre<ColSlice>(
+        (dk + BK - 1) / BK, A, B,
         [&](ColSlice &w, int s) { w.load(W, dh, dk, s * BK); },
         [&](const ColSlice &w) { w.store(stage); },
         [&](int s) {
             const int k0 = s * BK;
             mma_rows64<true>(acc, dZ + k0, ldz, stage);
         });
+    next();
     epi_rows64(acc, [&](int m, int n, float v) {
         if (n < dh) Hio[m * LDH + n] = v * act_grad(layer, Hio[m * LDH + n]);
     });
@@ -475,6 +515,8 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
     __syncthreads();
     if (tid < MB) H1[tid * LDH + dh] = 1.f;   // ones column: db2 in dW2's MFMAs
 
+    RowSlice<160> wa, wb;   // a forward phase's first two W slices, requested one phase early
+    ColSlice ta, tb;        // the same for the backward phases
     // ---- layer 1: H1 = relu(x W1^T + b1), K = din from HBM: x and W1 slices double-buffered in
     // LDS (the H2/H3 space, free until layer 2), the next two register-prefetched
     {
@@ -510,6 +552,7 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
                 mma_rows64<false>(acc, H2 + buf * IMG, LDS1, H2 + buf * IMG + MB * LDS1);
 #endif
             });
+        prefetch_w(wa, wb, mat(Xr, o_w2, dh), dh);   // layer 2's first slices
         epi_rows64_t(acc, [&](int m, int n, int t, float v) {
             if (n < dh) H1[m * LDH + n] = act_fwd(0, v + bv[t]);
         });
@@ -520,7 +563,8 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
     }
     __syncthreads();
     STAMP(1);
-    forward_hidden(mat(Xr, o_w2, dh), mat(Xr, o_b2, 0), dh, H1, H2, stage, 1);
+    forward_hidden(mat(Xr, o_w2, dh), mat(Xr, o_b2, 0), dh, H1, H2, stage, 1, wa, wb,
+                   [&] { prefetch_w(wa, wb, mat(Xr, o_w3, dh), dh); });
     __syncthreads();
     STAMP(2);
     // the logits' operands from HBM (W4 image values, b4, this wave's labels), issued now so they
@@ -537,7 +581,8 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
     int lab[MB / 8];
 #pragma unroll
     for (int i = 0; i < MB / 8; ++i) lab[i] = p.labels[(int64_t)a * p.s_lab + wave + 8 * i];
-    forward_hidden(mat(Xr, o_w3, dh), mat(Xr, o_b3, 0), dh, H2, H3, stage, 2);
+    forward_hidden(mat(Xr, o_w3, dh), mat(Xr, o_b3, 0), dh, H2, H3, stage, 2, wa, wb,
+                   [&] { prefetch_wt(ta, tb, mat(Xr, o_w4, dh), dout, dh); });
     STAMP(3);
     // ---- logits Z = H3 W4^T + b4 (waves 0-3, one 16 x 16 tile each), W4 image [16][LDW4]
 #pragma unroll
@@ -605,19 +650,21 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
     }
     __syncthreads();
     // ---- dZ3 = (dZ4 W4) * elu'(H3) in place, K = dout
-    backward_dz(mat(Xr, o_w4, dh), dout, dh, Zs, LDZ, H3, stage, 2);
+    backward_dz(mat(Xr, o_w4, dh), dout, dh, Zs, LDZ, H3, stage, 2, ta, tb,
+                [&] { prefetch_wt(ta, tb, mat(Xr, o_w3, dh), dh, dh); });
     __syncthreads();
     STAMP(5);
     weight_grad_hidden(H3, H2, dh, mat(Gr, o_w3, dh), mat(Gr, o_b3, 0));
     __syncthreads();
     STAMP(6);
-    backward_dz(mat(Xr, o_w3, dh), dh, dh, H3, LDH, H2, stage, 1);     // dZ2 into H2
+    backward_dz(mat(Xr, o_w3, dh), dh, dh, H3, LDH, H2, stage, 1, ta, tb,     // dZ2 into H2
+                [&] { prefetch_wt(ta, tb, mat(Xr, o_w2, dh), dh, dh); });
     __syncthreads();
     STAMP(7);
     weight_grad_hidden(H2, H1, dh, mat(Gr, o_w2, dh), mat(Gr, o_b2, 0));
     __syncthreads();
     STAMP(8);
-    backward_dz(mat(Xr, o_w2, dh), dh, dh, H2, LDH, H1, stage, 0);     // dZ1 into H1
+    backward_dz(mat(Xr, o_w2, dh), dh, dh, H2, LDH, H1, stage, 0, ta, tb, [] {});  // dZ1 into H1
     __syncthreads();
     STAMP(9);
     // ---- dW1 = dZ1^T x [dh x din] by 256-column chunks of x, staged in the H2/H3 space (free

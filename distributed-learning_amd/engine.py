@@ -151,9 +151,13 @@ class Workspace:
 
 
 def mix_round(W: DeviceCsr, X, Y, G=None, lr=0.0, halo=None, dev_sq=None, dev_max=None,
-              mean=None, workspace: Workspace = None, tiled=None):
+              mean=None, workspace: Workspace = None, tiled=None, mean_prev=None,
+              colsum_out=None):
     """One consensus round on the current stream: Y = W (X - lr G) [+ deviation of Y].
-    ``tiled=(n_params, tile_cols)``: X, G, Y are in the column-tiled layout."""
+    ``tiled=(n_params, tile_cols)``: X, G, Y are in the column-tiled layout.
+    Halo rounds (``halo`` rows): ``mean_prev`` (the global column mean of X), ``colsum_out`` and
+    ``dev_sq`` together give the lagged deviation -- dev_sq = ||x_a - mean_prev||^2 of the
+    INPUT rows, colsum_out = this rank's column sums of X - lr G (include/dlamd.h)."""
     lib = _lib.load()
     if tiled is not None:
         P = tiled[0]
@@ -161,6 +165,12 @@ def mix_round(W: DeviceCsr, X, Y, G=None, lr=0.0, halo=None, dev_sq=None, dev_ma
     else:
         P = X.shape[1]
         args = mix_args(W, X, Y, G, lr, halo, dev_sq, dev_max, mean)
+    for name, t in (("mean_prev", mean_prev), ("colsum_out", colsum_out)):
+        if t is not None:
+            if t.dtype != torch.float32 or t.device != W.device or t.numel() < P or \
+                    t.dim() != 1 or t.stride(0) != 1:
+                raise ValueError(f"{name} must be a contiguous float32 [n_params] device tensor")
+            setattr(args, name, _lib.ptr(t))
     workspace = workspace or Workspace(W.device)
     wp, wn = workspace.ptr_size(lib.dl_mix_workspace_bytes(W.n_rows, W.n_src - W.n_rows, P))
     _lib.check(lib.dl_mix_round(ctypes.byref(args), wp, wn, _lib.stream_handle(W.device)),

@@ -306,8 +306,14 @@ class HipOps:
     def step_rows(self, X, rows, out, G=None, lr=0.0):
         return self.E.step_rows(X, rows, out, G=G, lr=lr)
 
-    def mix(self, W, X, Y, G=None, lr=0.0, halo=None):
-        self.E.mix_round(W, X, Y, G=G, lr=lr, halo=halo, workspace=self.ws)
+    def mix(self, W, X, Y, G=None, lr=0.0, halo=None, lag=None):
+        """lag = (mean_prev, colsum_out, dev_sq): the lagged deviation of a halo round."""
+        if lag is None:
+            self.E.mix_round(W, X, Y, G=G, lr=lr, halo=halo, workspace=self.ws)
+        else:
+            mean_prev, colsum, dsq = lag
+            self.E.mix_round(W, X, Y, G=G, lr=lr, halo=halo, dev_sq=dsq, mean_prev=mean_prev,
+                             colsum_out=colsum, workspace=self.ws)
 
     def column_sum(self, X):
         return self.E.column_sum(X)
@@ -338,7 +344,7 @@ class HaloShard:
     """One rank's agent block with halo exchange (row-major X[n_local, P])."""
 
     def __init__(self, plan: RankPlan, n_params, device, transport, chunk_cols=None,
-                 n_agents_total=None, ops=None):
+                 n_agents_total=None, ops=None, doubly_stochastic=True):
         self.plan = plan
         self.P = int(n_params)
         self.device = torch.device(device)
@@ -354,6 +360,10 @@ class HaloShard:
         self.X = staggered_zeros((plan.n_local, self.P), 0, self.device)
         self.Y = staggered_zeros((plan.n_local, self.P), 1, self.device)
         self._bufs = {}
+        self.mean_prev = None      # global column mean of X (lagged deviation), once known
+        # the lagged deviation needs sum(W t) = sum(t): W doubly stochastic over ALL agents
+        # (column sums of the global W are not visible to one rank; the caller states it)
+        self.doubly_stochastic = bool(doubly_stochastic)
 
     def _buffers(self, slot, width):
         """Send/halo buffers of one pipeline slot; chunks alternate between two slots so the
@@ -376,20 +386,53 @@ class HaloShard:
             self.ops.step_rows(self.X[:, c0:c1], rows, send[q], G=Gc, lr=lr)
         return send, halo, recv
 
-    def mix_chunk(self, c0, c1, halo, G=None, lr=0.0):
+    def mix_chunk(self, c0, c1, halo, G=None, lr=0.0, lag=None):
         Gc = G[:, c0:c1] if G is not None else None
         self.ops.mix(self.W, self.X[:, c0:c1], self.Y[:, c0:c1], G=Gc, lr=lr,
-                     halo=halo if self.plan.n_halo else None)
+                     halo=halo if self.plan.n_halo else None, lag=lag)
 
     def chunks(self):
         return [(c, min(c + self.chunk, self.P)) for c in range(0, self.P, self.chunk)]
 
-    def round(self, G=None, lr=0.0):
+    def round(self, G=None, lr=0.0, deviation=False):
         """One round: the halo exchange of chunk j+1 is in flight while chunk j is mixed.
         (Stream order makes the reuse safe: a slot's next exchange is posted after the mix that
-        read it, and the collective waits for the current stream.)"""
-        chunks = self.chunks()
+        read it, and the collective waits for the current stream.)
 
+        deviation=True: the lagged deviation, with no HBM pass of its own.  Each chunk's kernel
+        also measures its INPUT rows -- the previous round's iterate, which it stages anyway --
+        against that iterate's global column mean (``mean_prev``), and publishes this rank's
+        column sums of the stepped inputs; one all-reduce of those sums (n_params floats) gives
+        the next round's ``mean_prev`` (the global W is doubly stochastic, so the sum of the
+        round's output is the sum of its stepped inputs).  Returns (dev_sq of my agents,
+        global max deviation) of the iterate this round started from -- the value
+        ``deviation()`` would have returned before the round.  (Halo rounds cannot fuse the
+        deviation of their own output: its global mean is only known after every rank's round.)
+        The first lagged round computes the starting mean with one column-sum pass."""
+        chunks = self.chunks()
+        lag = None
+        if deviation:
+            if self.plan.n_halo == 0 or not self.doubly_stochastic:
+                dev = self.deviation()
+                self._mix_all(chunks, G, lr, None)
+                return dev
+            if self.mean_prev is None:
+                self.mean_prev = self._global_mean(self.X)
+            colsum = torch.empty(self.P, dtype=torch.float32, device=self.device)
+            parts = torch.empty(len(chunks), self.plan.n_local, dtype=torch.float32,
+                                device=self.device)
+            lag = (self.mean_prev, colsum, parts)
+        self._mix_all(chunks, G, lr, lag)
+        if lag is None:
+            return None
+        dev_sq = parts.sum(0)
+        self.transport.all_reduce_(colsum, "sum")
+        self.mean_prev = colsum / float(self.n_total)
+        dev_max = torch.sqrt(dev_sq.max()).reshape(1)
+        self.transport.all_reduce_(dev_max, "max")
+        return dev_sq, dev_max
+
+    def _mix_all(self, chunks, G, lr, lag):
         def post(j):
             c0, c1 = chunks[j]
             send, halo, recv = self.pack(j % 2, c0, c1, G, lr)
@@ -401,9 +444,15 @@ class HaloShard:
             works, halo = pend
             for w in works:
                 w.wait()
-            self.mix_chunk(c0, c1, halo, G, lr)
+            cl = None if lag is None else (lag[0][c0:c1], lag[1][c0:c1], lag[2][j])
+            self.mix_chunk(c0, c1, halo, G, lr, cl)
             pend = nxt
         self.X, self.Y = self.Y, self.X
+
+    def _global_mean(self, X):
+        colsum = self.ops.column_sum(X)
+        self.transport.all_reduce_(colsum, "sum")
+        return colsum / float(self.n_total)
 
     def deviation(self):
         """Global ||x_a - mean||: column sums all-reduced into the global mean, then the local

@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define DLAMD_ABI_VERSION 3
+#define DLAMD_ABI_VERSION 4
 
 typedef void *dl_stream_t; /* hipStream_t; NULL = the legacy default stream */
 
@@ -97,19 +97,33 @@ typedef struct dl_mix_args {
     const float *halo;  /* nullable [n_halo, ldh]: remote rows, already stepped */
     int64_t ldh;
     int32_t n_halo;
-    float *dev_sq;      /* nullable [n_rows]: ||y_a - mean_b(y_b)||^2  (needs n_halo == 0) */
-    float *dev_max;     /* nullable [1]: max_a sqrt(dev_sq[a])          (needs n_halo == 0) */
+    float *dev_sq;      /* nullable [n_rows]: ||y_a - mean_b(y_b)||^2  (n_halo > 0: see mean_prev) */
+    float *dev_max;     /* nullable [1]: max_a sqrt(dev_sq[a])          (n_halo > 0: see mean_prev) */
     float *mean;        /* nullable [n_params]: mean_b(y_b)              (needs n_halo == 0) */
     int32_t tile_cols;  /* 0: x, g, y row-major with ld*.  T > 0: x, g, y in the column-tiled
                            layout [ceil(n_params/T)][n_rows][T] (each tile one contiguous block,
                            last tile zero-padded; ld* ignored); T must be the plan's tile_cols
                            (dl_mix_plan_query on the row-major args).  No halo rows. */
+    /* Agent-partitioned rounds (n_halo > 0) with the deviation pipelined one round behind: the
+     * global column mean of y needs every rank's rows, so this round's kernel publishes its
+     * share of it and measures the PREVIOUS round's iterate -- its input x, staged anyway --
+     * against the previous mean.  No HBM pass beyond the round's own. */
+    const float *mean_prev; /* nullable [n_params] (n_halo > 0 only; with colsum_out and dev_sq):
+                               the global column mean of x (the previous round's all-reduced
+                               colsum_out / N): dev_sq[a] = ||x_a - mean_prev||^2, dev_max =
+                               max sqrt (nullable). */
+    float *colsum_out;      /* nullable [n_params] (n_halo > 0 only): sum over this rank's rows of
+                               the stepped inputs t = x - lr*g, in a fixed order.  Summed over all
+                               ranks it is the column sum of the round's output when the global W
+                               is doubly stochastic (the numerator of the next mean_prev). */
 } dl_mix_args;
 
 /* Which kernel configuration dl_mix_round picks (introspection for tests and the bench). */
 typedef struct dl_mix_plan {
     int32_t path;       /* 1 = LDS tile kernel (all agents x T columns per tile), 2 = gather kernel,
-                           3 = multi-round LDS kernel (dl_mix_rounds) */
+                           3 = multi-round LDS kernel (dl_mix_rounds), 4 = tile kernel with the
+                           CSR in registers (regular graphs of 5 entries per row whose CSR does
+                           not fit LDS beside the tile) */
     int32_t tile_cols;  /* T: columns per tile (path 1) */
     int32_t grid;       /* workgroups launched */
     int32_t lds_bytes;  /* dynamic LDS per workgroup */

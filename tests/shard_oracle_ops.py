@@ -27,10 +27,16 @@ class OracleOps:
         out.copy_(torch.from_numpy(np.ascontiguousarray(Xn)))
         return out
 
-    def mix(self, W, X, Y, G=None, lr=0.0, halo=None):
+    def mix(self, W, X, Y, G=None, lr=0.0, halo=None, lag=None):
         T = X.numpy()
+        if lag is not None:     # lagged deviation of the input rows + sums of the stepped rows
+            mean_prev, colsum, dsq = lag
+            D = (T - mean_prev.numpy()).astype(np.float64)
+            dsq.copy_(torch.from_numpy((D * D).sum(1).astype(np.float32)))
         if G is not None:
             T = M.sgd_step(T, G.numpy(), lr)
+        if lag is not None:
+            colsum.copy_(torch.from_numpy(T.astype(np.float64).sum(0).astype(np.float32)))
         if halo is not None:
             T = np.concatenate([T, halo.numpy()])
         c = W.csr

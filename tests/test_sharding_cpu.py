@@ -58,7 +58,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, P, chunk, out_dir):
+def _worker(rank, world, port, P, chunk, out_dir, lag=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -77,25 +77,42 @@ def _worker(rank, world, port, P, chunk, out_dir):
                             n_agents_total=64, ops=OracleOps())
     sh.X = torch.from_numpy(X[plan.local].copy())
     Gl = torch.from_numpy(G[plan.local].copy())
+    lagged = []
     for _ in range(3):
-        sh.round(G=Gl, lr=0.05)
+        lagged.append(sh.round(G=Gl, lr=0.05, deviation=lag))
     dev_sq, dev_max = sh.deviation()
+    if lag:     # round i returned the deviation of the iterate it started from
+        for i, (dsq, dmax) in enumerate(lagged):
+            np.save(os.path.join(out_dir, f"lag{rank}_{i}.npy"), dsq.numpy())
+            np.save(os.path.join(out_dir, f"lagmax{rank}_{i}.npy"), dmax.numpy())
     np.save(os.path.join(out_dir, f"x{rank}.npy"), sh.X.numpy())
     np.save(os.path.join(out_dir, f"ids{rank}.npy"), plan.local)
     np.save(os.path.join(out_dir, f"dmax{rank}.npy"), dev_max.numpy())
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("chunk", [None, 7])
-def test_halo_rounds_over_gloo_equal_single_process(tmp_path, chunk):
+@pytest.mark.parametrize("chunk,lag", [(None, False), (7, False), (None, True), (7, True)])
+def test_halo_rounds_over_gloo_equal_single_process(tmp_path, chunk, lag):
+    """Real 2-rank gloo halo rounds equal the single-process oracle rounds bit for bit; with
+    deviation=True each round also returns the (lagged) deviation of the iterate it started from
+    -- measured inside the round, against the all-reduced column sums of the previous round's
+    stepped inputs -- within 1e-5 relative of the oracle's deviation of that iterate."""
     world, P = 2, 24
-    mp.spawn(_worker, args=(world, _free_port(), P, chunk, str(tmp_path)), nprocs=world,
+    mp.spawn(_worker, args=(world, _free_port(), P, chunk, str(tmp_path), lag), nprocs=world,
              join=True)
     csr = torus_csr(8, 8)
     rng = np.random.default_rng(0)
     X = rng.standard_normal((64, P), dtype=np.float32)
     G = rng.standard_normal((64, P), dtype=np.float32)
-    for _ in range(3):
+    for i in range(3):
+        if lag:
+            want = M.deviation(X)
+            for r in range(world):
+                ids = np.load(tmp_path / f"ids{r}.npy")
+                got = np.sqrt(np.load(tmp_path / f"lag{r}_{i}.npy"))
+                np.testing.assert_allclose(got, want[ids], rtol=1e-5)
+                np.testing.assert_allclose(np.load(tmp_path / f"lagmax{r}_{i}.npy")[0],
+                                           want.max(), rtol=1e-5)
         X = M.mix_once(M.sgd_step(X, G, 0.05), csr.rowptr, csr.col, csr.w)
     for r in range(world):
         ids = np.load(tmp_path / f"ids{r}.npy")

@@ -59,6 +59,58 @@ def test_virtual_ranks_equal_single_device(cuda, world, chunk):
         np.testing.assert_allclose(sh.dev[0].cpu().numpy(), dsq[ids].cpu().numpy(), rtol=1e-5)
 
 
+@pytest.mark.parametrize("world,chunk", [(2, None), (4, 300), (8, 1000)])
+def test_lagged_deviation_in_the_halo_round(cuda, world, chunk):
+    """HaloShard.round(deviation=True): the kernel measures its input rows against the previous
+    round's all-reduced mean and publishes the column sums of its stepped inputs (no HBM pass of
+    its own).  Iterates stay bit-identical to the single-device round; round i returns the
+    deviation of the iterate it started from within 1e-5 relative of ``GossipEngine.deviation``
+    on that iterate (the mean differs only by summation order)."""
+    from distributed_learning_amd import engine as E
+    R, C, P = 16, 16, 2048 + 36        # ragged tail tile
+    edges = torus_edges(R, C)
+    verts = list(range(R * C))
+    csr = from_edge_weights(edges, [best_constant_weight(edges, verts)] * len(edges), verts)
+    g = torch.Generator(device=cuda).manual_seed(7)
+    X = torch.randn(R * C, P, device=cuda, generator=g)
+    G = torch.randn(R * C, P, device=cuda, generator=g)
+    ref = E.GossipEngine(csr, P, device=cuda, X=X, layout="rows")
+    want = []
+    for _ in range(4):
+        want.append(ref.deviation())
+        ref.round(G=G, lr=0.01)
+    want = [(dsq.clone(), dmax.clone()) for dsq, dmax in want]
+    plans = sharding.halo_plans(csr, sharding.torus_block_partition(R, C, world))
+    tr = sharding.LocalTransport(world)
+    shards = []
+    for pl in plans:
+        sh = sharding.HaloShard(pl, P, cuda, tr.endpoint(pl.rank), chunk_cols=chunk,
+                                n_agents_total=R * C)
+        ids = torch.as_tensor(pl.local, device=cuda)
+        sh.X = X[ids].contiguous()
+        shards.append((sh, G[ids].contiguous(), ids))
+    errs = []
+
+    def run(sh, Gl):
+        try:
+            sh.got = [sh.round(G=Gl, lr=0.01, deviation=True) for _ in range(4)]
+        except Exception as e:  # pragma: no cover
+            errs.append(e)
+    ths = [threading.Thread(target=run, args=(sh, Gl)) for sh, Gl, _ in shards]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert not errs, errs
+    torch.cuda.synchronize()
+    full = ref.rows()
+    for sh, _, ids in shards:
+        assert torch.equal(sh.X.view(torch.int32), full[ids].view(torch.int32))
+        for (dsq, dmax), (wsq, wmax) in zip(sh.got, want):
+            np.testing.assert_allclose(dsq.cpu().numpy(), wsq[ids].cpu().numpy(), rtol=1e-5)
+            assert float(dmax.item()) == pytest.approx(float(wmax.item()), rel=1e-5)
+
+
 def _gloo_worker(rank, world, port, chunk, out_dir):
     """One rank of a real multi-process run on the shared GPU: torch.distributed gloo with the
     host-staged transport, the HIP halo path, checked against the single-device round."""

@@ -30,7 +30,8 @@ class DlMixArgs(ctypes.Structure):
     _fields_ = [("x", _vp), ("ldx", _i64), ("y", _vp), ("ldy", _i64), ("n_params", _i64),
                 ("W", DlCsr), ("g", _vp), ("ldg", _i64), ("lr", _f32), ("halo", _vp),
                 ("ldh", _i64), ("n_halo", _i32), ("dev_sq", _vp), ("dev_max", _vp),
-                ("mean", _vp), ("tile_cols", _i32), ("mean_prev", _vp), ("colsum_out", _vp)]
+                ("mean", _vp), ("tile_cols", _i32), ("mean_prev", _vp), ("colsum_out", _vp),
+                ("n_local_src", _i32)]
 
 
 class DlMixUntilArgs(ctypes.Structure):
@@ -140,7 +141,7 @@ SIGNATURES = {
     "dl_lds_slot_order": (_i32, [_i32, _i32, _vp, _i32, _i64, ctypes.c_uint64, _vp, _vp]),
 }
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 _lib = None
 
 

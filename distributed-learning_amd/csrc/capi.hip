@@ -135,10 +135,17 @@ int choose_tiled_chunks(int32_t R, uint32_t csr, bool want_dev, int32_t regular 
     return 0;
 }
 
+// Local source rows of a round: n_local_src, or n_rows when 0 (dlamd.h).
+inline int32_t local_src(const dl_mix_args *a) {
+    return a->n_local_src > 0 ? a->n_local_src : a->W.n_rows;
+}
+
 // Register-CSR plan (path 4) for c chunks, or false when it does not apply.
 bool plan_reg(const dl_mix_args *a, int c, bool want_dev, Plan *pl) {
     const int32_t R = a->W.n_rows;
-    if (a->n_halo > 0 || !dl::reg_csr_supported(c, R, a->W.uniform_row_nnz, 0)) return false;
+    if (a->n_halo > 0 || local_src(a) != R ||
+        !dl::reg_csr_supported(c, R, a->W.uniform_row_nnz, 0))
+        return false;
     const int64_t tile = (int64_t)R * c * 16;
     const int64_t scratch = want_dev ? (int64_t)(dl::kTileThreads / 64) * c * 16 : 0;
     if (tile + scratch > dl::kLdsBytes) return false;
@@ -163,7 +170,7 @@ bool plan_reg(const dl_mix_args *a, int c, bool want_dev, Plan *pl) {
 // Pick the kernel configuration for a mix round.
 int plan_mix(const dl_mix_args *a, Plan *pl) {
     std::memset(pl, 0, sizeof *pl);
-    const int32_t R = a->W.n_rows + a->n_halo;
+    const int32_t R = local_src(a) + a->n_halo;
     const int32_t nnz = a->W.nnz;
     // the halo round's column sums use the same LDS scratch as the fused deviation
     const bool want_dev = a->dev_sq || a->dev_max || a->mean || a->colsum_out;
@@ -247,6 +254,9 @@ int plan_mix(const dl_mix_args *a, Plan *pl) {
     if (a->mean_prev || a->colsum_out)
         return fail(DL_ERR_UNSUPPORTED, "dl_mix_round: the lagged halo deviation needs the LDS "
                                         "tile kernel; this graph takes the gather path");
+    if (local_src(a) != a->W.n_rows)
+        return fail(DL_ERR_UNSUPPORTED, "dl_mix_round: n_local_src != n_rows needs the LDS tile "
+                                        "kernel; this graph takes the gather path");
     pl->pub.path = 2;
     pl->pub.grid = (int32_t)(((a->n_params + 255) / 256) * ((a->W.n_rows + 3) / 4));
     pl->pub.regular = reg;
@@ -259,6 +269,15 @@ int check_mix_args(const dl_mix_args *a) {
     if (W.n_rows <= 0) return fail(DL_ERR_INVALID, "dl_mix_round: n_rows must be > 0 (got %d)", W.n_rows);
     if (a->n_params <= 0) return fail(DL_ERR_INVALID, "dl_mix_round: n_params must be > 0");
     if (a->n_halo < 0) return fail(DL_ERR_INVALID, "dl_mix_round: n_halo < 0");
+    if (a->n_local_src < 0) return fail(DL_ERR_INVALID, "dl_mix_round: n_local_src < 0");
+    const int32_t NL = local_src(a);
+    // an interior / boundary row set of an agent partition (outputs need not be source rows)
+    const bool part = NL != W.n_rows;
+    if ((int64_t)W.n_rows > (int64_t)NL + a->n_halo)
+        return fail(DL_ERR_INVALID, "dl_mix_round: n_rows %d > n_local_src + n_halo %lld",
+                    W.n_rows, (long long)NL + a->n_halo);
+    if (part && a->tile_cols != 0)
+        return fail(DL_ERR_INVALID, "dl_mix_round: n_local_src != n_rows needs row-major operands");
     if (W.nnz < 0) return fail(DL_ERR_INVALID, "dl_mix_round: nnz < 0");
     if (!a->x || !a->y || !W.row_ptr || (W.nnz > 0 && (!W.col || !W.w)))
         return fail(DL_ERR_INVALID, "dl_mix_round: null x/y/row_ptr/col/w");
@@ -280,13 +299,15 @@ int check_mix_args(const dl_mix_args *a) {
         return fail(DL_ERR_INVALID, "dl_mix_round: uniform_row_nnz * n_rows != nnz");
     if (W.shared_row_weights && W.uniform_row_nnz <= 0)
         return fail(DL_ERR_INVALID, "dl_mix_round: shared_row_weights needs uniform_row_nnz > 0");
-    if ((a->mean_prev || a->colsum_out) && a->n_halo == 0)
+    const bool halo_round = a->n_halo > 0 || part;
+    if ((a->mean_prev || a->colsum_out) && !halo_round)
         return fail(DL_ERR_INVALID, "dl_mix_round: mean_prev / colsum_out are for halo rounds "
-                                    "(n_halo > 0); local rounds fuse the exact deviation");
-    if (a->mean && a->n_halo > 0)
+                                    "(n_halo > 0 or n_local_src != n_rows); local rounds fuse "
+                                    "the exact deviation");
+    if (a->mean && halo_round)
         return fail(DL_ERR_INVALID, "dl_mix_round: the column mean of a halo round is global: "
                                     "use colsum_out and an all-reduce");
-    if ((a->dev_sq || a->dev_max || a->mean_prev || a->colsum_out) && a->n_halo > 0 &&
+    if ((a->dev_sq || a->dev_max || a->mean_prev || a->colsum_out) && halo_round &&
         !(a->mean_prev && a->colsum_out && a->dev_sq))
         return fail(DL_ERR_INVALID,
                     "dl_mix_round: a halo round's deviation is the lagged one: mean_prev, "
@@ -294,11 +315,11 @@ int check_mix_args(const dl_mix_args *a) {
     const size_t tiled_b = a->tile_cols > 0 ? (size_t)((a->n_params + a->tile_cols - 1) /
                                                        a->tile_cols) * a->tile_cols * W.n_rows * 4
                                             : 0;
-    const size_t xb = a->tile_cols ? tiled_b : ((size_t)(W.n_rows - 1) * a->ldx + a->n_params) * 4;
+    const size_t xb = a->tile_cols ? tiled_b : ((size_t)(NL - 1) * a->ldx + a->n_params) * 4;
     const size_t yb = a->tile_cols ? tiled_b : ((size_t)(W.n_rows - 1) * a->ldy + a->n_params) * 4;
     if (overlaps(a->x, xb, a->y, yb)) return fail(DL_ERR_INVALID, "dl_mix_round: y overlaps x");
     if (a->g) {
-        const size_t gb = a->tile_cols ? tiled_b : ((size_t)(W.n_rows - 1) * a->ldg + a->n_params) * 4;
+        const size_t gb = a->tile_cols ? tiled_b : ((size_t)(NL - 1) * a->ldg + a->n_params) * 4;
         if (overlaps(a->g, gb, a->y, yb)) return fail(DL_ERR_INVALID, "dl_mix_round: y overlaps g");
     }
     return DL_OK;
@@ -318,12 +339,13 @@ dl::TileArgs tile_args(const dl_mix_args *a) {
     t.col = a->W.col;
     t.w = a->W.w;
     t.n_rows = a->W.n_rows;
-    t.n_src = a->W.n_rows + a->n_halo;
+    t.n_loc = local_src(a);
+    t.n_src = t.n_loc + a->n_halo;
     t.nnz = a->W.nnz;
     t.regular = a->W.uniform_row_nnz;
     t.n_w = (a->W.uniform_row_nnz > 0 && a->W.shared_row_weights) ? a->W.uniform_row_nnz
                                                                    : a->W.nnz;
-    t.mean_from_inputs = (a->W.doubly_stochastic && a->n_halo == 0) ? 1 : 0;
+    t.mean_from_inputs = (a->W.doubly_stochastic && t.n_src == t.n_rows) ? 1 : 0;
     {
         // X, G and X' are streamed exactly once per round: non-temporal loads and stores keep
         // them out of L2/MALL (measured +1.5 % on c2).  DLAMD_NT_STORE/LOAD=0 disable them.
@@ -344,7 +366,7 @@ dl::TileArgs tile_args(const dl_mix_args *a) {
     t.colsum_out = a->colsum_out;
     // the float4 kernel addresses rows with 32-bit byte offsets from the tile base
     const int64_t lim = (int64_t)1 << 32;
-    const int64_t R = a->W.n_rows;
+    const int64_t R = t.n_loc > t.n_rows ? t.n_loc : t.n_rows;
     if (a->tile_cols > 0) {
         vec = aligned16(a->x) && aligned16(a->y) && (!a->g || aligned16(a->g)) &&
               (!a->mean || aligned16(a->mean));
@@ -406,7 +428,7 @@ int plan_rounds(const dl_mix_args *a, Plan *pl) {
     const int32_t R = a->W.n_rows;
     const bool want_dev = a->dev_sq || a->dev_max || a->mean;
     pl->dev = want_dev;
-    if (a->n_halo > 0)
+    if (a->n_halo > 0 || local_src(a) != a->W.n_rows)
         return fail(DL_ERR_UNSUPPORTED, "dl_mix_rounds: halo rows need one exchange per round");
     if (want_dev && !a->W.doubly_stochastic)
         return fail(DL_ERR_UNSUPPORTED, "dl_mix_rounds: the fused final deviation needs a doubly "
@@ -469,7 +491,7 @@ struct TracePlan {
 
 int plan_trace(const dl_mix_args *a, TracePlan *tp) {
     const int32_t N = a->W.n_rows;
-    if (a->n_halo > 0)
+    if (a->n_halo > 0 || local_src(a) != a->W.n_rows)
         return fail(DL_ERR_UNSUPPORTED, "dl_mix_rounds_trace: halo rows need one exchange per "
                                         "round");
     if (!a->W.doubly_stochastic)
@@ -833,6 +855,7 @@ int dl_mix_round(const dl_mix_args *args, void *workspace, size_t ws_bytes, dl_s
     // halo rounds with the lagged deviation: partials only when the deviation of x is asked for
     const bool lag = dl::tile_lag(t);
     const bool parts = pl.dev;   // a lagged halo round always writes its deviation partials
+    const int32_t Np = lag ? t.n_loc : Nr;   // partial rows: lagged = one per local source row
     if (parts && (!ws || (reinterpret_cast<uintptr_t>(ws) & 15u)))
         return fail(DL_ERR_WORKSPACE, "dl_mix_round: deviation outputs need a 16-byte aligned "
                                       "workspace of dl_mix_workspace_bytes()");
@@ -861,7 +884,7 @@ int dl_mix_round(const dl_mix_args *args, void *workspace, size_t ws_bytes, dl_s
         const int64_t n_tail = pl.pub.n_tiles - n_full;  // 0 or 1 when vec, else all tiles
         int grid_full = (int)(n_full < pl.pub.grid ? n_full : pl.pub.grid);
         int grid_tail = (int)(n_tail < pl.pub.grid ? n_tail : pl.pub.grid);
-        const size_t need = align_up((size_t)(grid_full + grid_tail) * Nr * 4);
+        const size_t need = align_up((size_t)(grid_full + grid_tail) * Np * 4);
         if (parts && ws_bytes < need)
             return fail(DL_ERR_WORKSPACE, "dl_mix_round: workspace %zu < %zu bytes", ws_bytes, need);
         t.csr_off = pl.csr_off;
@@ -887,14 +910,14 @@ int dl_mix_round(const dl_mix_args *args, void *workspace, size_t ws_bytes, dl_s
             if (reg_csr) return fail(DL_ERR_INVALID, "dl_mix_round: register-CSR plan with a tail");
             t.n_tiles = (int32_t)n_tail;
             t.col_base = n_full * T;
-            t.dev_partial = parts ? partial + (size_t)grid_full * Nr : nullptr;
+            t.dev_partial = parts ? partial + (size_t)grid_full * Np : nullptr;
             hipError_t e = dl::launch_mix_tile(t, pl.chunks, sgd, pl.dev, true, grid_tail,
                                                lds, false, s);
             if (e != hipSuccess) return hip_fail(e, "mix_tile_kernel (tail) launch");
         }
         if (parts) {
             if (Nr <= 1 && !lag) return zero_deviation(Nr, args->dev_sq, args->dev_max, s);
-            hipError_t e = dl::launch_dev_reduce(partial, grid_full + grid_tail, Nr, args->dev_sq,
+            hipError_t e = dl::launch_dev_reduce(partial, grid_full + grid_tail, Np, args->dev_sq,
                                                  args->dev_max, s, true);
             if (e != hipSuccess) return hip_fail(e, "dev_reduce launch");
         }
@@ -950,6 +973,7 @@ int deviation_one_pass(const float *x, int64_t ldx, int32_t tile_cols, int32_t n
     t.ldx = ldx;
     t.n_rows = n_rows;
     t.n_src = n_rows;
+    t.n_loc = n_rows;
     t.n_params = n_params;
     t.vec = vec ? 1 : 0;
     t.mean = mean_out;

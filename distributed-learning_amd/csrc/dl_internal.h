@@ -25,7 +25,9 @@ struct TileArgs {
     const int32_t *col;
     const float *w;
     int32_t n_rows;   // output rows (local agents)
-    int32_t n_src;    // rows staged in LDS = n_rows + n_halo
+    int32_t n_src;    // rows staged in LDS = n_loc + n_halo
+    int32_t n_loc;    // source rows read from x (and stepped with g); n_rows unless the round
+                      // mixes one row set of an agent partition from a wider local window
     int32_t nnz;
     int32_t regular;  // >0: every row has exactly `regular` entries (row_ptr not staged)
     int32_t n_w;      // weights staged in LDS: nnz, or `regular` when every row shares row 0's
@@ -48,6 +50,7 @@ struct TileArgs {
     uint32_t hrs;     // halo row stride in bytes (ldh*4)
     int32_t lchunks;     // mix_trace_kernel: float4 chunks per operand tile (1 = row-major)
     float *dev_partial;  // [gridDim.x][n_rows] per-workgroup partial ||y_a - mean||^2
+                         // (lagged halo deviation: [gridDim.x][n_loc], one per source row)
     float *mean;         // [n_params] nullable
     unsigned int *dev_max_zero;  // nullable: workgroup 0 zeroes it (dev_reduce's atomicMax target,
                                  // so that launch needs no memset of its own)
@@ -67,8 +70,12 @@ uint32_t csr_lds_bytes(int32_t n_rows, int32_t nnz, int32_t regular, int32_t n_w
 hipError_t launch_mix_tile(const TileArgs &a, int chunks, bool sgd, bool dev, bool mix, int grid,
                            int lds_bytes, bool fast, hipStream_t s);
 // true when a launch of this plan runs the halo instantiation with the lagged deviation
+// a round of an agent partition: halo source rows, or output rows that are not the source rows
+inline bool tile_partitioned(const TileArgs &a) {
+    return a.n_src != a.n_rows || a.n_loc != a.n_rows;
+}
 inline bool tile_lag(const TileArgs &a) {
-    return a.n_src > a.n_rows && (a.mean_prev != nullptr || a.colsum_out != nullptr);
+    return tile_partitioned(a) && (a.mean_prev != nullptr || a.colsum_out != nullptr);
 }
 hipError_t launch_mix_gather(const TileArgs &a, bool sgd, hipStream_t s);
 // Tile kernel with the CSR in registers (regular graphs of 5 entries per row whose CSR does not

@@ -110,7 +110,9 @@ __device__ __forceinline__ float4 *at(float *base, uint32_t off) {
 // SGD  : fused local step x - lr*g on local rows before mixing
 // DEV  : fused column mean + per-agent ||y_a - mean||^2 (needs all agents in the tile)
 // MIX  : false = deviation of x only (no LDS staging, no output rows)
-// HALO : source rows [n_rows, n_src) come from the halo buffer
+// HALO : source rows [n_loc, n_src) come from the halo buffer; output rows [0, n_rows) follow the
+//        CSR and need not be source rows (n_loc != n_rows: an interior or boundary row set of
+//        an agent partition, sharding.py)
 // FAST : every tile is full and every operand 16-byte aligned (float4 path with 32-bit
 //        offsets from a uniform tile base); false = guarded scalar path (tail, unaligned)
 // RD   : 0 = CSR staged in LDS; RD > 0 = regular graph with RD entries per row whose CSR does
@@ -120,7 +122,7 @@ __device__ __forceinline__ float4 *at(float *base, uint32_t off) {
 // Tiles cover columns [col_base + t*T, ...) for t < n_tiles.  Lanes whose row does not exist
 // (the last, ragged pass) re-read row 0 -- an L1 hit -- and never write LDS or y, so every
 // pass is straight-line code and the loads of the next tile stay in flight during the mix.
-// LAG  : halo rounds only: ||x_a - mean_prev||^2 of every local input row while it is staged
+// LAG  : halo rounds only: ||x_a - mean_prev||^2 of every local source row while it is staged
 //        (the deviation of the previous round's iterate against its all-reduced global mean) and
 //        this rank's column sums of the stepped inputs t into colsum_out -- all-reduced over the
 //        ranks, the numerator of the next mean_prev (sum(W t) = sum(t): W doubly stochastic).
@@ -137,6 +139,7 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
     const int s = tid / C;
     const int R = a.n_src;
     const int Nr = a.n_rows;
+    const int NL = a.n_loc;   // source rows [0, NL) from x (stepped), [NL, R) from the halo
     const int64_t P = a.n_params;
     const int nnz = a.nnz;
 
@@ -213,9 +216,9 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
 #pragma unroll
             for (int k = 0; k < KV; ++k) {
                 const int r = s + k * SLOTS;
-                const bool loc = r < Nr;
+                const bool loc = r < NL;
                 const bool ok = r < R;
-                const uint32_t oh = (uint32_t)(r - Nr) * a.hrs + 16u * c;
+                const uint32_t oh = (uint32_t)(r - NL) * a.hrs + 16u * c;
                 const char *bx = loc || !ok ? xt : ht;
                 const uint32_t o1 = loc ? ox + k * sx : ok ? oh : 16u * c;
                 const float4 *p1 = reinterpret_cast<const float4 *>(bx + o1);
@@ -251,9 +254,9 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
             for (int k = 0; k < KV; ++k) {
                 int r = s + k * SLOTS;
                 if (r >= R) r = 0;
-                const bool local = !HALO || r < Nr;
+                const bool local = !HALO || r < NL;
                 const float *row = local ? a.x + (int64_t)r * a.ldx
-                                         : a.halo + (int64_t)(r - Nr) * a.ldh;
+                                         : a.halo + (int64_t)(r - NL) * a.ldh;
                 px[k] = ld4(row, cc, P, FAST);
                 if (SGD) pg[k] = local ? ld4(a.g + (int64_t)r * a.ldg, cc, P, FAST) : zero4();
             }
@@ -344,15 +347,15 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
                 float4 t = px[k];
                 // lagged deviation of the input, local rows only: this lane's chunk of
                 // ||x_r - mean_prev||^2, summed over the row group's lanes once, at the end
-                if (LAG && r < Nr) {
+                if (LAG && r < NL) {
                     const float dx = t.x - pm.x, dy = t.y - pm.y;
                     const float dz = t.z - pm.z, dw = t.w - pm.w;
                     lacc[k] += (dx * dx + dy * dy) + (dz * dz + dw * dw);
                 }
-                if (SGD && (!HALO || r < Nr)) t = local_step(t, pg[k], a.lr);
+                if (SGD && (!HALO || r < NL)) t = local_step(t, pg[k], a.lr);
                 if (r < R) {
                     tile[r * C + c] = t;
-                    if (DEV || (LAG && r < Nr)) add4(cst, t);
+                    if (DEV || (LAG && r < NL)) add4(cst, t);
                 }
             }
             // mean(W t) = mean(t) when W is doubly stochastic: reduce the column sums of the
@@ -442,8 +445,8 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
             float v = lacc[k];
 #pragma unroll
             for (int m = 1; m < C; m <<= 1) v += __shfl_xor(v, m);   // over the row group
-            const int ag = s + k * SLOTS;
-            if (c == 0 && ag < Nr) a.dev_partial[(int64_t)blockIdx.x * Nr + ag] = v;
+            const int ag = s + k * SLOTS;   // a local source row
+            if (c == 0 && ag < NL) a.dev_partial[(int64_t)blockIdx.x * NL + ag] = v;
         }
         if (a.dev_max_zero != nullptr && blockIdx.x == 0 && tid == 0) *a.dev_max_zero = 0u;
     }
@@ -616,7 +619,7 @@ template <int C, int KV, bool FAST>
 hipError_t launch_mode(const TileArgs &a, bool sgd, bool dev, bool mix, int grid, int lds,
                        hipStream_t s) {
     if (!mix) return launch_one<C, KV, false, true, false, false, FAST>(a, grid, lds, s);
-    if (a.n_src > a.n_rows) {  // halo rows: the exact deviation needs the global mean
+    if (tile_partitioned(a)) {  // halo rows / a row set: the exact deviation needs the global mean
         if (tile_lag(a))        // lagged: previous iterate vs mean_prev, colsum_out for the next
             return sgd ? launch_one<C, KV, true, false, true, true, FAST, 0, true>(a, grid, lds, s)
                        : launch_one<C, KV, false, false, true, true, FAST, 0, true>(a, grid, lds, s);

@@ -29,6 +29,7 @@ class DeviceCsr:
         self.w = torch.as_tensor(csr.w.astype(np.float32), device=self.device)
         self.n_rows = csr.n_rows
         self.n_src = csr.n_src
+        self.n_local = csr.n_local      # local source rows (n_rows unless a partition row set)
         self.nnz = csr.nnz
         self.uniform_row_nnz = csr.uniform_row_nnz
         self.doubly_stochastic = int(csr.doubly_stochastic)
@@ -115,13 +116,14 @@ def mix_args_tiled(W: DeviceCsr, n_params, tile_cols, X, Y, G=None, lr=0.0, dev_
 
 def mix_args(W: DeviceCsr, X, Y, G=None, lr=0.0, halo=None, dev_sq=None, dev_max=None,
              mean=None):
-    """Build the dl_mix_args struct for X -> Y (shapes checked here, the rest in the ABI)."""
+    """Build the dl_mix_args struct for X -> Y (shapes checked here, the rest in the ABI).
+    X (and G) hold the W.n_local local source rows, Y the W.n_rows output rows."""
     n, P = W.n_rows, X.shape[1]
-    _check(X, "X", n, P, W.device)
+    _check(X, "X", W.n_local, P, W.device)
     _check(Y, "Y", n, P, W.device)
     if G is not None:
-        _check(G, "G", n, P, W.device)
-    n_halo = W.n_src - W.n_rows
+        _check(G, "G", W.n_local, P, W.device)
+    n_halo = W.n_src - W.n_local
     if n_halo > 0:
         if halo is None:
             raise ValueError(f"graph has {n_halo} halo rows but no halo buffer was given")
@@ -130,7 +132,8 @@ def mix_args(W: DeviceCsr, X, Y, G=None, lr=0.0, halo=None, dev_sq=None, dev_max
         _lib.ptr(X), _ld(X), _lib.ptr(Y), _ld(Y), P, W.c_struct(),
         _lib.ptr(G), _ld(G) if G is not None else 0, float(lr),
         _lib.ptr(halo) if n_halo > 0 else None, _ld(halo) if n_halo > 0 else 0, n_halo,
-        _lib.ptr(dev_sq), _lib.ptr(dev_max), _lib.ptr(mean))
+        _lib.ptr(dev_sq), _lib.ptr(dev_max), _lib.ptr(mean), 0, None, None,
+        W.n_local if W.n_local != n else 0)
 
 
 class Workspace:
@@ -172,7 +175,8 @@ def mix_round(W: DeviceCsr, X, Y, G=None, lr=0.0, halo=None, dev_sq=None, dev_ma
                 raise ValueError(f"{name} must be a contiguous float32 [n_params] device tensor")
             setattr(args, name, _lib.ptr(t))
     workspace = workspace or Workspace(W.device)
-    wp, wn = workspace.ptr_size(lib.dl_mix_workspace_bytes(W.n_rows, W.n_src - W.n_rows, P))
+    wp, wn = workspace.ptr_size(lib.dl_mix_workspace_bytes(max(W.n_rows, W.n_local),
+                                                           W.n_src - W.n_local, P))
     _lib.check(lib.dl_mix_round(ctypes.byref(args), wp, wn, _lib.stream_handle(W.device)),
                "dl_mix_round")
 

@@ -19,19 +19,27 @@ import numpy as np
 @dataclass
 class Csr:
     """Host CSR of a mixing matrix.  Source rows [0, n_rows) are local agents; rows
-    [n_rows, n_src) (multi-GPU only) are halo rows owned by other ranks."""
+    [n_rows, n_src) (multi-GPU only) are halo rows owned by other ranks.  A row set of an agent
+    partition (sharding.py: interior / boundary rows) sets ``n_local``: source rows
+    [0, n_local) are local, [n_local, n_src) halo, and the n_rows output rows need not be
+    source rows (dl_mix_args.n_local_src)."""
     rowptr: np.ndarray          # int64 [n_rows + 1]
     col: np.ndarray             # int64 [nnz]
     w: np.ndarray               # float64 [nnz] (cast to fp32 on upload)
     keys: list = field(default_factory=list)   # agent key of each local row
     n_src: int = -1
+    n_local: int = -1
 
     def __post_init__(self):
         self.rowptr = np.asarray(self.rowptr, np.int64)
         self.col = np.asarray(self.col, np.int64)
         self.w = np.asarray(self.w, np.float64)
+        if self.n_local < 0:
+            self.n_local = self.n_rows
         if self.n_src < 0:
-            self.n_src = self.n_rows
+            self.n_src = self.n_local
+        if self.n_src < self.n_local:
+            raise ValueError("n_src < n_local")
         if len(self.rowptr) < 1 or self.rowptr[0] != 0 or np.any(np.diff(self.rowptr) < 0):
             raise ValueError("row_ptr must start at 0 and be non-decreasing")
         if self.rowptr[-1] != len(self.col) or len(self.col) != len(self.w):

@@ -100,6 +100,11 @@ class RankPlan:
     halo_from: dict = field(default_factory=dict)   # peer -> global ids I receive (halo order)
     send_to: dict = field(default_factory=dict)     # peer -> my local row indices I send
     halo_offset: dict = field(default_factory=dict)  # peer -> first halo row of its block
+    # boundary-last row order (split_halo_plans): rows [0, n_deep) are interior rows no
+    # boundary row reads, [n_deep, n_interior) interior rows a boundary row reads,
+    # [n_interior, n_local) boundary rows (they read halo rows).  -1: not in that order.
+    n_deep: int = -1
+    n_interior: int = -1
 
     @property
     def n_local(self):
@@ -108,6 +113,27 @@ class RankPlan:
     @property
     def n_halo(self):
         return self.csr.n_src - self.csr.n_rows
+
+    def row_sets(self):
+        """(interior CSR, boundary CSR) of a boundary-last plan, for the two launches of a split
+        round (``HaloShard(overlap="split")``):
+
+        * interior: output rows [0, n_interior), sources = every local row (no halo);
+        * boundary: output rows [n_interior, n_local), sources = the local window
+          [n_deep, n_local) then the halo, columns renumbered into that window.
+
+        Each row keeps its entries in the same order, so both launches fold exactly as the
+        single-device round does."""
+        if self.n_interior < 0:
+            raise ValueError("plan is not in boundary-last order (use split_halo_plans)")
+        c, n, nd, ni = self.csr, self.n_local, self.n_deep, self.n_interior
+        e_i = c.rowptr[ni]
+        interior = Csr(c.rowptr[:ni + 1], c.col[:e_i], c.w[:e_i], n_src=n, n_local=n)
+        col = c.col[e_i:] - nd            # local c -> c - n_deep; halo h -> (n - nd) + (h - n)
+        if len(col) and col.min() < 0:
+            raise ValueError("a boundary row reads a row before the window (n_deep)")
+        boundary = Csr(c.rowptr[ni:] - e_i, col, c.w[e_i:], n_src=c.n_src - nd, n_local=n - nd)
+        return interior, boundary
 
 
 def halo_plans(csr: Csr, parts):
@@ -153,6 +179,32 @@ def halo_plans(csr: Csr, parts):
         send_to = {q: pos[np.asarray(sorted(need[q][r]), np.int64)]
                    for q in range(world) if need[q][r]}
         plans.append(RankPlan(r, np.asarray(p), local_csr, halo_from, send_to, halo_offset))
+    return plans
+
+
+def split_halo_plans(csr: Csr, parts):
+    """halo_plans with every rank's agents in boundary-last order: [interior rows no boundary row
+    reads | interior rows a boundary row reads | boundary rows (they read halo rows)], each group
+    in the partition's order.  The interior rows then mix while the halo is in flight, and the
+    boundary rows read only the window [n_deep, n_local) of local rows plus the halo
+    (RankPlan.row_sets).  Entry order within every row is kept (bit-identical rounds)."""
+    first = halo_plans(csr, parts)
+    new_parts, counts = [], []
+    for pl in first:
+        c, n = pl.csr, pl.n_local
+        row_of = np.repeat(np.arange(n), np.diff(c.rowptr))
+        bnd = np.zeros(n, bool)
+        bnd[row_of[c.col >= n]] = True
+        adj = np.zeros(n, bool)          # interior rows a boundary row reads
+        adj[c.col[bnd[row_of] & (c.col < n)]] = True
+        adj &= ~bnd
+        deep = ~bnd & ~adj
+        order = np.concatenate([np.flatnonzero(deep), np.flatnonzero(adj), np.flatnonzero(bnd)])
+        new_parts.append(pl.local[order])
+        counts.append((int(deep.sum()), int(deep.sum() + adj.sum())))
+    plans = halo_plans(csr, new_parts)
+    for pl, (nd, ni) in zip(plans, counts):
+        pl.n_deep, pl.n_interior = nd, ni
     return plans
 
 
@@ -344,13 +396,26 @@ class HaloShard:
     """One rank's agent block with halo exchange (row-major X[n_local, P])."""
 
     def __init__(self, plan: RankPlan, n_params, device, transport, chunk_cols=None,
-                 n_agents_total=None, ops=None, doubly_stochastic=True):
+                 n_agents_total=None, ops=None, doubly_stochastic=True, overlap="chunks"):
+        """overlap="chunks": the columns are processed in chunks, the exchange of chunk j+1 in
+        flight while chunk j is mixed.  overlap="split" (a boundary-last plan from
+        split_halo_plans): ONE exchange of every column per round, in flight while the interior
+        rows mix; the boundary rows mix after it lands (RankPlan.row_sets)."""
+        if overlap not in ("chunks", "split"):
+            raise ValueError(f"overlap must be 'chunks' or 'split' (got {overlap!r})")
+        if overlap == "split" and plan.n_interior < 0:
+            raise ValueError("overlap='split' needs a boundary-last plan (split_halo_plans)")
+        self.overlap = overlap
         self.plan = plan
         self.P = int(n_params)
         self.device = torch.device(device)
         self.transport = transport
         self.ops = ops if ops is not None else HipOps(self.device)
         self.W = self.ops.csr(plan.csr)
+        if overlap == "split":
+            ci, cb = plan.row_sets()
+            self.W_int = self.ops.csr(ci) if plan.n_interior > 0 else None
+            self.W_bnd = self.ops.csr(cb) if plan.n_interior < plan.n_local else None
         self.n_total = n_agents_total
         self.chunk = int(chunk_cols or self.P)
         self.send_rows = {q: torch.as_tensor(rows.astype(np.int32), device=self.device)
@@ -409,7 +474,8 @@ class HaloShard:
         ``deviation()`` would have returned before the round.  (Halo rounds cannot fuse the
         deviation of their own output: its global mean is only known after every rank's round.)
         The first lagged round computes the starting mean with one column-sum pass."""
-        chunks = self.chunks()
+        split = self.overlap == "split" and self.plan.n_halo > 0
+        chunks = [(0, self.P)] if split else self.chunks()
         lag = None
         if deviation:
             if self.plan.n_halo == 0 or not self.doubly_stochastic:
@@ -422,7 +488,10 @@ class HaloShard:
             parts = torch.empty(len(chunks), self.plan.n_local, dtype=torch.float32,
                                 device=self.device)
             lag = (self.mean_prev, colsum, parts)
-        self._mix_all(chunks, G, lr, lag)
+        if split:
+            self._split_round(G, lr, None if lag is None else (lag[0], lag[1], lag[2][0]))
+        else:
+            self._mix_all(chunks, G, lr, lag)
         if lag is None:
             return None
         dev_sq = parts.sum(0)
@@ -447,6 +516,24 @@ class HaloShard:
             cl = None if lag is None else (lag[0][c0:c1], lag[1][c0:c1], lag[2][j])
             self.mix_chunk(c0, c1, halo, G, lr, cl)
             pend = nxt
+        self.X, self.Y = self.Y, self.X
+
+    def _split_round(self, G, lr, lag):
+        """One exchange of the whole boundary; the interior rows mix from the local rows while
+        it is in flight (and, with ``lag``, measure every local row -- the interior launch stages
+        them all); the boundary rows mix from the window [n_deep, n_local) and the halo once it
+        has landed."""
+        pl = self.plan
+        ni, nd, n = pl.n_interior, pl.n_deep, pl.n_local
+        send, halo, recv = self.pack(0, 0, self.P, G, lr)
+        works = self.transport.exchange(send, recv)
+        if ni > 0:
+            self.ops.mix(self.W_int, self.X, self.Y[:ni], G=G, lr=lr, lag=lag)
+        for w in works:
+            w.wait()
+        if ni < n:
+            self.ops.mix(self.W_bnd, self.X[nd:], self.Y[ni:], G=None if G is None else G[nd:],
+                         lr=lr, halo=halo, lag=None if ni > 0 else lag)
         self.X, self.Y = self.Y, self.X
 
     def _global_mean(self, X):

@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define DLAMD_ABI_VERSION 4
+#define DLAMD_ABI_VERSION 5
 
 typedef void *dl_stream_t; /* hipStream_t; NULL = the legacy default stream */
 
@@ -62,7 +62,8 @@ enum dl_status {
 /* Mixing matrix W in CSR form (device pointers).  Row a lists its (source row, weight) pairs in
  * the reference's dict insertion order (mixer.py:47) -- that order is the fp32 summation order,
  * and the result is bit-identical to the reference's left fold when it is kept.  Source rows
- * index [0, n_rows) = local agents, [n_rows, n_rows + n_halo) = halo rows. */
+ * index [0, n_rows) = local agents, [n_rows, n_rows + n_halo) = halo rows (with
+ * dl_mix_args.n_local_src = L: [0, L) local, [L, L + n_halo) halo). */
 typedef struct dl_csr {
     const int32_t *row_ptr; /* [n_rows + 1] */
     const int32_t *col;     /* [nnz] */
@@ -108,14 +109,25 @@ typedef struct dl_mix_args {
      * global column mean of y needs every rank's rows, so this round's kernel publishes its
      * share of it and measures the PREVIOUS round's iterate -- its input x, staged anyway --
      * against the previous mean.  No HBM pass beyond the round's own. */
-    const float *mean_prev; /* nullable [n_params] (n_halo > 0 only; with colsum_out and dev_sq):
+    const float *mean_prev; /* nullable [n_params] (n_halo > 0 or n_local_src > n_rows only; with
+                               colsum_out and dev_sq):
                                the global column mean of x (the previous round's all-reduced
                                colsum_out / N): dev_sq[a] = ||x_a - mean_prev||^2, dev_max =
                                max sqrt (nullable). */
-    float *colsum_out;      /* nullable [n_params] (n_halo > 0 only): sum over this rank's rows of
+    float *colsum_out;      /* nullable [n_params] (as mean_prev): sum over the local source rows of
                                the stepped inputs t = x - lr*g, in a fixed order.  Summed over all
                                ranks it is the column sum of the round's output when the global W
                                is doubly stochastic (the numerator of the next mean_prev). */
+    /* Row sets of an agent partition (sharding.py, interior/boundary split): 0 = n_rows.
+     * Otherwise source rows [0, n_local_src) come from x (and g, stepped), [n_local_src,
+     * n_local_src + n_halo) from halo, and the n_rows OUTPUT rows follow the CSR -- they need
+     * not be the first source rows: an interior launch mixes rows [0, n_I) of a rank's window
+     * from all its local rows while the halo is in flight; a boundary launch passes x (and g)
+     * offset to the first local row the boundary rows read, and y offset to the first boundary
+     * row.  Needs n_rows <= n_local_src + n_halo, the LDS tile kernel, no fused exact deviation
+     * (dev_sq / dev_max / mean only as the lagged deviation, which is then per SOURCE row:
+     * dev_sq[n_local_src]; workspace dl_mix_workspace_bytes(max(n_rows, n_local_src), ...)). */
+    int32_t n_local_src;
 } dl_mix_args;
 
 /* Which kernel configuration dl_mix_round picks (introspection for tests and the bench). */

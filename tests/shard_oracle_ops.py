@@ -40,8 +40,8 @@ class OracleOps:
         if halo is not None:
             T = np.concatenate([T, halo.numpy()])
         c = W.csr
-        Y.copy_(torch.from_numpy(M.mix_once(np.ascontiguousarray(T), c.rowptr, c.col, c.w)
-                                 [:W.n_rows]))
+        out = M.mix_once(np.ascontiguousarray(T), c.rowptr, c.col, c.w)
+        Y.copy_(torch.from_numpy(out[:W.n_rows]))
 
     def column_sum(self, X):
         Xn = X.numpy()

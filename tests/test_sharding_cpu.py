@@ -52,13 +52,51 @@ def test_halo_plans_reconstruct_the_graph(kind):
             assert np.array_equal(pl.local[rows], plans[q].halo_from[pl.rank])
 
 
+@pytest.mark.parametrize("kind", ["torus", "rr4", "bfs"])
+def test_split_plans_row_sets(kind):
+    """split_halo_plans orders every rank's rows [deep interior | interior read by the boundary |
+    boundary]; the boundary rows are exactly the rows with halo entries, they read only the
+    window [n_deep, n_local) of local rows, and the interior + boundary launches of
+    RankPlan.row_sets reproduce the full local round bit for bit (oracle fold)."""
+    if kind == "torus":
+        csr = torus_csr(8, 8)
+        parts = sharding.torus_block_partition(8, 8, 4)
+    else:
+        edges = random_regular_edges(4, 60, seed=1)
+        csr = from_edge_weights(edges, [0.2] * len(edges), list(range(60)))
+        parts = (sharding.contiguous_partition(60, 3) if kind == "rr4"
+                 else sharding.greedy_bfs_partition(csr, 3))
+    plans = sharding.split_halo_plans(csr, parts)
+    for pl, part in zip(plans, parts):
+        assert sorted(pl.local.tolist()) == sorted(part.tolist())
+        c, n, nd, ni = pl.csr, pl.n_local, pl.n_deep, pl.n_interior
+        assert 0 <= nd <= ni <= n
+        has_halo = np.array([np.any(c.col[c.rowptr[a]:c.rowptr[a + 1]] >= n) for a in range(n)])
+        assert not has_halo[:ni].any() and has_halo[ni:].all()
+        e_i = c.rowptr[ni]
+        assert np.all((c.col[e_i:] >= nd))            # boundary reads only the window
+        ci, cb = pl.row_sets()
+        assert (ci.n_rows, ci.n_local, ci.n_src) == (ni, n, n)
+        assert (cb.n_rows, cb.n_local, cb.n_src) == (n - ni, n - nd, c.n_src - nd)
+        rng = np.random.default_rng(pl.rank)
+        T = rng.standard_normal((c.n_src, 9), dtype=np.float32)
+        full = M.mix_once(T, c.rowptr, c.col, c.w)[:n]
+        yi = M.mix_once(T[:n], ci.rowptr, ci.col, ci.w)[:ni]
+        yb = M.mix_once(T[nd:], cb.rowptr, cb.col, cb.w)[:n - ni]
+        assert np.array_equal(np.concatenate([yi, yb]).view(np.uint32), full.view(np.uint32))
+    # the plans still describe the same exchange (what I send is what my peer expects)
+    for pl in plans:
+        for q, rows in pl.send_to.items():
+            assert np.array_equal(pl.local[rows], plans[q].halo_from[pl.rank])
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, P, chunk, out_dir, lag=False):
+def _worker(rank, world, port, P, chunk, out_dir, lag=False, overlap="chunks"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -67,14 +105,15 @@ def _worker(rank, world, port, P, chunk, out_dir, lag=False):
     from shard_oracle_ops import OracleOps
     csr = torus_csr(8, 8)
     parts = sharding.torus_block_partition(8, 8, world)
-    plan = sharding.halo_plans(csr, parts)[rank]
+    plan = (sharding.split_halo_plans if overlap == "split" else sharding.halo_plans)(
+        csr, parts)[rank]
     rng = np.random.default_rng(0)
     X = rng.standard_normal((64, P), dtype=np.float32)
     G = rng.standard_normal((64, P), dtype=np.float32)
     # chunked case through the host-staged transport that gloo ranks sharing a GPU use
     tr = sharding.dist_transport() if chunk else sharding.DistTransport()
     sh = sharding.HaloShard(plan, P, "cpu", tr, chunk_cols=chunk,
-                            n_agents_total=64, ops=OracleOps())
+                            n_agents_total=64, ops=OracleOps(), overlap=overlap)
     sh.X = torch.from_numpy(X[plan.local].copy())
     Gl = torch.from_numpy(G[plan.local].copy())
     lagged = []
@@ -91,15 +130,19 @@ def _worker(rank, world, port, P, chunk, out_dir, lag=False):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("chunk,lag", [(None, False), (7, False), (None, True), (7, True)])
-def test_halo_rounds_over_gloo_equal_single_process(tmp_path, chunk, lag):
+@pytest.mark.parametrize("chunk,lag,overlap", [(None, False, "chunks"), (7, False, "chunks"),
+                                               (None, True, "chunks"), (7, True, "chunks"),
+                                               (None, False, "split"), (None, True, "split")])
+def test_halo_rounds_over_gloo_equal_single_process(tmp_path, chunk, lag, overlap):
     """Real 2-rank gloo halo rounds equal the single-process oracle rounds bit for bit; with
     deviation=True each round also returns the (lagged) deviation of the iterate it started from
     -- measured inside the round, against the all-reduced column sums of the previous round's
-    stepped inputs -- within 1e-5 relative of the oracle's deviation of that iterate."""
+    stepped inputs -- within 1e-5 relative of the oracle's deviation of that iterate.
+    overlap="split": boundary-last plans, one exchange per round in flight while the interior
+    rows mix, then the boundary rows (same bits)."""
     world, P = 2, 24
-    mp.spawn(_worker, args=(world, _free_port(), P, chunk, str(tmp_path), lag), nprocs=world,
-             join=True)
+    mp.spawn(_worker, args=(world, _free_port(), P, chunk, str(tmp_path), lag, overlap),
+             nprocs=world, join=True)
     csr = torus_csr(8, 8)
     rng = np.random.default_rng(0)
     X = rng.standard_normal((64, P), dtype=np.float32)

@@ -12,8 +12,10 @@ from distributed_learning_amd.graph import best_constant_weight, from_edge_weigh
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("world,chunk", [(2, None), (4, 300), (8, 1000)])
-def test_virtual_ranks_equal_single_device(cuda, world, chunk):
+@pytest.mark.parametrize("world,chunk,overlap", [(2, None, "chunks"), (4, 300, "chunks"),
+                                                 (8, 1000, "chunks"), (2, None, "split"),
+                                                 (4, None, "split"), (8, None, "split")])
+def test_virtual_ranks_equal_single_device(cuda, world, chunk, overlap):
     from distributed_learning_amd import engine as E
     R, C, P = 16, 16, 2048
     edges = torus_edges(R, C)
@@ -25,12 +27,13 @@ def test_virtual_ranks_equal_single_device(cuda, world, chunk):
     ref = E.GossipEngine(csr, P, device=cuda, X=X, layout="rows")
     for _ in range(3):
         ref.round(G=G, lr=0.01)
-    plans = sharding.halo_plans(csr, sharding.torus_block_partition(R, C, world))
+    plans = (sharding.split_halo_plans if overlap == "split" else sharding.halo_plans)(
+        csr, sharding.torus_block_partition(R, C, world))
     tr = sharding.LocalTransport(world)
     shards = []
     for pl in plans:
         sh = sharding.HaloShard(pl, P, cuda, tr.endpoint(pl.rank), chunk_cols=chunk,
-                                n_agents_total=R * C)
+                                n_agents_total=R * C, overlap=overlap)
         ids = torch.as_tensor(pl.local, device=cuda)
         sh.X = X[ids].contiguous()
         shards.append((sh, G[ids].contiguous(), ids))
@@ -59,8 +62,10 @@ def test_virtual_ranks_equal_single_device(cuda, world, chunk):
         np.testing.assert_allclose(sh.dev[0].cpu().numpy(), dsq[ids].cpu().numpy(), rtol=1e-5)
 
 
-@pytest.mark.parametrize("world,chunk", [(2, None), (4, 300), (8, 1000)])
-def test_lagged_deviation_in_the_halo_round(cuda, world, chunk):
+@pytest.mark.parametrize("world,chunk,overlap", [(2, None, "chunks"), (4, 300, "chunks"),
+                                                 (8, 1000, "chunks"), (4, None, "split"),
+                                                 (8, None, "split")])
+def test_lagged_deviation_in_the_halo_round(cuda, world, chunk, overlap):
     """HaloShard.round(deviation=True): the kernel measures its input rows against the previous
     round's all-reduced mean and publishes the column sums of its stepped inputs (no HBM pass of
     its own).  Iterates stay bit-identical to the single-device round; round i returns the
@@ -77,15 +82,15 @@ def test_lagged_deviation_in_the_halo_round(cuda, world, chunk):
     ref = E.GossipEngine(csr, P, device=cuda, X=X, layout="rows")
     want = []
     for _ in range(4):
-        want.append(ref.deviation())
+        want.append(tuple(t.clone() for t in ref.deviation()))   # engine buffers are reused
         ref.round(G=G, lr=0.01)
-    want = [(dsq.clone(), dmax.clone()) for dsq, dmax in want]
-    plans = sharding.halo_plans(csr, sharding.torus_block_partition(R, C, world))
+    plans = (sharding.split_halo_plans if overlap == "split" else sharding.halo_plans)(
+        csr, sharding.torus_block_partition(R, C, world))
     tr = sharding.LocalTransport(world)
     shards = []
     for pl in plans:
         sh = sharding.HaloShard(pl, P, cuda, tr.endpoint(pl.rank), chunk_cols=chunk,
-                                n_agents_total=R * C)
+                                n_agents_total=R * C, overlap=overlap)
         ids = torch.as_tensor(pl.local, device=cuda)
         sh.X = X[ids].contiguous()
         shards.append((sh, G[ids].contiguous(), ids))
@@ -111,7 +116,7 @@ def test_lagged_deviation_in_the_halo_round(cuda, world, chunk):
             assert float(dmax.item()) == pytest.approx(float(wmax.item()), rel=1e-5)
 
 
-def _gloo_worker(rank, world, port, chunk, out_dir):
+def _gloo_worker(rank, world, port, chunk, out_dir, overlap="chunks"):
     """One rank of a real multi-process run on the shared GPU: torch.distributed gloo with the
     host-staged transport, the HIP halo path, checked against the single-device round."""
     import os
@@ -128,10 +133,12 @@ def _gloo_worker(rank, world, port, chunk, out_dir):
     g = torch.Generator(device=dev).manual_seed(9)
     X = torch.randn(R * C, P, device=dev, generator=g)
     G = torch.randn(R * C, P, device=dev, generator=g)
-    plan = sharding.halo_plans(csr, sharding.torus_block_partition(R, C, world))[rank]
+    plan = (sharding.split_halo_plans if overlap == "split" else sharding.halo_plans)(
+        csr, sharding.torus_block_partition(R, C, world))[rank]
     tr = sharding.dist_transport()
     assert isinstance(tr, sharding.StagedTransport)
-    sh = sharding.HaloShard(plan, P, dev, tr, chunk_cols=chunk, n_agents_total=R * C)
+    sh = sharding.HaloShard(plan, P, dev, tr, chunk_cols=chunk, n_agents_total=R * C,
+                            overlap=overlap)
     ids = torch.as_tensor(plan.local, device=dev)
     sh.X = X[ids].contiguous()
     Gl = G[ids].contiguous()
@@ -151,8 +158,9 @@ def _gloo_worker(rank, world, port, chunk, out_dir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,chunk", [(2, None), (4, 700)])
-def test_processes_over_gloo_equal_single_device(cuda, tmp_path, world, chunk):
+@pytest.mark.parametrize("world,chunk,overlap", [(2, None, "chunks"), (4, 700, "chunks"),
+                                                 (4, None, "split")])
+def test_processes_over_gloo_equal_single_device(cuda, tmp_path, world, chunk, overlap):
     """world processes share the GPU and exchange halos through torch.distributed (gloo, staged
     through the host): the multi-process protocol of bench --workload c4 with the HIP kernels."""
     import socket
@@ -160,7 +168,59 @@ def test_processes_over_gloo_equal_single_device(cuda, tmp_path, world, chunk):
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
-    mp.spawn(_gloo_worker, args=(world, port, chunk, str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_gloo_worker, args=(world, port, chunk, str(tmp_path), overlap), nprocs=world,
+             join=True)
     for r in range(world):
         txt = (tmp_path / f"ok{r}").read_text()
         assert txt.startswith("1 "), (r, txt)
+
+
+@pytest.mark.parametrize("overlap", ["chunks", "split"])
+def test_virtual_ranks_random_graph_bfs_partition(cuda, overlap):
+    """A random 4-regular graph with per-edge weights, agents split by greedy BFS over 3 virtual
+    ranks (irregular halos, every rank a different row-set shape): 3 rounds bit-identical to the
+    single-device round, with the lagged deviation within 1e-5 of the exact one."""
+    from distributed_learning_amd import engine as E
+    from distributed_learning_amd.graph import random_regular_edges
+    n, P, world = 300, 1024 + 20, 3
+    edges = random_regular_edges(4, n, seed=11)
+    rng = np.random.default_rng(3)
+    csr = from_edge_weights(edges, list(rng.uniform(0.05, 0.2, len(edges))), list(range(n)))
+    g = torch.Generator(device=cuda).manual_seed(2)
+    X = torch.randn(n, P, device=cuda, generator=g)
+    G = torch.randn(n, P, device=cuda, generator=g)
+    ref = E.GossipEngine(csr, P, device=cuda, X=X, layout="rows")
+    want = []
+    for _ in range(3):
+        want.append(tuple(t.clone() for t in ref.deviation()))
+        ref.round(G=G, lr=0.02)
+    parts = sharding.greedy_bfs_partition(csr, world)
+    plans = (sharding.split_halo_plans if overlap == "split" else sharding.halo_plans)(csr, parts)
+    tr = sharding.LocalTransport(world)
+    shards = []
+    for pl in plans:
+        sh = sharding.HaloShard(pl, P, cuda, tr.endpoint(pl.rank), n_agents_total=n,
+                                overlap=overlap, chunk_cols=None if overlap == "split" else 512)
+        ids = torch.as_tensor(pl.local, device=cuda)
+        sh.X = X[ids].contiguous()
+        shards.append((sh, G[ids].contiguous(), ids))
+    errs = []
+
+    def run(sh, Gl):
+        try:
+            sh.got = [sh.round(G=Gl, lr=0.02, deviation=True) for _ in range(3)]
+        except Exception as e:  # pragma: no cover
+            errs.append(e)
+    ths = [threading.Thread(target=run, args=(sh, Gl)) for sh, Gl, _ in shards]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert not errs, errs
+    torch.cuda.synchronize()
+    full = ref.rows()
+    for sh, _, ids in shards:
+        assert torch.equal(sh.X.view(torch.int32), full[ids].view(torch.int32))
+        for (dsq, dmax), (wsq, wmax) in zip(sh.got, want):
+            np.testing.assert_allclose(dsq.cpu().numpy(), wsq[ids].cpu().numpy(), rtol=1e-5)
+            assert float(dmax.item()) == pytest.approx(float(wmax.item()), rel=1e-5)

@@ -89,6 +89,8 @@ def parse():
                         "per-edge FDLA SDP weights of the c2 graph, tests/golden/fdla_rr4_1024.npz)")
     p.add_argument("--no-fdla-probe", action="store_true",
                    help="c2 at N=1: skip the second measurement with per-edge FDLA weights")
+    p.add_argument("--halo-overlap", default="both", choices=["both", "chunks", "split"],
+                   help="c4 at N>1: halo overlap scheme(s) to time (sharding.HaloShard)")
     p.add_argument("--dist-backend", default="nccl",
                    help="nccl (= RCCL, default) or gloo (multi-rank rehearsal on one GPU)")
     return p.parse_args()
@@ -549,9 +551,13 @@ def run_gather(args, dev, rank, world):
 def run_c4(args, dev, rank, world):
     """Config c4: 64x64 periodic torus, 4096 agents x 2^18 params, uniform best-constant weight
     2/(lambda_2 + 8).  N=1: the whole torus resident in the tiled layout, one fused round
-    (local step + mix + deviation) per step.  N>1: 2-D torus blocks per rank (HaloShard), the
-    boundary rows of each column chunk exchanged with RCCL send/recv while the previous chunk is
-    mixed, deviation via an all-reduced column sum (strong scaling: total work fixed)."""
+    (local step + mix + deviation) per step.  N>1: 2-D torus blocks per rank (HaloShard, strong
+    scaling: total work fixed), the deviation lagged one round inside the round's own kernel
+    (no extra HBM pass; one all-reduce of n_params column sums + one of the max).  Two overlap
+    schemes, both timed (--halo-overlap both, the default): "chunks" -- the boundary rows of each
+    column chunk exchanged with RCCL send/recv while the previous chunk is mixed; "split" -- one
+    exchange per round in flight while the interior rows mix, the boundary rows after it lands.
+    ``value`` is the faster scheme's rate; both are in the line."""
     import math
     from distributed_learning_amd import engine, graph, sharding
     rows = cols = 64
@@ -561,9 +567,10 @@ def run_c4(args, dev, rank, world):
     csr = graph.from_edge_weights(edges, [wconst] * len(edges), list(range(n)))
     gen = torch.Generator(device=dev).manual_seed(1000 + rank)
     stream = torch.cuda.current_stream(dev)
-    evs = event_pairs(args.steps, 2)
     halo_rows = 0
+    schemes = {}
     if world == 1:
+        evs = event_pairs(args.steps, 2)
         X = torch.randn(n, P, device=dev, generator=gen)
         eng = engine.GossipEngine(csr, P, device=dev, X=X)
         G = eng.layout_like(torch.randn(n, P, device=dev, generator=gen))
@@ -577,27 +584,48 @@ def run_c4(args, dev, rank, world):
             if i is not None:
                 evs[i][1].record(stream)
         bytes_per_round = 12 * n * P
+        elapsed = timed_loop(step, args, world, dev)
+        launch_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
     else:
         parts = sharding.torus_block_partition(rows, cols, world)
-        rp = sharding.halo_plans(csr, parts)[rank]
-        shard = sharding.HaloShard(rp, P, dev, sharding.dist_transport(), chunk_cols=P // 8,
-                                   n_agents_total=n)
-        shard.X.normal_(generator=gen)
-        G = engine.staggered_zeros((rp.n_local, P), 2, dev).normal_(generator=gen)
-        halo_rows = rp.n_halo
-        plan = {"path": "halo", "n_local": rp.n_local, "n_halo": rp.n_halo,
-                "peers": sorted(rp.halo_from)}
+        G = None
+        names = ["chunks", "split"] if args.halo_overlap == "both" else [args.halo_overlap]
+        for name in names:
+            rp = (sharding.split_halo_plans if name == "split" else sharding.halo_plans)(
+                csr, parts)[rank]
+            shard = sharding.HaloShard(rp, P, dev, sharding.dist_transport(),
+                                       chunk_cols=P // 8 if name == "chunks" else None,
+                                       n_agents_total=n, overlap=name)
+            shard.X.normal_(generator=gen)
+            if G is None:   # synthetic gradient rows, shared by both schemes (same row count)
+                G = engine.staggered_zeros((rp.n_local, P), 2, dev).normal_(generator=gen)
+            halo_rows = rp.n_halo
+            evs = event_pairs(args.steps, 2)
 
-        def step(i):
-            if i is not None:
-                evs[i][0].record(stream)
-            shard.round(G=G, lr=lr)
-            shard.deviation()
-            if i is not None:
-                evs[i][1].record(stream)
-        bytes_per_round = 12 * rp.n_local * P
-    elapsed = timed_loop(step, args, world, dev)
-    launch_ms = max_over_ranks(float(np.mean([a.elapsed_time(b) for a, b in evs])), world, dev)
+            def step(i, shard=shard, evs=evs):
+                if i is not None:
+                    evs[i][0].record(stream)
+                shard.round(G=G, lr=lr, deviation=True)   # lagged deviation, in the round
+                if i is not None:
+                    evs[i][1].record(stream)
+            el = timed_loop(step, args, world, dev)
+            lm = max_over_ranks(float(np.mean([a.elapsed_time(b) for a, b in evs])), world, dev)
+            extra = 0
+            if name == "split":   # boundary launch re-reads its local window (X and G)
+                extra = 8 * (rp.n_local - rp.n_deep) * P
+            schemes[name] = {"rounds_per_s": args.steps / el, "elapsed_s": el, "launch_ms": lm,
+                             "n_local": rp.n_local, "n_halo": rp.n_halo,
+                             "n_interior": rp.n_interior if name == "split" else None,
+                             "n_deep": rp.n_deep if name == "split" else None,
+                             "reread_bytes_per_round": extra,
+                             "peers": sorted(rp.halo_from)}
+            del shard
+            torch.cuda.empty_cache()
+        best = max(schemes, key=lambda k: schemes[k]["rounds_per_s"])
+        elapsed, launch_ms = schemes[best]["elapsed_s"], schemes[best]["launch_ms"]
+        plan = {"path": "halo", "overlap": best, "n_local": schemes[best]["n_local"],
+                "n_halo": halo_rows, "peers": schemes[best]["peers"]}
+        bytes_per_round = 12 * schemes[best]["n_local"] * P
     if rank != 0:
         return
     achieved = bytes_per_round / (launch_ms / 1e3) / 1e9
@@ -617,6 +645,9 @@ def run_c4(args, dev, rank, world):
                 "frac": hb / (launch_ms / 1e3) / 1e9 / (XGMI_LINK_GBS * n_peers),
                 "note": "received halo bytes over the rank's round time (HIP events); one "
                         "link per peer"}
+        for v in schemes.values():
+            v["hbm_frac"] = bytes_per_round / (v["launch_ms"] / 1e3) / 1e9 / HBM_PEAK_GBS
+            v["xgmi_frac"] = hb / (v["launch_ms"] / 1e3) / 1e9 / (XGMI_LINK_GBS * n_peers)
     rec = {
         "metric": "c4 torus consensus rounds/sec (4096 agents x 2^18 fp32 params)",
         "value": args.steps / elapsed,
@@ -635,6 +666,8 @@ def run_c4(args, dev, rank, world):
                    "parallelism": f"2-D torus blocks x{world}, "
                                   f"{'RCCL' if args.dist_backend == 'nccl' else args.dist_backend}"
                                   f" halo exchange" if world > 1 else "single GPU", "plan": plan,
+                   "deviation": "fused exact" if world == 1 else
+                                "lagged one round, inside the round kernel (dlamd.h mean_prev)",
                    "halo_rows_rank0": halo_rows,
                    "halo_bytes_per_round_rank0": halo_rows * P * 4},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -643,6 +676,7 @@ def run_c4(args, dev, rank, world):
                      "kernel": "per-round HIP-event time (rank 0 local work)",
                      "bytes_per_launch": bytes_per_round, "launch_ms": launch_ms},
         "xgmi": xgmi,
+        "overlap_schemes": schemes or None,
         "cpu_baseline": None,
     }
     print(json.dumps(rec), flush=True)
@@ -1039,7 +1073,8 @@ def halo_probe(world, backend, steps=20, warmup=3, timeout_s=240):
             "scaling": r["scaling"], "ms_per_step": r["ms_per_step"], "steps": r["steps"],
             "parallelism": r["config"]["parallelism"], "plan": r["config"]["plan"],
             "hbm": {k: r["roofline"][k] for k in ("achieved", "peak", "frac", "launch_ms")},
-            "xgmi": r["xgmi"], "wall_s": time.perf_counter() - t0}
+            "xgmi": r["xgmi"], "overlap_schemes": r.get("overlap_schemes"),
+            "wall_s": time.perf_counter() - t0}
 
 
 def main():
@@ -1190,7 +1225,13 @@ def main():
         if world > 1 and not args.no_halo_probe and sgd:
             del eng, G
             torch.cuda.empty_cache()
-            rec["c4_halo"] = halo_probe(world, args.dist_backend)
+            rec["c4_halo"] = h = halo_probe(world, args.dist_backend)
+            # the agent-partitioned path's figures as first-class fields of the line
+            ok = h.get("status") == "ok"
+            rec["c4_halo_rounds_per_s"] = h["value"] if ok else None
+            rec["c4_halo_hbm_frac"] = h["hbm"]["frac"] if ok else None
+            rec["c4_halo_xgmi_frac"] = h["xgmi"]["frac"] if ok and h.get("xgmi") else None
+            rec["c4_halo_overlap"] = h["plan"].get("overlap") if ok else None
         print(json.dumps(rec), flush=True)
 
 

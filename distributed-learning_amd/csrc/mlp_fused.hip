@@ -63,6 +63,79 @@ __device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
 }
 
 
+// ---- fp32 GEMM on the bf16 matrix cores ("bf16x6").  Every fp32 operand x is split exactly into
+// three bf16 pieces x = h + m + l (h = bf16(x), m = bf16(x - h), l = bf16(x - h - m); each
+// difference is exact, so h + m + l carries x's 24 significand bits).  A product a*b is then
+// the six terms whose magnitude reaches 2^-16 |ab|: hh + (hm + mh) + (hl + lh + mm); the three
+// dropped terms are below 2^-23 |ab| together, i.e. at fp32 rounding level.  bf16 x bf16
+// products are exact in the fp32 accumulators.  hh goes to one accumulator, the five smaller
+// terms to a second one that is added at the end, so the big accumulator's rounding is the fp32
+// MFMA's own.  v_mfma_f32_16x16x32_bf16 does 16x the FLOPs per cycle of v_mfma_f32_16x16x4_f32,
+// so the six products cost 6/16 of the fp32 MFMA time (MI355X_MICROARCH.md, matrix cores).
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ f32x4 mfma_bf(const bf16x8 &a, const bf16x8 &b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// split two floats into their (h, m, l) bf16 pairs (v_cvt_pk_bf16_f32, round to nearest even)
+__device__ __forceinline__ void split2(float x0, float x1, bf16x2 &h, bf16x2 &m, bf16x2 &l) {
+    h = bf16x2{(__bf16)x0, (__bf16)x1};
+    const float r0 = x0 - (float)h[0], r1 = x1 - (float)h[1];
+    m = bf16x2{(__bf16)r0, (__bf16)r1};
+    l = bf16x2{(__bf16)(r0 - (float)m[0]), (__bf16)(r1 - (float)m[1])};
+}
+
+__device__ __forceinline__ void split4(const f32x4 &x, bf16x4 &h, bf16x4 &m, bf16x4 &l) {
+    bf16x2 h0, m0, l0, h1, m1, l1;
+    split2(x.x, x.y, h0, m0, l0);
+    split2(x.z, x.w, h1, m1, l1);
+    h = bf16x4{h0[0], h0[1], h1[0], h1[1]};
+    m = bf16x4{m0[0], m0[1], m1[0], m1[1]};
+    l = bf16x4{l0[0], l0[1], l1[0], l1[1]};
+}
+
+__device__ __forceinline__ void split8(const f32x4 &x0, const f32x4 &x1, bf16x8 &h, bf16x8 &m,
+                                       bf16x8 &l) {
+    bf16x4 h0, m0, l0, h1, m1, l1;
+    split4(x0, h0, m0, l0);
+    split4(x1, h1, m1, l1);
+    h = bf16x8{h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+    m = bf16x8{m0[0], m0[1], m0[2], m0[3], m1[0], m1[1], m1[2], m1[3]};
+    l = bf16x8{l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
+}
+
+__device__ __forceinline__ f32x16 mfma_bf32(const bf16x8 &a, const bf16x8 &b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// the same six products on v_mfma_f32_32x32x16_bf16 (32 x 32 tiles)
+__device__ __forceinline__ void mfma32_x6(const bf16x8 &ah, const bf16x8 &am, const bf16x8 &al,
+                                          const bf16x8 &bh, const bf16x8 &bm, const bf16x8 &bl,
+                                          f32x16 &big, f32x16 &small) {
+    small = mfma_bf32(al, bh, small);
+    small = mfma_bf32(ah, bl, small);
+    small = mfma_bf32(am, bm, small);
+    small = mfma_bf32(am, bh, small);
+    small = mfma_bf32(ah, bm, small);
+    big = mfma_bf32(ah, bh, big);
+}
+
+// acc_big += Ah Bh;  acc_small += Al Bh + Ah Bl + Am Bm + Am Bh + Ah Bm  (smallest terms first)
+__device__ __forceinline__ void mfma_x6(const bf16x8 &ah, const bf16x8 &am, const bf16x8 &al,
+                                        const bf16x8 &bh, const bf16x8 &bm, const bf16x8 &bl,
+                                        f32x4 &big, f32x4 &small) {
+    small = mfma_bf(al, bh, small);
+    small = mfma_bf(ah, bl, small);
+    small = mfma_bf(am, bm, small);
+    small = mfma_bf(am, bh, small);
+    small = mfma_bf(ah, bm, small);
+    big = mfma_bf(ah, bh, big);
+}
+
+
 // Two slices in flight: while the MFMAs consume slice s from LDS, the global loads of slices
 // s + 1 and s + 2 are outstanding in two register sets (HBM latency under full load is longer
 // than one slice of MFMAs).  load(set, s) issues slice s, store(set) writes it to LDS,
@@ -256,6 +329,58 @@ struct RowSlice4 {
         }
     }
 };
+
+// Layer-1 slice image for the bf16x6 path, one activation buffer (H_FLOATS floats) in size:
+// x as fp32 [64][LDS1] (split per fragment read: each x fragment feeds five N-tiles), then W1's
+// three bf16 planes [160][32] (64-byte rows, no pad), split once when staged.  A lane's
+// B fragment is 8 consecutive k of one row = one ds_read_b128 per plane; the 16-byte chunk c of
+// row n sits at chunk c ^ ((n >> 2) & 3), so the 16 rows a read spans cover all 64 banks.
+constexpr int L1X_BYTES = MB * LDS1 * 4;          // 9216
+constexpr int L1P_BYTES = 160 * BK * 2;           // 10240 per plane
+__device__ __forceinline__ uint32_t l1_wofs(int n, int k) {   // byte offset in a plane
+    return (uint32_t)(n * 64 + ((((k >> 3) ^ (n >> 2)) & 3) << 4) + (k & 7) * 2);
+}
+
+template <int ROWS>
+__device__ __forceinline__ void store_split_w(const RowSlice4<ROWS> &w, char *planes) {
+#pragma unroll
+    for (int i = 0; i < RowSlice4<ROWS>::PER; ++i) {
+        const int e = threadIdx.x + i * NTHR;
+        if (e < ROWS * RowSlice4<ROWS>::Q) {
+            const int n = e / RowSlice4<ROWS>::Q, k = 4 * (e % RowSlice4<ROWS>::Q);
+            bf16x4 h, m, l;
+            split4(w.v[i], h, m, l);
+            const uint32_t o = l1_wofs(n, k);
+            *reinterpret_cast<bf16x4 *>(planes + o) = h;
+            *reinterpret_cast<bf16x4 *>(planes + L1P_BYTES + o) = m;
+            *reinterpret_cast<bf16x4 *>(planes + 2 * L1P_BYTES + o) = l;
+        }
+    }
+}
+
+// One BK = 32 slice of layer 1 on the bf16x6 path: wave w owns M-tile (w & 3) and N-tiles
+// 5 (w >> 2) + t, as mma_rows64.
+__device__ __forceinline__ void mma_l1_x6(f32x4 (&big)[5], f32x4 (&small)[5], const float *xs,
+                                          const char *planes) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int m = (wave & 3) * 16 + (lane & 15), h = lane >> 4;
+    const float *xa = xs + m * LDS1 + 8 * h;
+    const f32x4 a0 = *reinterpret_cast<const f32x4 *>(xa);
+    const f32x4 a1 = *reinterpret_cast<const f32x4 *>(xa + 4);
+    bf16x8 bh[5], bm[5], bl[5];
+#pragma unroll
+    for (int t = 0; t < 5; ++t) {
+        const int n = (wave >> 2) * 80 + 16 * t + (lane & 15);
+        const uint32_t o = l1_wofs(n, 8 * h);
+        bh[t] = *reinterpret_cast<const bf16x8 *>(planes + o);
+        bm[t] = *reinterpret_cast<const bf16x8 *>(planes + L1P_BYTES + o);
+        bl[t] = *reinterpret_cast<const bf16x8 *>(planes + 2 * L1P_BYTES + o);
+    }
+    bf16x8 ah, am, al;
+    split8(a0, a1, ah, am, al);
+#pragma unroll
+    for (int t = 0; t < 5; ++t) mfma_x6(ah, am, al, bh[t], bm[t], bl[t], big[t], small[t]);
+}
 
 // BK rows [k0, k0 + BK) of a row-major [K][ld] matrix, columns [0, n_cols), zero outside, into
 // S[kl * LDT + n] (cols < 160)
@@ -481,7 +606,9 @@ struct MlpArgs {
 #define STAMP(i) \
     if (p.stamps && threadIdx.x == 0) p.stamps[(int64_t)blockIdx.x * 16 + (i)] = wall_clock64()
 
-template <bool TILED>
+// L1X6: layer 1 on the bf16 matrix cores with the exact 3-way split (bf16x6, above); false =
+// fp32 MFMA (DLAMD_MLP_L1=fp32, a measurement knob)
+template <bool TILED, bool L1X6>
 __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     float *H1 = lds, *H2 = lds + H_FLOATS, *H3 = lds + 2 * H_FLOATS;
@@ -519,7 +646,39 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
     ColSlice ta, tb;        // the same for the backward phases
     // ---- layer 1: H1 = relu(x W1^T + b1), K = din from HBM: x and W1 slices double-buffered in
     // LDS (the H2/H3 space, free until layer 2), the next two register-prefetched
-    {
+    if constexpr (L1X6) {
+        f32x4 acc[5], sml[5];
+        zero(acc);
+        zero(sml);
+        float bv[5];
+        load_bias5(mat(Xr, o_b1, 0), dh, bv);
+        static_assert(L1X_BYTES + 3 * L1P_BYTES <= H_FLOATS * 4, "a split slice image fits H2");
+        struct L1 {
+            RowSlice4<MB> x;
+            RowSlice4<160> w;
+        };
+        pipeline_db<L1>(
+            (din + BK - 1) / BK,
+            [&](L1 &v, int s) {
+                v.x.load(PlainMat{x, din}, MB, din, s * BK);
+                v.w.load(mat(Xr, o_w1, din), dh, din, s * BK);
+            },
+            [&](const L1 &v, int buf) {
+                float *img = H2 + buf * H_FLOATS;
+                v.x.store(img);
+                store_split_w(v.w, reinterpret_cast<char *>(img) + L1X_BYTES);
+            },
+            [&](int s, int buf) {
+                const float *img = H2 + buf * H_FLOATS;
+                mma_l1_x6(acc, sml, img, reinterpret_cast<const char *>(img) + L1X_BYTES);
+            });
+        prefetch_w(wa, wb, mat(Xr, o_w2, dh), dh);   // layer 2's first slices
+#pragma unroll
+        for (int t = 0; t < 5; ++t) acc[t] += sml[t];
+        epi_rows64_t(acc, [&](int m, int n, int t, float v) {
+            if (n < dh) H1[m * LDH + n] = act_fwd(0, v + bv[t]);
+        });
+    } else {
         f32x4 acc[5];
         zero(acc);
         float bv[5];
@@ -667,10 +826,103 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
     backward_dz(mat(Xr, o_w2, dh), dh, dh, H2, LDH, H1, stage, 0, ta, tb, [] {});  // dZ1 into H1
     __syncthreads();
     STAMP(9);
-    // ---- dW1 = dZ1^T x [dh x din] by 256-column chunks of x, staged in the H2/H3 space (free
-    // now: dZ2 and dZ3 are consumed); wave w owns the chunk's 32-column N-tile w and all five
-    // 32-row M-tiles (v_mfma_f32_32x32x2_f32); the next chunk is loaded during the MFMAs.  db1.
-    {
+    // ---- dW1 = dZ1^T x [dh x din], K = the 64 batch rows.
+    if constexpr (L1X6) {
+        // bf16x6 on v_mfma_f32_32x32x16_bf16.  Both operands are batch-major in LDS, the MFMA
+        // wants 8 consecutive k (= batch rows) per lane, so both are split once into bf16 planes
+        // stored TRANSPOSED, [row][64 batch] (128-byte rows, 16-byte chunk q of row r at
+        // q ^ ((r >> 1) & 7): a 16-lane group of a fragment read covers every bank):
+        //   dZ1^T planes [160][64] in the H2/H3 space (free: dZ2, dZ3 consumed), split once;
+        //   x chunk planes [96][64] in H1 (free once dZ1 is split), per 96-column chunk, the
+        //   next chunk's x register-prefetched during the MFMAs.
+        // Wave items = (N-tile, M-tile) 32 x 32 tiles of the chunk, K = 64 = 4 k-steps x 6
+        // products; tiles stored straight into G as before (store_tile).  db1 from x's ones
+        // column (din).
+        constexpr int CW = 96;                          // chunk columns (3 N-tiles)
+        constexpr int ROWB = MB * 2;                    // 128 bytes per transposed plane row
+        constexpr int AP = 160 * ROWB;                  // dZ1^T plane bytes
+        constexpr int XP = CW * ROWB;                   // x chunk plane bytes
+        static_assert(3 * AP <= 2 * H_FLOATS * 4, "dZ1^T planes fit the H2/H3 space");
+        static_assert(3 * XP <= H_FLOATS * 4, "x chunk planes fit H1");
+        char *aplanes = reinterpret_cast<char *>(H2);
+        char *xplanes = reinterpret_cast<char *>(H1);
+        auto tofs = [](int r, int b) {   // byte offset of (row r, batch b) in a transposed plane
+            return (uint32_t)(r * ROWB + ((((b >> 3) ^ (r >> 1)) & 7) << 4) + (b & 7) * 2);
+        };
+        // one item = 4 batch rows x 4 columns: 4 float4 in, 4 columns x 3 planes of bf16x4 out
+        auto split_store = [&](const f32x4 (&v)[4], int b0, int c, char *planes, int pbytes) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                bf16x4 h, m, l;
+                split4(f32x4{v[0][j], v[1][j], v[2][j], v[3][j]}, h, m, l);
+                const uint32_t o = tofs(c + j, b0);
+                *reinterpret_cast<bf16x4 *>(planes + o) = h;
+                *reinterpret_cast<bf16x4 *>(planes + pbytes + o) = m;
+                *reinterpret_cast<bf16x4 *>(planes + 2 * pbytes + o) = l;
+            }
+        };
+        constexpr int XITEMS = (MB / 4) * (CW / 4);    // 384 items per chunk
+        f32x4 xv[4];
+        const bool xt = tid < XITEMS;
+        const int xb0 = 4 * (tid / (CW / 4)), xc = 4 * (tid % (CW / 4));
+        auto load = [&](int c0) {
+            if (!xt) return;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int c = c0 + xc;
+                // column din is the ones column (db1); din % 4 == 0 puts it at a float4 start
+                xv[i] = c < din ? *reinterpret_cast<const f32x4 *>(x + (int64_t)(xb0 + i) * din + c)
+                        : c == din ? f32x4{1.f, 0.f, 0.f, 0.f} : f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+        };
+        load(0);
+        // dZ1^T planes from H1 (fp32 [b][LDH]; columns dh.. hold the ones column / zeros and
+        // only feed rows >= dh, which store_tile skips)
+        for (int e = tid; e < (MB / 4) * 40; e += NTHR) {
+            const int b0 = 4 * (e / 40), i0 = 4 * (e % 40);
+            f32x4 v[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                v[i] = i0 + 3 < LDH ? *reinterpret_cast<const f32x4 *>(H1 + (b0 + i) * LDH + i0)
+                                    : f32x4{0.f, 0.f, 0.f, 0.f};
+            split_store(v, b0, i0, aplanes, AP);
+        }
+        __syncthreads();   // H1 (dZ1 fp32) is read: the x planes may overwrite it
+        const int nc = (din + CW) / CW;          // through column din (the ones column)
+        const PM gw1 = mat(Gr, o_w1, din), gb1 = mat(Gr, o_b1, 0);
+        const int r = lane & 31, hh = lane >> 5;
+        for (int ci = 0; ci < nc; ++ci) {
+            if (xt) split_store(xv, xb0, xc, xplanes, XP);
+            __syncthreads();
+            const int c0 = ci * CW;
+            if (ci + 1 < nc) load(c0 + CW);
+            const int ntc = min(CW / 32, (din + 1 - c0 + 31) / 32);
+            for (int it = wave; it < 5 * ntc; it += 8) {
+                const int nt = it % ntc, t = it / ntc;
+                f32x16 big, sml;
+#pragma unroll
+                for (int q = 0; q < 16; ++q) big[q] = sml[q] = 0.f;
+#pragma unroll
+                for (int ks = 0; ks < MB / 16; ++ks) {
+                    const int b = 16 * ks + 8 * hh;
+                    const uint32_t oa = tofs(32 * t + r, b), ob = tofs(32 * nt + r, b);
+                    const bf16x8 ah = *reinterpret_cast<const bf16x8 *>(aplanes + oa);
+                    const bf16x8 am = *reinterpret_cast<const bf16x8 *>(aplanes + AP + oa);
+                    const bf16x8 al = *reinterpret_cast<const bf16x8 *>(aplanes + 2 * AP + oa);
+                    const bf16x8 bh = *reinterpret_cast<const bf16x8 *>(xplanes + ob);
+                    const bf16x8 bm = *reinterpret_cast<const bf16x8 *>(xplanes + XP + ob);
+                    const bf16x8 bl = *reinterpret_cast<const bf16x8 *>(xplanes + 2 * XP + ob);
+                    mfma32_x6(ah, am, al, bh, bm, bl, big, sml);
+                }
+                big += sml;
+                store_tile(big, 32 * t + 4 * hh, c0 + 32 * nt + r, gw1, dh, din, gb1);
+            }
+            __syncthreads();
+        }
+    } else {
+    // fp32: dW1 by 256-column chunks of x, staged in the H2/H3 space (free now: dZ2 and dZ3
+    // are consumed); wave w owns the chunk's 32-column N-tile w and all five 32-row M-tiles
+    // (v_mfma_f32_32x32x2_f32); the next chunk is loaded during the MFMAs.  db1.
         constexpr int CW = 256, LDC = 288;   // chunk width, row stride (= 32 mod 64)
         static_assert(MB * LDC <= 2 * H_FLOATS, "x chunk fits the H2/H3 space");
         float *xs = H2;
@@ -741,17 +993,20 @@ hipError_t launch_mlp_fused(const float *X, int64_t ldx, const float *data, int6
     while (tile_cols > 0 && (1 << tsh) < tile_cols) ++tsh;
     MlpArgs p{X, ldx, data, s_data, labels, s_lab, G, ldg, loss, din, dh, dout, tsh,
               (int64_t)n_agents * tile_cols, nullptr};
-    const void *k = tile_cols > 0 ? reinterpret_cast<const void *>(mlp_fused_kernel<true>)
-                                  : reinterpret_cast<const void *>(mlp_fused_kernel<false>);
-    hipError_t e = allow_full_lds(k);
-    if (e != hipSuccess) return e;
+    static const bool l1_fp32 = [] {
+        const char *v = getenv("DLAMD_MLP_L1");
+        return v && v[0] == 'f';
+    }();
+    auto go = [&](auto kern) {
+        hipError_t e = allow_full_lds(reinterpret_cast<const void *>(kern));
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(kern, dim3((unsigned)n_agents), dim3(NTHR),
+                           LDS_FLOATS * sizeof(float), s, p);
+        return hipGetLastError();
+    };
     if (tile_cols > 0)
-        hipLaunchKernelGGL(mlp_fused_kernel<true>, dim3((unsigned)n_agents), dim3(NTHR),
-                           LDS_FLOATS * sizeof(float), s, p);
-    else
-        hipLaunchKernelGGL(mlp_fused_kernel<false>, dim3((unsigned)n_agents), dim3(NTHR),
-                           LDS_FLOATS * sizeof(float), s, p);
-    return hipGetLastError();
+        return l1_fp32 ? go(mlp_fused_kernel<true, false>) : go(mlp_fused_kernel<true, true>);
+    return l1_fp32 ? go(mlp_fused_kernel<false, false>) : go(mlp_fused_kernel<false, true>);
 }
 
 }  // namespace dl

@@ -23,7 +23,10 @@ hipError_t allow_full_lds(const void *k) {
 }
 }  // namespace dl
 
-int main() {
+int main(int argc, char **argv) {
+    // argv[1] == "fp32": layer 1 and dW1 on the fp32 MFMA (default: the bf16x6 split)
+    const bool x6 = !(argc > 1 && argv[1][0] == 'f');
+    auto kern = x6 ? dl::mlp_fused_kernel<false, true> : dl::mlp_fused_kernel<false, false>;
     const int N = 256, B = 64, din = 784, dh = 150, dout = 10;
     const long P = (long)dh * din + dh + 2 * (dh * dh + dh) + dout * dh + dout;
     const long ld = (P + 63) / 64 * 64;
@@ -46,7 +49,7 @@ int main() {
     CHECK(hipMemcpy(X, hx.data(), hx.size() * 4, hipMemcpyHostToDevice));
     CHECK(hipMemcpy(D, hd.data(), hd.size() * 4, hipMemcpyHostToDevice));
     CHECK(hipMemcpy(Y, hl.data(), hl.size() * 4, hipMemcpyHostToDevice));
-    CHECK(dl::allow_full_lds(reinterpret_cast<const void *>(dl::mlp_fused_kernel<false>)));
+    CHECK(dl::allow_full_lds(reinterpret_cast<const void *>(kern)));
     dl::MlpArgs p{X, ld, D, (long)B * din, Y, B, G, ld, L, din, dh, dout, 0, 0, st};
     int rate_khz = 0;
     CHECK(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, 0));
@@ -57,7 +60,7 @@ int main() {
     CHECK(hipEventCreate(&e1));
     for (int rep = 0; rep < 6; ++rep) {
         CHECK(hipEventRecord(e0));
-        hipLaunchKernelGGL(dl::mlp_fused_kernel<false>, dim3(N), dim3(dl::NTHR),
+        hipLaunchKernelGGL(kern, dim3(N), dim3(dl::NTHR),
                            dl::LDS_FLOATS * sizeof(float), 0, p);
         CHECK(hipEventRecord(e1));
         CHECK(hipDeviceSynchronize());

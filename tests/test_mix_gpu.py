@@ -412,3 +412,4 @@ def test_tcp_run_once_round(cuda, edges, w):
     assert np.array_equal(bits(got), bits(M.mix_once(X, csr.rowptr, csr.col, csr.w)))
     want = M.tcp_run_once(edges, w, {k: X[i] for i, k in enumerate(csr.keys)})
     np.testing.assert_allclose(got, np.stack([want[k] for k in csr.keys]), rtol=1e-5, atol=1e-6)
+

@@ -33,7 +33,7 @@ namespace {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 #ifndef MLP_PROBE_MODE
-#define MLP_PROBE_MODE 0   // scripts/mlp_probe builds 1 and 2 to time the phases' parts
+#define MLP_PROBE_MODE 0   // scripts/mlp_probe builds measurement variants (modes below)
 #endif
 
 constexpr int NTHR = 512;     // 8 waves, 2 per SIMD
@@ -89,22 +89,18 @@ __device__ __forceinline__ void split2(float x0, float x1, bf16x2 &h, bf16x2 &m,
 }
 
 __device__ __forceinline__ void split4(const f32x4 &x, bf16x4 &h, bf16x4 &m, bf16x4 &l) {
+#if MLP_PROBE_MODE == 10   // measurement only: no split arithmetic (raw bits as the planes)
+    h = __builtin_bit_cast(bf16x4, __builtin_shufflevector(x, x, 0, 1));
+    m = __builtin_bit_cast(bf16x4, __builtin_shufflevector(x, x, 2, 3));
+    l = h;
+    return;
+#endif
     bf16x2 h0, m0, l0, h1, m1, l1;
     split2(x.x, x.y, h0, m0, l0);
     split2(x.z, x.w, h1, m1, l1);
     h = bf16x4{h0[0], h0[1], h1[0], h1[1]};
     m = bf16x4{m0[0], m0[1], m1[0], m1[1]};
     l = bf16x4{l0[0], l0[1], l1[0], l1[1]};
-}
-
-__device__ __forceinline__ void split8(const f32x4 &x0, const f32x4 &x1, bf16x8 &h, bf16x8 &m,
-                                       bf16x8 &l) {
-    bf16x4 h0, m0, l0, h1, m1, l1;
-    split4(x0, h0, m0, l0);
-    split4(x1, h1, m1, l1);
-    h = bf16x8{h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
-    m = bf16x8{m0[0], m0[1], m0[2], m0[3], m1[0], m1[1], m1[2], m1[3]};
-    l = bf16x8{l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
 }
 
 __device__ __forceinline__ f32x16 mfma_bf32(const bf16x8 &a, const bf16x8 &b, f32x16 c) {
@@ -282,24 +278,33 @@ struct PlainMat {
 // ---------------------------------------------------------------- staging (global -> LDS)
 // rows x BK slice of a row-major [rows][ld] matrix, columns [k0, k0 + BK), zero outside
 // [0, n_rows) x [0, K), into S[r * LDS1 + c].  Register-prefetched: load() then store().
+// Every load issues unconditionally from a clamped in-range address and the out-of-range
+// elements are zeroed in store(), at the registers' only use: a load the compiler may branch
+// around, or a select right after it, makes the wait before the store a vmcnt(0) that drains
+// every slice in flight (as the layer-1 producer measured).
 template <int ROWS>
 struct RowSlice {
     static constexpr int PER = (ROWS * BK + NTHR - 1) / NTHR;
     float v[PER];
+    int k0_, nr_, K_;
     template <typename M>
     __device__ __forceinline__ void load(const M &W, int n_rows, int K, int k0) {
+        k0_ = k0;
+        nr_ = n_rows;
+        K_ = K;
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
             const int e = threadIdx.x + i * NTHR;
             const int r = e / BK, c = e % BK;
-            v[i] = (e < ROWS * BK && r < n_rows && k0 + c < K) ? *W.at(r, k0 + c) : 0.f;
+            v[i] = *W.at(r < n_rows ? r : n_rows - 1, k0 + c < K ? k0 + c : K - 1);
         }
     }
     __device__ __forceinline__ void store(float *S) const {
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
             const int e = threadIdx.x + i * NTHR;
-            if (e < ROWS * BK) S[(e / BK) * LDS1 + e % BK] = v[i];
+            const int r = e / BK, c = e % BK;
+            if (e < ROWS * BK) S[r * LDS1 + c] = (r < nr_ && k0_ + c < K_) ? v[i] : 0.f;
         }
     }
 };
@@ -330,77 +335,42 @@ struct RowSlice4 {
     }
 };
 
-// Layer-1 slice image for the bf16x6 path, one activation buffer (H_FLOATS floats) in size:
-// x as fp32 [64][LDS1] (split per fragment read: each x fragment feeds five N-tiles), then W1's
-// three bf16 planes [160][32] (64-byte rows, no pad), split once when staged.  A lane's
-// B fragment is 8 consecutive k of one row = one ds_read_b128 per plane; the 16-byte chunk c of
-// row n sits at chunk c ^ ((n >> 2) & 3), so the 16 rows a read spans cover all 64 banks.
-constexpr int L1X_BYTES = MB * LDS1 * 4;          // 9216
+// bf16x6 layer-1 planes: x [64][32] and W1 [160][32] bf16 per plane (64-byte rows, no pad),
+// split once when the producer waves stage them.  A lane's fragment is 8 consecutive k of one
+// row = one ds_read_b128 per plane; the 16-byte chunk c of row n sits at chunk c ^ ((n >> 2) & 3),
+// so the 16 rows a read spans cover all 64 banks.
+#ifndef L1_RING
+#define L1_RING 4                                 // layer-1 slices in flight (producer register sets)
+#endif
 constexpr int L1P_BYTES = 160 * BK * 2;           // 10240 per plane
 __device__ __forceinline__ uint32_t l1_wofs(int n, int k) {   // byte offset in a plane
     return (uint32_t)(n * 64 + ((((k >> 3) ^ (n >> 2)) & 3) << 4) + (k & 7) * 2);
 }
 
-template <int ROWS>
-__device__ __forceinline__ void store_split_w(const RowSlice4<ROWS> &w, char *planes) {
-#pragma unroll
-    for (int i = 0; i < RowSlice4<ROWS>::PER; ++i) {
-        const int e = threadIdx.x + i * NTHR;
-        if (e < ROWS * RowSlice4<ROWS>::Q) {
-            const int n = e / RowSlice4<ROWS>::Q, k = 4 * (e % RowSlice4<ROWS>::Q);
-            bf16x4 h, m, l;
-            split4(w.v[i], h, m, l);
-            const uint32_t o = l1_wofs(n, k);
-            *reinterpret_cast<bf16x4 *>(planes + o) = h;
-            *reinterpret_cast<bf16x4 *>(planes + L1P_BYTES + o) = m;
-            *reinterpret_cast<bf16x4 *>(planes + 2 * L1P_BYTES + o) = l;
-        }
-    }
-}
-
-// One BK = 32 slice of layer 1 on the bf16x6 path: wave w owns M-tile (w & 3) and N-tiles
-// 5 (w >> 2) + t, as mma_rows64.
-__device__ __forceinline__ void mma_l1_x6(f32x4 (&big)[5], f32x4 (&small)[5], const float *xs,
-                                          const char *planes) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int m = (wave & 3) * 16 + (lane & 15), h = lane >> 4;
-    const float *xa = xs + m * LDS1 + 8 * h;
-    const f32x4 a0 = *reinterpret_cast<const f32x4 *>(xa);
-    const f32x4 a1 = *reinterpret_cast<const f32x4 *>(xa + 4);
-    bf16x8 bh[5], bm[5], bl[5];
-#pragma unroll
-    for (int t = 0; t < 5; ++t) {
-        const int n = (wave >> 2) * 80 + 16 * t + (lane & 15);
-        const uint32_t o = l1_wofs(n, 8 * h);
-        bh[t] = *reinterpret_cast<const bf16x8 *>(planes + o);
-        bm[t] = *reinterpret_cast<const bf16x8 *>(planes + L1P_BYTES + o);
-        bl[t] = *reinterpret_cast<const bf16x8 *>(planes + 2 * L1P_BYTES + o);
-    }
-    bf16x8 ah, am, al;
-    split8(a0, a1, ah, am, al);
-#pragma unroll
-    for (int t = 0; t < 5; ++t) mfma_x6(ah, am, al, bh[t], bm[t], bl[t], big[t], small[t]);
-}
-
 // BK rows [k0, k0 + BK) of a row-major [K][ld] matrix, columns [0, n_cols), zero outside, into
 // S[kl * LDT + n] (cols < 160)
-struct ColSlice {
+struct ColSlice {   // loads unconditional, zeroing in store() (see RowSlice)
     static constexpr int PER = BK * 160 / NTHR;  // 10
     float v[PER];
+    int k0_, nc_, K_;
     template <typename M>
     __device__ __forceinline__ void load(const M &W, int n_cols, int K, int k0) {
+        k0_ = k0;
+        nc_ = n_cols;
+        K_ = K;
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
             const int e = threadIdx.x + i * NTHR;
             const int kl = e / 160, n = e % 160;
-            v[i] = (n < n_cols && k0 + kl < K) ? *W.at(k0 + kl, n) : 0.f;
+            v[i] = *W.at(k0 + kl < K ? k0 + kl : K - 1, n < n_cols ? n : n_cols - 1);
         }
     }
     __device__ __forceinline__ void store(float *S) const {
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
             const int e = threadIdx.x + i * NTHR;
-            S[(e / 160) * LDT + e % 160] = v[i];
+            const int kl = e / 160, n = e % 160;
+            S[kl * LDT + n] = (n < nc_ && k0_ + kl < K_) ? v[i] : 0.f;
         }
     }
 };
@@ -647,37 +617,133 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
     // ---- layer 1: H1 = relu(x W1^T + b1), K = din from HBM: x and W1 slices double-buffered in
     // LDS (the H2/H3 space, free until layer 2), the next two register-prefetched
     if constexpr (L1X6) {
-        f32x4 acc[5], sml[5];
-        zero(acc);
-        zero(sml);
-        float bv[5];
-        load_bias5(mat(Xr, o_b1, 0), dh, bv);
-        static_assert(L1X_BYTES + 3 * L1P_BYTES <= H_FLOATS * 4, "a split slice image fits H2");
-        struct L1 {
-            RowSlice4<MB> x;
-            RowSlice4<160> w;
-        };
-        pipeline_db<L1>(
-            (din + BK - 1) / BK,
-            [&](L1 &v, int s) {
-                v.x.load(PlainMat{x, din}, MB, din, s * BK);
-                v.w.load(mat(Xr, o_w1, din), dh, din, s * BK);
-            },
-            [&](const L1 &v, int buf) {
-                float *img = H2 + buf * H_FLOATS;
-                v.x.store(img);
-                store_split_w(v.w, reinterpret_cast<char *>(img) + L1X_BYTES);
-            },
-            [&](int s, int buf) {
-                const float *img = H2 + buf * H_FLOATS;
-                mma_l1_x6(acc, sml, img, reinterpret_cast<const char *>(img) + L1X_BYTES);
-            });
-        prefetch_w(wa, wb, mat(Xr, o_w2, dh), dh);   // layer 2's first slices
+        // Warp-specialised: waves 4-7 (one per SIMD) load slice s + 2 from HBM and split slice
+        // s into bf16 planes while waves 0-3 (the other wave of each SIMD) run slice s - 1's
+        // MFMAs, one barrier per slice.  (Both roles in every wave, split between barriers,
+        // measured: the split VALU and the LDS stores did not overlap the MFMAs -- 47.8 us.)
+        // Images: x planes [64][32] and W1 planes [160][32] (bf16, l1_wofs layout), 43 KB each,
+        // two of them across H2, H3 and the staging area (contiguous, all free until layer 2).
+        constexpr int XPL = MB * BK * 2;                    // 4096 bytes per x plane
+        constexpr int IMGB = 3 * XPL + 3 * L1P_BYTES;       // 43008
+        static_assert(2 * IMGB <= (2 * H_FLOATS + STAGE_FLOATS) * 4, "two L1 images fit");
+        char *img0 = reinterpret_cast<char *>(H2);
+        const int ns = (din + BK - 1) / BK;
+        if (wave >= 4) {
+            const int pt = tid - NTHR / 2;                  // 0..255
+            constexpr int XQ = MB * BK / 4 / (NTHR / 2);    // 2 float4 of x per thread
+            constexpr int WQ = 160 * BK / 4 / (NTHR / 2);   // 5 float4 of W1 per thread
+            f32x4 rx[L1_RING][XQ], rw[L1_RING][WQ];   // L1_RING slices in flight
+            const PM W1 = mat(Xr, o_w1, din);
+            // Every load instruction issues unconditionally (out-of-range lanes read a clamped
+            // in-range address and are zeroed by a select afterwards): a load the compiler may
+            // skip -- a branch around it, or a slice not fetched -- makes the number of younger
+            // loads unknown, and the wait before a set's LDS store degrades to vmcnt(0), which
+            // drains every slice in flight (measured on this kernel: all 61 waits were vmcnt(0)).
+            auto load = [&](int set, int sl) {
+#if MLP_PROBE_MODE == 2   // measurement only: every slice re-reads slice 0 (L2-resident)
+                sl = 0;
+#endif
+                const int k0 = sl * BK;
 #pragma unroll
-        for (int t = 0; t < 5; ++t) acc[t] += sml[t];
-        epi_rows64_t(acc, [&](int m, int n, int t, float v) {
-            if (n < dh) H1[m * LDH + n] = act_fwd(0, v + bv[t]);
-        });
+                for (int i = 0; i < XQ; ++i) {
+                    const int e = pt + i * (NTHR / 2), r = e / 8, c = 4 * (e % 8);
+                    rx[set][i] = *reinterpret_cast<const f32x4 *>(
+                        x + (int64_t)r * din + (k0 + c < din ? k0 + c : din - 4));
+                }
+#pragma unroll
+                for (int i = 0; i < WQ; ++i) {
+                    const int e = pt + i * (NTHR / 2), r = e / 8, c = 4 * (e % 8);
+                    rw[set][i] = *reinterpret_cast<const f32x4 *>(
+                        W1.at(r < dh ? r : dh - 1, k0 + c < din ? k0 + c : din - 4));
+                }
+            };
+            // the out-of-range lanes are zeroed here, at the registers' only use (a select next
+            // to the load would be the load's first use, and the wait would move there)
+            auto store = [&](int set, int sl, char *img) {
+                const int k0 = sl * BK;
+                const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int i = 0; i < XQ; ++i) {
+                    const int e = pt + i * (NTHR / 2), r = e / 8, c = 4 * (e % 8);
+                    bf16x4 h, m, l;
+                    split4(k0 + c < din ? rx[set][i] : z, h, m, l);
+                    const uint32_t o = l1_wofs(r, c);
+                    *reinterpret_cast<bf16x4 *>(img + o) = h;
+                    *reinterpret_cast<bf16x4 *>(img + XPL + o) = m;
+                    *reinterpret_cast<bf16x4 *>(img + 2 * XPL + o) = l;
+                }
+                char *wpl = img + 3 * XPL;
+#pragma unroll
+                for (int i = 0; i < WQ; ++i) {
+                    const int e = pt + i * (NTHR / 2), r = e / 8, c = 4 * (e % 8);
+                    bf16x4 h, m, l;
+                    split4(r < dh && k0 + c < din ? rw[set][i] : z, h, m, l);
+                    const uint32_t o = l1_wofs(r, c);
+                    *reinterpret_cast<bf16x4 *>(wpl + o) = h;
+                    *reinterpret_cast<bf16x4 *>(wpl + L1P_BYTES + o) = m;
+                    *reinterpret_cast<bf16x4 *>(wpl + 2 * L1P_BYTES + o) = l;
+                }
+            };
+            // loads past the last slice re-read it (unconditional issue, see load)
+#pragma unroll
+            for (int j = 0; j < L1_RING; ++j) load(j, j < ns ? j : ns - 1);
+            for (int s0 = 0; s0 < ns; s0 += L1_RING) {
+#pragma unroll
+                for (int j = 0; j < L1_RING; ++j) {   // register set j holds slice s0 + j
+                    const int sl = s0 + j;
+                    if (sl < ns) store(j, sl, img0 + (sl & 1) * IMGB);
+                    load(j, sl + L1_RING < ns ? sl + L1_RING : ns - 1);
+                    if (sl < ns) __syncthreads();
+                }
+            }
+        } else {
+            // wave c: M-tile c (rows 16c..16c+15) x all ten 16-column N-tiles
+            f32x4 acc[10], sml[10];
+#pragma unroll
+            for (int t = 0; t < 10; ++t) acc[t] = sml[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+            float bv[10];
+#pragma unroll
+            for (int t = 0; t < 10; ++t) {
+                const int n = 16 * t + (lane & 15);
+                bv[t] = n < dh ? *Xr.at(o_b1 + n) : 0.f;
+            }
+            const int m = wave * 16 + (lane & 15), hq = lane >> 4;
+            auto compute = [&](const char *img) {
+#if MLP_PROBE_MODE != 1   // measurement only: 1 = no MFMAs
+                const uint32_t oa = l1_wofs(m, 8 * hq);
+                const bf16x8 ah = *reinterpret_cast<const bf16x8 *>(img + oa);
+                const bf16x8 am = *reinterpret_cast<const bf16x8 *>(img + XPL + oa);
+                const bf16x8 al = *reinterpret_cast<const bf16x8 *>(img + 2 * XPL + oa);
+                const char *wpl = img + 3 * XPL;
+#pragma unroll
+                for (int t = 0; t < 10; ++t) {
+                    const uint32_t ob = l1_wofs(16 * t + (lane & 15), 8 * hq);
+                    const bf16x8 bh = *reinterpret_cast<const bf16x8 *>(wpl + ob);
+                    const bf16x8 bm = *reinterpret_cast<const bf16x8 *>(wpl + L1P_BYTES + ob);
+                    const bf16x8 bl = *reinterpret_cast<const bf16x8 *>(wpl + 2 * L1P_BYTES + ob);
+                    mfma_x6(ah, am, al, bh, bm, bl, acc[t], sml[t]);
+                }
+#else
+                (void)img;
+#endif
+            };
+            for (int sl = 0; sl < ns; ++sl) {
+                if (sl > 0) compute(img0 + ((sl - 1) & 1) * IMGB);
+                __syncthreads();
+            }
+            compute(img0 + ((ns - 1) & 1) * IMGB);
+#pragma unroll
+            for (int t = 0; t < 10; ++t) {
+                acc[t] += sml[t];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = wave * 16 + 4 * hq + r, n = 16 * t + (lane & 15);
+                    if (n < dh) H1[row * LDH + n] = act_fwd(0, acc[t][r] + bv[t]);
+                }
+            }
+        }
+        prefetch_w(wa, wb, mat(Xr, o_w2, dh), dh);   // layer 2's first slices
+        __syncthreads();   // every consumer is done with the images before H2/H3 are written
     } else {
         f32x4 acc[5];
         zero(acc);
@@ -834,7 +900,7 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
         // q ^ ((r >> 1) & 7): a 16-lane group of a fragment read covers every bank):
         //   dZ1^T planes [160][64] in the H2/H3 space (free: dZ2, dZ3 consumed), split once;
         //   x chunk planes [96][64] in H1 (free once dZ1 is split), per 96-column chunk, the
-        //   next chunk's x register-prefetched during the MFMAs.
+        //   next two chunks' x register-prefetched during the MFMAs.
         // Wave items = (N-tile, M-tile) 32 x 32 tiles of the chunk, K = 64 = 4 k-steps x 6
         // products; tiles stored straight into G as before (store_tile).  db1 from x's ones
         // column (din).
@@ -862,10 +928,10 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
             }
         };
         constexpr int XITEMS = (MB / 4) * (CW / 4);    // 384 items per chunk
-        f32x4 xv[4];
+        f32x4 xva[4], xvb[4];                          // two chunks in flight
         const bool xt = tid < XITEMS;
         const int xb0 = 4 * (tid / (CW / 4)), xc = 4 * (tid % (CW / 4));
-        auto load = [&](int c0) {
+        auto load = [&](f32x4 (&xv)[4], int c0) {
             if (!xt) return;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -875,7 +941,8 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
                         : c == din ? f32x4{1.f, 0.f, 0.f, 0.f} : f32x4{0.f, 0.f, 0.f, 0.f};
             }
         };
-        load(0);
+        load(xva, 0);
+        load(xvb, CW);
         // dZ1^T planes from H1 (fp32 [b][LDH]; columns dh.. hold the ones column / zeros and
         // only feed rows >= dh, which store_tile skips)
         for (int e = tid; e < (MB / 4) * 40; e += NTHR) {
@@ -891,11 +958,11 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
         const int nc = (din + CW) / CW;          // through column din (the ones column)
         const PM gw1 = mat(Gr, o_w1, din), gb1 = mat(Gr, o_b1, 0);
         const int r = lane & 31, hh = lane >> 5;
-        for (int ci = 0; ci < nc; ++ci) {
+        auto chunk = [&](int ci, f32x4 (&xv)[4]) {
             if (xt) split_store(xv, xb0, xc, xplanes, XP);
             __syncthreads();
             const int c0 = ci * CW;
-            if (ci + 1 < nc) load(c0 + CW);
+            if (ci + 2 < nc) load(xv, c0 + 2 * CW);
             const int ntc = min(CW / 32, (din + 1 - c0 + 31) / 32);
             for (int it = wave; it < 5 * ntc; it += 8) {
                 const int nt = it % ntc, t = it / ntc;
@@ -918,6 +985,10 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
                 store_tile(big, 32 * t + 4 * hh, c0 + 32 * nt + r, gw1, dh, din, gb1);
             }
             __syncthreads();
+        };
+        for (int ci = 0; ci < nc; ci += 2) {
+            chunk(ci, xva);
+            if (ci + 1 < nc) chunk(ci + 1, xvb);
         }
     } else {
     // fp32: dW1 by 256-column chunks of x, staged in the H2/H3 space (free now: dZ2 and dZ3

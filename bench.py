@@ -398,8 +398,8 @@ def run_c3(args, dev, rank, world):
     gbs = mix_bytes / (mix_ms / 1e3) / 1e9
     if rank != 0:
         return
-    # HBM bytes per launch from the committed PMC passes of this workload (profiles/r05/c3)
-    c3_path = os.path.join(ROOT, "profiles", "r05", "c3", "summary.json")
+    # HBM bytes per launch from the committed PMC passes of this workload (profiles/r08/c3)
+    c3_path = os.path.join(ROOT, "profiles", "r08", "c3", "summary.json")
     c3_grad_traffic, c3_src = (traffic_from_profile("mlp_fused_kernel", c3_path)
                                if ann.path == "fused" and args.c3_layout == "rows"
                                else (None, None))
@@ -410,7 +410,11 @@ def run_c3(args, dev, rank, world):
                  "traffic": c3_grad_traffic, "traffic_source": c3_src if c3_grad_traffic else None,
                  "kernel": ("mlp_fused_kernel" if ann.path == "fused" else
                             "dl_bgemm x11 + dl_xent_grad") + " (per-step HIP-event time)",
-                 "flops_per_launch": flops, "launch_ms": grad_ms}
+                 "flops_per_launch": flops, "launch_ms": grad_ms,
+                 "arithmetic": "fp32 GEMMs: hidden layers on the fp32 MFMA; layer 1 and dW1 on the "
+                               "bf16 matrix cores as exact 3-way bf16 splits (six products, "
+                               "csrc/mlp_fused.hip); achieved counts the fp32 FLOPs, peak is the "
+                               "fp32 MFMA peak"}
     mix_roof = {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": gbs / HBM_PEAK_GBS, "traffic": c3_mix_traffic,
                 "traffic_source": c3_src if c3_mix_traffic else None,

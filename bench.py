@@ -208,7 +208,7 @@ def kernel_name(plan, sgd, dev, n_src):
     return f"mix_tile_kernel<{c}, {kv}, {b(sgd)}, {b(dev)}, true, false, true>"
 
 
-def traffic_from_profile(kname, path=os.path.join(ROOT, "profiles", "r05", "summary.json")):
+def traffic_from_profile(kname, path=os.path.join(ROOT, "profiles", "r08", "summary.json")):
     """HBM bytes per launch of this kernel from the committed rocprofv3 PMC summary
     (FETCH_SIZE x 2 + WRITE_SIZE, gfx950 correction), or None if it was not profiled."""
     try:

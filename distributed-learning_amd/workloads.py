@@ -64,10 +64,14 @@ class ConsensusGDRun:
     consensus rounds (weighted by shard size, ``convergence_eps`` one-sided test), fp64 on the
     device with no host round trip per iteration.  The constructor makes everything resident
     (shards, adjacency, step sizes, zero weights); ``launch()`` is stream-ordered; ``result()``
-    copies back ({token: final w}, Jacobi iterations per round)."""
+    copies back ({token: final w}, Jacobi iterations per round).
+    ``edge_weight``: mix with a uniform per-edge weight w (x' = x(1 - w deg) + w sum_j x_j, the
+    TCP agent's update with a fast-averaging weight, consensus_tcp/agent.py:204-207) instead of
+    the asyncio network's Perron eps 0.95 / max degree (consensus_asyncio.py:78-86).  The FDLA
+    optimum is such a uniform weight on edge-transitive graphs (ring, torus)."""
 
     def __init__(self, topology, X, y, iterations, alpha=1e-1, tau=1e-4, convergence_eps=1e-10,
-                 schedule="sqrt", device=None, max_iter=10_000_000):
+                 schedule="sqrt", device=None, max_iter=10_000_000, edge_weight=None):
         import torch
 
         from . import _lib
@@ -93,7 +97,8 @@ class ConsensusGDRun:
         t = self.t
         self.args = _lib.DlConsensusGdArgs(
             _lib.ptr(t["X"]), _lib.ptr(t["y"]), _lib.ptr(t["sp"]), len(self.tokens), F,
-            _lib.ptr(t["rp"]), _lib.ptr(t["cl"]), float(perron_eps(topology, self.tokens)),
+            _lib.ptr(t["rp"]), _lib.ptr(t["cl"]),
+            float(perron_eps(topology, self.tokens) if edge_weight is None else edge_weight),
             float(convergence_eps), sum(sizes) / len(sizes), float(tau), _lib.ptr(t["steps"]),
             self.iterations, int(max_iter), _lib.ptr(t["w"]), _lib.ptr(self.iters))
 
@@ -114,11 +119,11 @@ class ConsensusGDRun:
 
 
 def consensus_gd_device(topology, X, y, iterations, alpha=1e-1, tau=1e-4, convergence_eps=1e-10,
-                        schedule="sqrt", device=None, max_iter=10_000_000):
+                        schedule="sqrt", device=None, max_iter=10_000_000, edge_weight=None):
     """One-launch ``consensus_gd`` (ConsensusGDRun).  Returns ({token: final w}, Jacobi
     iterations per round)."""
     run = ConsensusGDRun(topology, X, y, iterations, alpha, tau, convergence_eps, schedule,
-                         device, max_iter)
+                         device, max_iter, edge_weight)
     run.launch()
     return run.result()
 

@@ -125,7 +125,7 @@ def perron_eps(topology, tokens):
     return 0.95 / np.max(np.sum(E, axis=1))
 
 
-def jacobi_round(topology, values, weights, conv_eps, max_iter=1_000_000):
+def jacobi_round(topology, values, weights, conv_eps, max_iter=1_000_000, edge_weight=None):
     """Synchronous restatement of one ``ConsensusAgent.run_round`` over all agents.
 
     values/weights: dicts token -> ndarray / number.  Pre-scale ``y = v * w / mean_w``
@@ -133,10 +133,13 @@ def jacobi_round(topology, values, weights, conv_eps, max_iter=1_000_000):
     ``y <- y*(1 - eps*deg) + eps*sum(nbr y)`` (:295); agent flag
     ``all((y - v) <= conv_eps for v in nbr values)`` with the neighbours' PRE-update values
     (:297); stop at the first iteration where every flag is set (master DONE, :170-174).
-    Returns (dict token -> y, k).
+    Returns (dict token -> y, k).  ``edge_weight``: a uniform mixing weight per edge in place of
+    the Perron eps (x' = x + w sum_j (x_j - x) in the (1 - w deg) form above: the TCP agent's
+    update, consensus_tcp/agent.py:204-207, with a fast-averaging weight that is the same on
+    every edge, as the FDLA optimum is on the ring).
     """
     tokens = asyncio_tokens(topology)
-    eps = perron_eps(topology, tokens)
+    eps = perron_eps(topology, tokens) if edge_weight is None else edge_weight
     nbrs = {t: asyncio_neighbors(topology, t) for t in tokens}
     mean_w = sum(weights[t] for t in tokens) / len(tokens)
     y = {t: values[t] * weights[t] / mean_w for t in tokens}
@@ -162,7 +165,7 @@ def logreg_gradient(X, y, w, tau=1e-4):
 
 
 def consensus_gd(topology, X, y, iterations, alpha=1e-1, tau=1e-4, conv_eps=1e-10,
-                 schedule="sqrt"):
+                 schedule="sqrt", edge_weight=None):
     """The Titanic notebook's consensus GD run (cells 12-14) restated synchronously: shards split
     in ``ConsensusNetwork.tokens`` order, a local step per agent, then ``jacobi_round`` weighted
     by shard size.  Pinned bit for bit to the reference's 4000-step asyncio run by
@@ -179,6 +182,7 @@ def consensus_gd(topology, X, y, iterations, alpha=1e-1, tau=1e-4, conv_eps=1e-1
         step = alpha * np.power(it + 1, -0.5) if schedule == "sqrt" else alpha
         for t in toks:
             w[t] = w[t] - step * logreg_gradient(*sh[t], w[t], tau)
-        w, k = jacobi_round(topology, w, {t: sh[t][0].shape[0] for t in toks}, conv_eps)
+        w, k = jacobi_round(topology, w, {t: sh[t][0].shape[0] for t in toks}, conv_eps,
+                            edge_weight=edge_weight)
         ks.append(k)
     return w, ks

@@ -32,6 +32,26 @@ def test_matches_synchronous_restatement(golden, cuda, topo_name, eps, iters):
         np.testing.assert_allclose(got[t], want[t], rtol=1e-9, atol=1e-12)
 
 
+@pytest.mark.parametrize("eps,iters", [(10, 300), (1e-3, 60)])
+def test_ring8_fast_averaging_weights(golden, cuda, eps, iters):
+    """BASELINE c1's wording, "ring with fast-averaging weights": the ring's FDLA weights are one
+    weight on every edge, w* = 1 / (3 - cos(2 pi / 8)) (find_optimal_weights, pinned by
+    tests/test_fast_averaging.py), mixed as x' = x(1 - 2 w*) + w* sum_j x_j.  The one-launch run
+    equals the restatement with that weight (same Jacobi counts, 1e-9 relative)."""
+    from distributed_learning_amd import workloads
+    from distributed_learning_amd.utils.fast_averaging import find_optimal_weights
+    _, X, y = titanic(golden)
+    topo = [(i, (i + 1) % 8) for i in range(8)]
+    w, _ = find_optimal_weights(topo)
+    assert np.allclose(w, w[0]) and abs(w[0] - 1 / (3 - np.cos(2 * np.pi / 8))) < 1e-8
+    want, ks = M.consensus_gd(topo, X, y, iters, conv_eps=eps, edge_weight=float(w[0]))
+    got, kd = workloads.consensus_gd_device(topo, X, y, iters, convergence_eps=eps, device=cuda,
+                                            edge_weight=float(w[0]))
+    assert list(kd) == ks
+    for t in want:
+        np.testing.assert_allclose(got[t], want[t], rtol=1e-9, atol=1e-12)
+
+
 def test_reference_4000_step_run(golden, cuda):
     """The reference's ring-8, eps = 10, 4000-step asyncio run (golden final weights)."""
     from distributed_learning_amd import workloads

@@ -57,7 +57,8 @@ def parse():
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--workload", default="c2",
-                   choices=["c1", "c2", "c2-mix", "c2-gossip", "c3", "c4", "c4-gather", "c5"])
+                   choices=["c1", "c2", "c2-mix", "c2-gossip", "c2-halo", "c3", "c4", "c4-gather",
+                            "c5"])
     p.add_argument("--graph", default="rr4", choices=["rr4", "circ4", "torus"],
                    help="c2-gossip: agent graph (circ4 = conflict-free control)")
     p.add_argument("--relabel", type=int, default=2_000_000,
@@ -552,84 +553,121 @@ def run_gather(args, dev, rank, world):
         }), flush=True)
 
 
+def _halo_schemes(args, dev, rank, world, csr, parts, P, lr, gen):
+    """The agent-partitioned round on this rank (HaloShard over RCCL, strong scaling), the
+    deviation lagged one round inside the round's own kernel (no extra HBM pass; one all-reduce
+    of n_params column sums + one of the max).  Times each overlap scheme of --halo-overlap
+    ("both" by default): "chunks" -- the boundary rows of each column chunk exchanged with RCCL
+    send/recv while the previous chunk is mixed; "split" -- one exchange per round in flight
+    while the interior rows mix, the boundary rows after it lands.  Returns the faster scheme's
+    (elapsed, launch_ms, plan) and every scheme's figures."""
+    from distributed_learning_amd import engine, sharding
+    stream = torch.cuda.current_stream(dev)
+    n = csr.n_rows
+    G = None
+    schemes = {}
+    names = ["chunks", "split"] if args.halo_overlap == "both" else [args.halo_overlap]
+    for name in names:
+        rp = (sharding.split_halo_plans if name == "split" else sharding.halo_plans)(
+            csr, parts)[rank]
+        shard = sharding.HaloShard(rp, P, dev, sharding.dist_transport(),
+                                   chunk_cols=P // 8 if name == "chunks" else None,
+                                   n_agents_total=n, overlap=name)
+        shard.X.normal_(generator=gen)
+        if G is None:   # synthetic gradient rows, shared by both schemes (same row count)
+            G = engine.staggered_zeros((rp.n_local, P), 2, dev).normal_(generator=gen)
+        evs = event_pairs(args.steps, 2)
+
+        def step(i, shard=shard, evs=evs):
+            if i is not None:
+                evs[i][0].record(stream)
+            shard.round(G=G, lr=lr, deviation=True)   # lagged deviation, in the round
+            if i is not None:
+                evs[i][1].record(stream)
+        el = timed_loop(step, args, world, dev)
+        lm = max_over_ranks(float(np.mean([a.elapsed_time(b) for a, b in evs])), world, dev)
+        extra = 8 * (rp.n_local - rp.n_deep) * P if name == "split" else 0
+        schemes[name] = {"rounds_per_s": args.steps / el, "elapsed_s": el, "launch_ms": lm,
+                         "n_local": rp.n_local, "n_halo": rp.n_halo,
+                         "n_interior": rp.n_interior if name == "split" else None,
+                         "n_deep": rp.n_deep if name == "split" else None,
+                         "reread_bytes_per_round": extra,
+                         "halo_rows_per_peer": {int(q): len(ids) for q, ids in
+                                                sorted(rp.halo_from.items())}}
+        del shard
+        torch.cuda.empty_cache()
+    best = max(schemes, key=lambda k: schemes[k]["rounds_per_s"])
+    plan = {"path": "halo", "overlap": best, "n_local": schemes[best]["n_local"],
+            "n_halo": schemes[best]["n_halo"],
+            "peers": sorted(schemes[best]["halo_rows_per_peer"])}
+    return schemes[best]["elapsed_s"], schemes[best]["launch_ms"], plan, schemes
+
+
+def _halo_xgmi(schemes, best, P, launch_ms):
+    """xGMI figures of rank 0: halo bytes received per round and the busiest link's rate (one
+    xGMI link per peer on the fully connected 8-GPU node) over the round time."""
+    per_peer = schemes[best]["halo_rows_per_peer"]
+    hb = sum(per_peer.values()) * P * 4
+    link = max(per_peer.values()) * P * 4 if per_peer else 0
+    out = {"halo_bytes_per_round": hb, "peers": len(per_peer),
+           "busiest_link_bytes_per_round": link,
+           "achieved_GBs": hb / (launch_ms / 1e3) / 1e9,
+           "busiest_link_GBs": link / (launch_ms / 1e3) / 1e9,
+           "peak_GBs_per_link": XGMI_LINK_GBS,
+           "frac": link / (launch_ms / 1e3) / 1e9 / XGMI_LINK_GBS,
+           "note": "received halo bytes over the rank's round time (HIP events); frac = the "
+                   "busiest link's rate / one link's peak"}
+    for v in schemes.values():
+        lm = v["launch_ms"]
+        v["hbm_frac"] = 12 * v["n_local"] * P / (lm / 1e3) / 1e9 / HBM_PEAK_GBS
+        v["xgmi_frac"] = max(v["halo_rows_per_peer"].values()) * P * 4 / (lm / 1e3) / 1e9 / \
+            XGMI_LINK_GBS if v["halo_rows_per_peer"] else 0.0
+    return out
+
+
+def _single_gpu_round(args, dev, csr, P, lr, gen):
+    from distributed_learning_amd import engine
+    stream = torch.cuda.current_stream(dev)
+    n = csr.n_rows
+    evs = event_pairs(args.steps, 2)
+    X = torch.randn(n, P, device=dev, generator=gen)
+    eng = engine.GossipEngine(csr, P, device=dev, X=X)
+    G = eng.layout_like(torch.randn(n, P, device=dev, generator=gen))
+    del X
+    plan = eng.plan(deviation=True)
+
+    def step(i):
+        if i is not None:
+            evs[i][0].record(stream)
+        eng.round(G=G, lr=lr, deviation=True)
+        if i is not None:
+            evs[i][1].record(stream)
+    elapsed = timed_loop(step, args, 1, dev)
+    return elapsed, float(np.mean([a.elapsed_time(b) for a, b in evs])), plan
+
+
 def run_c4(args, dev, rank, world):
     """Config c4: 64x64 periodic torus, 4096 agents x 2^18 params, uniform best-constant weight
     2/(lambda_2 + 8).  N=1: the whole torus resident in the tiled layout, one fused round
-    (local step + mix + deviation) per step.  N>1: 2-D torus blocks per rank (HaloShard, strong
-    scaling: total work fixed), the deviation lagged one round inside the round's own kernel
-    (no extra HBM pass; one all-reduce of n_params column sums + one of the max).  Two overlap
-    schemes, both timed (--halo-overlap both, the default): "chunks" -- the boundary rows of each
-    column chunk exchanged with RCCL send/recv while the previous chunk is mixed; "split" -- one
-    exchange per round in flight while the interior rows mix, the boundary rows after it lands.
-    ``value`` is the faster scheme's rate; both are in the line."""
+    (local step + mix + deviation) per step.  N>1: 2-D torus blocks per rank (_halo_schemes:
+    both overlap schemes timed, ``value`` the faster one's rate, both in the line)."""
     import math
-    from distributed_learning_amd import engine, graph, sharding
+    from distributed_learning_amd import graph, sharding
     rows = cols = 64
     n, P, lr = rows * cols, 1 << 18, 1e-3
     edges = graph.torus_edges(rows, cols)
     wconst = 2.0 / (2.0 - 2.0 * math.cos(2 * math.pi / cols) + 8.0)
     csr = graph.from_edge_weights(edges, [wconst] * len(edges), list(range(n)))
     gen = torch.Generator(device=dev).manual_seed(1000 + rank)
-    stream = torch.cuda.current_stream(dev)
-    halo_rows = 0
     schemes = {}
     if world == 1:
-        evs = event_pairs(args.steps, 2)
-        X = torch.randn(n, P, device=dev, generator=gen)
-        eng = engine.GossipEngine(csr, P, device=dev, X=X)
-        G = eng.layout_like(torch.randn(n, P, device=dev, generator=gen))
-        del X
-        plan = eng.plan(deviation=True)
-
-        def step(i):
-            if i is not None:
-                evs[i][0].record(stream)
-            eng.round(G=G, lr=lr, deviation=True)
-            if i is not None:
-                evs[i][1].record(stream)
-        bytes_per_round = 12 * n * P
-        elapsed = timed_loop(step, args, world, dev)
-        launch_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+        elapsed, launch_ms, plan = _single_gpu_round(args, dev, csr, P, lr, gen)
+        bytes_per_round, halo_rows = 12 * n * P, 0
     else:
         parts = sharding.torus_block_partition(rows, cols, world)
-        G = None
-        names = ["chunks", "split"] if args.halo_overlap == "both" else [args.halo_overlap]
-        for name in names:
-            rp = (sharding.split_halo_plans if name == "split" else sharding.halo_plans)(
-                csr, parts)[rank]
-            shard = sharding.HaloShard(rp, P, dev, sharding.dist_transport(),
-                                       chunk_cols=P // 8 if name == "chunks" else None,
-                                       n_agents_total=n, overlap=name)
-            shard.X.normal_(generator=gen)
-            if G is None:   # synthetic gradient rows, shared by both schemes (same row count)
-                G = engine.staggered_zeros((rp.n_local, P), 2, dev).normal_(generator=gen)
-            halo_rows = rp.n_halo
-            evs = event_pairs(args.steps, 2)
-
-            def step(i, shard=shard, evs=evs):
-                if i is not None:
-                    evs[i][0].record(stream)
-                shard.round(G=G, lr=lr, deviation=True)   # lagged deviation, in the round
-                if i is not None:
-                    evs[i][1].record(stream)
-            el = timed_loop(step, args, world, dev)
-            lm = max_over_ranks(float(np.mean([a.elapsed_time(b) for a, b in evs])), world, dev)
-            extra = 0
-            if name == "split":   # boundary launch re-reads its local window (X and G)
-                extra = 8 * (rp.n_local - rp.n_deep) * P
-            schemes[name] = {"rounds_per_s": args.steps / el, "elapsed_s": el, "launch_ms": lm,
-                             "n_local": rp.n_local, "n_halo": rp.n_halo,
-                             "n_interior": rp.n_interior if name == "split" else None,
-                             "n_deep": rp.n_deep if name == "split" else None,
-                             "reread_bytes_per_round": extra,
-                             "peers": sorted(rp.halo_from)}
-            del shard
-            torch.cuda.empty_cache()
-        best = max(schemes, key=lambda k: schemes[k]["rounds_per_s"])
-        elapsed, launch_ms = schemes[best]["elapsed_s"], schemes[best]["launch_ms"]
-        plan = {"path": "halo", "overlap": best, "n_local": schemes[best]["n_local"],
-                "n_halo": halo_rows, "peers": schemes[best]["peers"]}
-        bytes_per_round = 12 * schemes[best]["n_local"] * P
+        elapsed, launch_ms, plan, schemes = _halo_schemes(args, dev, rank, world, csr, parts, P,
+                                                          lr, gen)
+        bytes_per_round, halo_rows = 12 * plan["n_local"] * P, plan["n_halo"]
     if rank != 0:
         return
     achieved = bytes_per_round / (launch_ms / 1e3) / 1e9
@@ -637,21 +675,7 @@ def run_c4(args, dev, rank, world):
     c4_traffic, c4_src = (traffic_from_profile(
         "mix_tile_kernel<", os.path.join(ROOT, "profiles", "r05", "c4", "summary.json"))
         if world == 1 else (None, None))
-    xgmi = None
-    if world > 1:
-        # halo bytes rank 0 receives per round (it sends as many); every peer is one xGMI link
-        # of the fully connected 8-GPU node
-        n_peers = len(plan["peers"])
-        hb = halo_rows * P * 4
-        xgmi = {"halo_bytes_per_round": hb, "peers": n_peers,
-                "achieved_GBs": hb / (launch_ms / 1e3) / 1e9,
-                "peak_GBs": XGMI_LINK_GBS * n_peers,
-                "frac": hb / (launch_ms / 1e3) / 1e9 / (XGMI_LINK_GBS * n_peers),
-                "note": "received halo bytes over the rank's round time (HIP events); one "
-                        "link per peer"}
-        for v in schemes.values():
-            v["hbm_frac"] = bytes_per_round / (v["launch_ms"] / 1e3) / 1e9 / HBM_PEAK_GBS
-            v["xgmi_frac"] = hb / (v["launch_ms"] / 1e3) / 1e9 / (XGMI_LINK_GBS * n_peers)
+    xgmi = _halo_xgmi(schemes, plan["overlap"], P, launch_ms) if world > 1 else None
     rec = {
         "metric": "c4 torus consensus rounds/sec (4096 agents x 2^18 fp32 params)",
         "value": args.steps / elapsed,
@@ -680,6 +704,93 @@ def run_c4(args, dev, rank, world):
                      "kernel": "per-round HIP-event time (rank 0 local work)",
                      "bytes_per_launch": bytes_per_round, "launch_ms": launch_ms},
         "xgmi": xgmi,
+        "overlap_schemes": schemes or None,
+        "cpu_baseline": None,
+    }
+    print(json.dumps(rec), flush=True)
+
+
+def partition_report(csr, P, worlds=(2, 4, 8)):
+    """Host-side partition of a graph for each GPU count: sharding.graph_partition (BFS growth +
+    Kernighan-Lin refinement) against contiguous blocks -- cut edges, halo rows and halo bytes
+    per round of every rank, peers, busiest-link bytes."""
+    from distributed_learning_amd import sharding
+    rows = np.repeat(np.arange(csr.n_rows), np.diff(csr.rowptr))
+    out = {}
+    for world in worlds:
+        rec = {}
+        for name, parts in (("graph_partition", sharding.graph_partition(csr, world)),
+                            ("contiguous", sharding.contiguous_partition(csr.n_rows, world))):
+            owner = np.empty(csr.n_rows, np.int64)
+            for r, p in enumerate(parts):
+                owner[p] = r
+            keep = csr.col != rows
+            cut = int(np.sum(owner[rows[keep]] != owner[csr.col[keep]]) // 2)
+            plans = sharding.halo_plans(csr, parts)
+            halo = [pl.n_halo for pl in plans]
+            link = [max((len(ids) for ids in pl.halo_from.values()), default=0) for pl in plans]
+            rec[name] = {"cut_edges": cut, "halo_rows_per_rank": halo,
+                         "halo_bytes_per_round_max": max(halo) * P * 4,
+                         "busiest_link_bytes_per_round": max(link) * P * 4,
+                         "peers_max": max(len(pl.halo_from) for pl in plans)}
+        out[str(world)] = rec
+    return out
+
+
+def run_c2halo(args, dev, rank, world):
+    """The c2 graph agent-partitioned (a general partitioner for random graphs, halo
+    bytes per GPU): networkx random_regular_graph(4, 1024, seed=0), best-constant weights, 2^20
+    params per agent, the fused local step + mix + lagged deviation per round.  N=1: the single
+    -device round and the host-side partition report for 2/4/8 GPUs.  N>1: graph_partition (BFS
+    + Kernighan-Lin) over the ranks, both halo overlap schemes timed (_halo_schemes); strong
+    scaling.  Random 4-regular graphs cut badly (most boundary agents read several remote rows),
+    so this path is expected to be xGMI-bound -- the column stripes of the headline are the
+    c2 decomposition; this line measures the general agent partition on the same graph."""
+    from distributed_learning_amd import sharding
+    n, P, lr = args.agents, args.params, 1e-3
+    csr, wconst = build_graph(n)
+    gen = torch.Generator(device=dev).manual_seed(1000 + rank)
+    schemes = {}
+    report = partition_report(csr, P) if rank == 0 else None
+    if world == 1:
+        elapsed, launch_ms, plan = _single_gpu_round(args, dev, csr, P, lr, gen)
+        bytes_per_round, halo_rows = 12 * n * P, 0
+    else:
+        parts = sharding.graph_partition(csr, world)
+        elapsed, launch_ms, plan, schemes = _halo_schemes(args, dev, rank, world, csr, parts, P,
+                                                          lr, gen)
+        bytes_per_round, halo_rows = 12 * plan["n_local"] * P, plan["n_halo"]
+    if rank != 0:
+        return
+    achieved = bytes_per_round / (launch_ms / 1e3) / 1e9
+    rec = {
+        "metric": "c2 graph agent-partitioned consensus rounds/sec (1024 agents x 2^20 fp32 "
+                  "params, random 4-regular, halo exchange)",
+        "value": args.steps / elapsed,
+        "unit": "rounds/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (X, G ~ N(0,1) resident in HBM)",
+        "config": {"workload": "c2-halo: c2 graph agent-partitioned, fused local step + mix + "
+                               "deviation",
+                   "agents": n, "params": P, "weights": f"best-constant {wconst:.6f}",
+                   "partitioner": "sharding.graph_partition (BFS growth + Kernighan-Lin swaps)",
+                   "parallelism": f"agent partition x{world}, "
+                                  f"{'RCCL' if args.dist_backend == 'nccl' else args.dist_backend}"
+                                  f" halo exchange" if world > 1 else "single GPU", "plan": plan,
+                   "halo_rows_rank0": halo_rows},
+        "partition_report": report,
+        "roofline": {"bound": "hbm" if world == 1 else "xgmi", "achieved": achieved,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": None, "kernel": "per-round HIP-event time (rank 0 local work)",
+                     "bytes_per_launch": bytes_per_round, "launch_ms": launch_ms},
+        "xgmi": _halo_xgmi(schemes, plan["overlap"], P, launch_ms) if world > 1 else None,
         "overlap_schemes": schemes or None,
         "cpu_baseline": None,
     }
@@ -1064,7 +1175,7 @@ def run_gossip(args, dev, rank, world):
     print(json.dumps(rec), flush=True)
 
 
-def halo_probe(world, backend, steps=20, warmup=3, timeout_s=240):
+def halo_probe(world, backend, steps=20, warmup=3, timeout_s=240, workload="c4"):
     """The agent-partitioned path at this GPU count: bench --workload c4 (64 x 64 torus, 2-D
     blocks, boundary rows exchanged with RCCL send/recv over xGMI each round, overlapped with
     the mix of the previous column chunk) as a CHILD job on the same GPUs, after this job's own
@@ -1083,7 +1194,7 @@ def halo_probe(world, backend, steps=20, warmup=3, timeout_s=240):
                "MASTER_PORT")}
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
            f"--nproc-per-node={world}", "--master-addr", "127.0.0.1", f"--master-port={port}",
-           os.path.join(ROOT, "bench.py"), "--workload", "c4", "--gpus", str(world),
+           os.path.join(ROOT, "bench.py"), "--workload", workload, "--gpus", str(world),
            "--steps", str(steps), "--warmup", str(warmup), "--dist-backend", backend]
     t0 = time.perf_counter()
     p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, env=env,
@@ -1103,7 +1214,7 @@ def halo_probe(world, backend, steps=20, warmup=3, timeout_s=240):
             "parallelism": r["config"]["parallelism"], "plan": r["config"]["plan"],
             "hbm": {k: r["roofline"][k] for k in ("achieved", "peak", "frac", "launch_ms")},
             "xgmi": r["xgmi"], "overlap_schemes": r.get("overlap_schemes"),
-            "wall_s": time.perf_counter() - t0}
+            "partition_report": r.get("partition_report"), "wall_s": time.perf_counter() - t0}
 
 
 def main():
@@ -1124,9 +1235,10 @@ def main():
         else:
             dist.init_process_group(args.dist_backend)
 
-    if args.workload in ("c1", "c2-gossip", "c3", "c4", "c4-gather", "c5"):
-        {"c1": run_c1, "c2-gossip": run_gossip, "c3": run_c3, "c4": run_c4,
-         "c4-gather": run_gather, "c5": run_c5}[args.workload](args, dev, rank, world)
+    if args.workload in ("c1", "c2-gossip", "c2-halo", "c3", "c4", "c4-gather", "c5"):
+        {"c1": run_c1, "c2-gossip": run_gossip, "c2-halo": run_c2halo, "c3": run_c3,
+         "c4": run_c4, "c4-gather": run_gather, "c5": run_c5}[args.workload](args, dev, rank,
+                                                                              world)
         if world > 1:
             dist.destroy_process_group()
         return
@@ -1254,6 +1366,9 @@ def main():
         if world > 1 and not args.no_halo_probe and sgd:
             del eng, G
             torch.cuda.empty_cache()
+            # the general partitioner on the c2 graph itself (halo bytes per GPU)
+            rec["c2_halo"] = halo_probe(world, args.dist_backend, timeout_s=180,
+                                        workload="c2-halo")
             rec["c4_halo"] = h = halo_probe(world, args.dist_backend)
             # the agent-partitioned path's figures as first-class fields of the line
             ok = h.get("status") == "ok"

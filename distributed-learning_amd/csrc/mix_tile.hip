@@ -505,8 +505,20 @@ __global__ void __launch_bounds__(1024) dev_reduce_kernel(const float *__restric
     const int ai = threadIdx.x & 63, j = threadIdx.x >> 6;
     const int ag = blockIdx.x * 64 + ai;
     double s = 0.0;
-    if (ag < n_rows)
-        for (int b = j; b < nparts; b += 16) s += (double)partial[(int64_t)b * n_rows + ag];
+    if (ag < n_rows) {
+        // eight partials in flight per lane, added in the same order as one at a time (the sum
+        // is bit-identical): a dependent load per add left this launch latency-bound (11.8 us for
+        // c2's 512 x 1024 partials, profiles/r08)
+        int b = j;
+        for (; b + 16 * 7 < nparts; b += 16 * 8) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = partial[(int64_t)(b + 16 * u) * n_rows + ag];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s += (double)v[u];
+        }
+        for (; b < nparts; b += 16) s += (double)partial[(int64_t)b * n_rows + ag];
+    }
     red[j][ai] = s;
     __syncthreads();
     float f = 0.f;

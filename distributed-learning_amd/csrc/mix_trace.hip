@@ -364,8 +364,17 @@ __global__ void __launch_bounds__(1024) trace_reduce_kernel(const float *__restr
     const int r = blockIdx.x, tid = threadIdx.x;
     float best = 0.f;
     for (int ag = tid; ag < n; ag += 1024) {
+        // eight partials in flight, added in the same order (bit-identical to one at a time)
         double s = 0.0;
-        for (int b = 0; b < nparts; ++b) s += (double)partial[((int64_t)b * rounds + r) * n + ag];
+        int b = 0;
+        for (; b + 7 < nparts; b += 8) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = partial[((int64_t)(b + u) * rounds + r) * n + ag];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s += (double)v[u];
+        }
+        for (; b < nparts; ++b) s += (double)partial[((int64_t)b * rounds + r) * n + ag];
         best = fmaxf(best, sqrtf((float)s));
     }
 #pragma unroll

@@ -29,7 +29,28 @@ def test_torus_block_partition(world):
     assert len({len(p) for p in parts}) == 1
 
 
-@pytest.mark.parametrize("kind", ["torus", "rr4", "bfs"])
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_graph_partition_refines_the_cut(world):
+    """graph_partition (BFS growth + Kernighan-Lin swaps) on the c2 graph: every agent exactly
+    once, part sizes as balanced as BFS's, an edge cut and a largest halo below BFS's."""
+    edges = random_regular_edges(4, 1024, seed=0)
+    csr = from_edge_weights(edges, [0.2] * len(edges), list(range(1024)))
+    bfs = sharding.greedy_bfs_partition(csr, world)
+    ref = sharding.graph_partition(csr, world)
+    assert np.array_equal(np.sort(np.concatenate(ref)), np.arange(1024))
+    assert sorted(len(p) for p in ref) == sorted(len(p) for p in bfs)
+
+    def cut(parts):
+        owner = np.empty(1024, np.int64)
+        for r, p in enumerate(parts):
+            owner[p] = r
+        return sum(int(owner[u] != owner[v]) for u, v in edges)
+    assert cut(ref) < cut(bfs)
+    assert max(p.n_halo for p in sharding.halo_plans(csr, ref)) < \
+        max(p.n_halo for p in sharding.halo_plans(csr, bfs))
+
+
+@pytest.mark.parametrize("kind", ["torus", "rr4", "bfs", "refined"])
 def test_halo_plans_reconstruct_the_graph(kind):
     if kind == "torus":
         csr = torus_csr(8, 8)
@@ -38,7 +59,8 @@ def test_halo_plans_reconstruct_the_graph(kind):
         edges = random_regular_edges(4, 60, seed=1)
         csr = from_edge_weights(edges, [0.2] * len(edges), list(range(60)))
         parts = (sharding.contiguous_partition(60, 3) if kind == "rr4"
-                 else sharding.greedy_bfs_partition(csr, 3))
+                 else sharding.greedy_bfs_partition(csr, 3) if kind == "bfs"
+                 else sharding.graph_partition(csr, 3))
     assert np.array_equal(np.sort(np.concatenate(parts)), np.arange(csr.n_rows))
     plans = sharding.halo_plans(csr, parts)
     for pl in plans:

@@ -527,6 +527,78 @@ __device__ __forceinline__ void backward_dz(const M &W, int dk, int dh, const fl
     });
 }
 
+// W3 held in registers from the layer-3 forward to the dZ2 backward (W_HOLD): the five forward
+// slices RowSlice<160> [n][32s..32s+31] cover W3 once, 50 floats per thread, so the backward's
+// row slices [32j..32j+31][*] are restaged from registers instead of re-read from HBM (the W3
+// re-read was 23 MB of the kernel's 315).  Thread element i of forward slice s is W3[n][32s + c]
+// with n = (tid + 512 i) / 32, c = tid % 32; backward slice j holds rows 32j..32j+31, i.e. the
+// thread's elements i = 2j and 2j + 1 of every forward slice.
+// Measured time-neutral (fwd3 -0.5, dZ2 -1.8 us, fwd2 +3.2 us issuing the 50 hold loads;
+// 240 VGPRs): off by default, kept as the measured alternative (-DW_HOLD=1).
+#ifndef W_HOLD
+#define W_HOLD 0
+#endif
+struct WHold {
+    RowSlice<160> s[5];
+};
+
+template <typename M>
+__device__ __forceinline__ void hold_load(WHold &h, const M &W, int dh) {
+#pragma unroll
+    for (int i = 0; i < 5; ++i) h.s[i].load(W, dh, dh, i * BK);
+}
+
+// forward layer from a held W (all five slices already in registers)
+template <typename M>
+__device__ __forceinline__ void forward_hidden_held(const M &bias, int dh, const float *Hin,
+                                                    float *Hout, float *stage, int layer,
+                                                    const WHold &h) {
+    f32x4 acc[5];
+    zero(acc);
+    float bv[5];
+    load_bias5(bias, dh, bv);
+#pragma unroll
+    for (int sl = 0; sl < 5; ++sl) {
+        if (sl * BK < dh) {
+            h.s[sl].store(stage);
+            __syncthreads();
+            mma_rows64<false>(acc, Hin + sl * BK, LDH, stage);
+            __syncthreads();
+        }
+    }
+    epi_rows64_t(acc, [&](int m, int n, int t, float v) {
+        if (n < dh) Hout[m * LDH + n] = act_fwd(layer, v + bv[t]);
+    });
+}
+
+// backward through a hidden layer from the held W: row slice j restaged [k][n] (ColSlice layout)
+__device__ __forceinline__ void backward_dz_held(int dh, const float *dZ, int ldz, float *Hio,
+                                                 float *stage, int layer, const WHold &h) {
+    f32x4 acc[5];
+    zero(acc);
+    const int tid = threadIdx.x, c = tid % BK;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+        if (j * BK < dh) {
+#pragma unroll
+            for (int s = 0; s < 5; ++s)
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    const int i = 2 * j + q;
+                    const int n = (tid + i * NTHR) / BK;     // W row (the backward's K)
+                    const int k = s * BK + c;                // W column (the backward's N)
+                    stage[(n - j * BK) * LDT + k] = (n < dh && k < dh) ? h.s[s].v[i] : 0.f;
+                }
+            __syncthreads();
+            mma_rows64<true>(acc, dZ + j * BK, ldz, stage);
+            __syncthreads();
+        }
+    }
+    epi_rows64(acc, [&](int m, int n, float v) {
+        if (n < dh) Hio[m * LDH + n] = v * act_grad(layer, Hio[m * LDH + n]);
+    });
+}
+
 // Weight gradient of a hidden layer: dW[i][j] = sum_b dZ[b][i] Hin[b][j] (both LDS-resident,
 // [64][LDH]), i, j < dh, straight into G; bias gradient db[i] = sum_b dZ[b][i] from Hin's ones
 // column j = dh (N-tile 4).
@@ -788,8 +860,14 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
     }
     __syncthreads();
     STAMP(1);
+#if W_HOLD
+    WHold w3h;   // W3 from HBM once, for the layer-3 forward and the dZ2 backward
+    forward_hidden(mat(Xr, o_w2, dh), mat(Xr, o_b2, 0), dh, H1, H2, stage, 1, wa, wb,
+                   [&] { hold_load(w3h, mat(Xr, o_w3, dh), dh); });
+#else
     forward_hidden(mat(Xr, o_w2, dh), mat(Xr, o_b2, 0), dh, H1, H2, stage, 1, wa, wb,
                    [&] { prefetch_w(wa, wb, mat(Xr, o_w3, dh), dh); });
+#endif
     __syncthreads();
     STAMP(2);
     // the logits' operands from HBM (W4 image values, b4, this wave's labels), issued now so they
@@ -806,8 +884,13 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
     int lab[MB / 8];
 #pragma unroll
     for (int i = 0; i < MB / 8; ++i) lab[i] = p.labels[(int64_t)a * p.s_lab + wave + 8 * i];
+#if W_HOLD
+    prefetch_wt(ta, tb, mat(Xr, o_w4, dh), dout, dh);
+    forward_hidden_held(mat(Xr, o_b3, 0), dh, H2, H3, stage, 2, w3h);
+#else
     forward_hidden(mat(Xr, o_w3, dh), mat(Xr, o_b3, 0), dh, H2, H3, stage, 2, wa, wb,
                    [&] { prefetch_wt(ta, tb, mat(Xr, o_w4, dh), dout, dh); });
+#endif
     STAMP(3);
     // ---- logits Z = H3 W4^T + b4 (waves 0-3, one 16 x 16 tile each), W4 image [16][LDW4]
 #pragma unroll
@@ -875,15 +958,24 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
     }
     __syncthreads();
     // ---- dZ3 = (dZ4 W4) * elu'(H3) in place, K = dout
+#if W_HOLD
+    backward_dz(mat(Xr, o_w4, dh), dout, dh, Zs, LDZ, H3, stage, 2, ta, tb,
+                [&] { prefetch_wt(ta, tb, mat(Xr, o_w2, dh), dh, dh); });   // for dZ1
+#else
     backward_dz(mat(Xr, o_w4, dh), dout, dh, Zs, LDZ, H3, stage, 2, ta, tb,
                 [&] { prefetch_wt(ta, tb, mat(Xr, o_w3, dh), dh, dh); });
+#endif
     __syncthreads();
     STAMP(5);
     weight_grad_hidden(H3, H2, dh, mat(Gr, o_w3, dh), mat(Gr, o_b3, 0));
     __syncthreads();
     STAMP(6);
+#if W_HOLD
+    backward_dz_held(dh, H3, LDH, H2, stage, 1, w3h);                         // dZ2 into H2
+#else
     backward_dz(mat(Xr, o_w3, dh), dh, dh, H3, LDH, H2, stage, 1, ta, tb,     // dZ2 into H2
                 [&] { prefetch_wt(ta, tb, mat(Xr, o_w2, dh), dh, dh); });
+#endif
     __syncthreads();
     STAMP(7);
     weight_grad_hidden(H2, H1, dh, mat(Gr, o_w2, dh), mat(Gr, o_b2, 0));

@@ -538,6 +538,7 @@ __device__ __forceinline__ void backward_dz(const M &W, int dk, int dh, const fl
 #ifndef W_HOLD
 #define W_HOLD 0
 #endif
+#if W_HOLD
 struct WHold {
     RowSlice<160> s[5];
 };
@@ -598,6 +599,7 @@ __device__ __forceinline__ void backward_dz_held(int dh, const float *dZ, int ld
         if (n < dh) Hio[m * LDH + n] = v * act_grad(layer, Hio[m * LDH + n]);
     });
 }
+#endif
 
 // Weight gradient of a hidden layer: dW[i][j] = sum_b dZ[b][i] Hin[b][j] (both LDS-resident,
 // [64][LDH]), i, j < dh, straight into G; bias gradient db[i] = sum_b dZ[b][i] from Hin's ones

@@ -11,7 +11,8 @@ import os
 import torch  # loads torch's HIP runtime first, so libdlamd.so binds to the same one
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libdlamd.so")
+# DLAMD_LIB: another build of the same ABI (A/B measurements of kernel variants on one box)
+LIB_PATH = os.environ.get("DLAMD_LIB") or os.path.join(_HERE, "_lib", "libdlamd.so")
 
 DL_OK, DL_ERR_INVALID, DL_ERR_WORKSPACE, DL_ERR_HIP, DL_ERR_UNSUPPORTED = 0, 1, 2, 3, 4
 

@@ -1148,8 +1148,8 @@ int dl_mlp_grad(const dl_mlp_args *a, dl_stream_t stream) {
     if (a->n_agents == 0) return DL_OK;
     if (!dl::mlp_fused_supported(a->batch, a->input_dim, a->hidden_dim, a->output_dim))
         return fail(DL_ERR_UNSUPPORTED, "dl_mlp_grad: fused path needs batch 64, input_dim %% 4 "
-                                        "== 0, hidden_dim <= 152, output_dim <= 16 (got %d, %d, "
-                                        "%d, %d)", a->batch, a->input_dim, a->hidden_dim,
+                                        "== 0, even hidden_dim <= 152, output_dim <= 16 (got %d, "
+                                        "%d, %d, %d)", a->batch, a->input_dim, a->hidden_dim,
                     a->output_dim);
     const int64_t din = a->input_dim, dh = a->hidden_dim, dout = a->output_dim;
     const int64_t P = dh * din + dh + 2 * (dh * dh + dh) + dout * dh + dout;

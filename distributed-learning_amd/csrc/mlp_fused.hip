@@ -9,8 +9,8 @@
 //     backward overwrites each in place with its dZ once its weight gradient is done;
 //   * only the agent's parameter row of X, its input batch (read twice) and its gradient row of
 //     G touch HBM: ~1.7 MB per agent, every byte once;
-//   * weights stream through one LDS staging area, two slices ahead in registers while the
-//     MFMAs consume the current one (pipeline2);
+//   * weights stream through one LDS staging area; a hidden phase's whole weight matrix is in
+//     registers (requested during the phase before, load_all_w) while the MFMAs consume it;
 //   * weight gradients go from the MFMA accumulators straight into the agent's row of G (the
 //     Mixer flatten order, mixer.py:69), and the per-agent loss is summed in a fixed order
 //     (deterministic, hipGraph-replay stable);
@@ -26,6 +26,8 @@
 // f32 MFMA (16x16x4) products are exact fp32 fma chains; summation order differs from
 // autograd's BLAS, so parity is a tolerance (tests/test_batched_ann_gpu.py).
 #include "dl_internal.h"
+
+#include <type_traits>
 
 namespace dl {
 namespace {
@@ -132,56 +134,9 @@ __device__ __forceinline__ void mfma_x6(const bf16x8 &ah, const bf16x8 &am, cons
 }
 
 
-// Two slices in flight: while the MFMAs consume slice s from LDS, the global loads of slices
-// s + 1 and s + 2 are outstanding in two register sets (HBM latency under full load is longer
-// than one slice of MFMAs).  load(set, s) issues slice s, store(set) writes it to LDS,
-// compute(s) runs on the LDS image.  Plain loads stay in flight across the barriers.
-template <typename Set, typename Load, typename Store, typename Compute>
-__device__ __forceinline__ void pipeline2(int ns, Load load, Store store, Compute compute) {
-    Set A, B;
-    load(A, 0);
-    if (ns > 1) load(B, 1);
-    for (int s = 0; s < ns; s += 2) {
-        store(A);
-        __syncthreads();
-        if (s + 2 < ns) load(A, s + 2);
-        compute(s);
-        __syncthreads();
-        if (s + 1 < ns) {
-            store(B);
-            __syncthreads();
-            if (s + 3 < ns) load(B, s + 3);
-            compute(s + 1);
-            __syncthreads();
-        }
-    }
-}
-
-// pipeline2 whose first two slices were issued by the caller (A = slice 0, B = slice 1): a phase
-// whose weights were requested during the previous phase's last MFMAs starts on data that has
-// already landed instead of waiting a full HBM latency with the matrix cores idle.
-template <typename Set, typename Load, typename Store, typename Compute>
-__device__ __forceinline__ void pipeline2_pre(int ns, Set &A, Set &B, Load load, Store store,
-                                              Compute compute) {
-    for (int s = 0; s < ns; s += 2) {
-        store(A);
-        __syncthreads();
-        if (s + 2 < ns) load(A, s + 2);
-        compute(s);
-        __syncthreads();
-        if (s + 1 < ns) {
-            store(B);
-            __syncthreads();
-            if (s + 3 < ns) load(B, s + 3);
-            compute(s + 1);
-            __syncthreads();
-        }
-    }
-}
-
-// Same, with two LDS images: slice s + 1 is written into the other image while the MFMAs read
-// slice s, so each slice costs one barrier and the LDS writes overlap the matrix work.  The
-// register set of slice s + 1 was issued two compute phases before it is stored.
+// Two LDS images (layer 1 on the fp32 MFMA): slice s + 1 is written into the other image while the
+// MFMAs read slice s, so each slice costs one barrier and the LDS writes overlap the matrix work.
+// The register set of slice s + 1 was issued two compute phases before it is stored.
 template <typename Set, typename Load, typename Store, typename Compute>
 __device__ __forceinline__ void pipeline_db(int ns, Load load, Store store, Compute compute) {
     Set A, B;
@@ -422,8 +377,13 @@ __device__ __forceinline__ void mma_rows64(f32x4 (&acc)[5], const float *A, int 
 #pragma unroll
     for (int s = 0; s < BK / 4; ++s) {
         if (s + 1 < BK / 4) read(s + 1, (s + 1) & 1);
+#if MLP_PROBE_MODE == 11   // measurement only: hidden fwd / dZ fragments read, no MFMAs
+#pragma unroll
+        for (int t = 0; t < 5; ++t) acc[t][0] += a[s & 1] * b[s & 1][t];
+#else
 #pragma unroll
         for (int t = 0; t < 5; ++t) acc[t] = mfma4(a[s & 1], b[s & 1][t], acc[t]);
+#endif
     }
 }
 
@@ -469,137 +429,220 @@ __device__ __forceinline__ void epi_rows64_t(const f32x4 (&acc)[5], F f) {
               acc[t][r]);
 }
 
-// Forward layer on an LDS-resident input: H = act(Hin W^T + b), K = N = dh, W staged by slices.
-// A / B hold W's slices 0 and 1 (issued by the caller, ``prefetch_w``); ``next`` runs after the
-// last MFMAs, before the epilogue -- where the following phase's first slices are requested.
-template <typename M>
-__device__ __forceinline__ void prefetch_w(RowSlice<160> &A, RowSlice<160> &B, const M &W, int dh) {
-    A.load(W, dh, dh, 0);
-    B.load(W, dh, dh, BK);
-}
-template <typename M>
-__device__ __forceinline__ void prefetch_wt(ColSlice &A, ColSlice &B, const M &W, int dk, int dh) {
-    A.load(W, dh, dk, 0);
-    if (dk > BK) B.load(W, dh, dk, BK);
-}
+// ---- bf16x6 hidden phases (X6).  A staged weight slice is split once, by the threads that stage
+// it, into three bf16 planes [160 n][32 k] (l1_wofs layout, as layer 1's W1 planes: a lane's B
+// fragment is one ds_read_b128 per plane).  The LDS-resident fp32 activation operand is split per
+// fragment in registers (8 consecutive k of one row: two ds_read_b128).  Per K slice a wave then
+// issues 30 bf16 MFMAs (16 cycles each) instead of 40 fp32 ones (32 cycles each) and 17 wide LDS
+// reads instead of 48 ds_read_b32.
+constexpr int HPL = 160 * BK * 2;   // bytes per plane
+static_assert(3 * HPL <= STAGE_FLOATS * 4, "three W planes fit the staging area");
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
-template <typename M, typename Next>
-__device__ __forceinline__ void forward_hidden(const M &W, const M &bias, int dh, const float *Hin,
-                                               float *Hout, float *stage, int layer,
-                                               RowSlice<160> &A, RowSlice<160> &B, Next next) {
-    f32x4 acc[5];
-    zero(acc);
-    float bv[5];
-    load_bias5(bias, dh, bv);
-    pipeline2_pre<RowSlice<160>>(
-        (dh + BK - 1) / BK, A, B,
-        [&](RowSlice<160> &w, int s) { w.load(W, dh, dh, s * BK); },
-        [&](const RowSlice<160> &w) { w.store(stage); },
-        [&](int s) {
-            const int k0 = s * BK;
-            mma_rows64<false>(acc, Hin + k0, LDH, stage);
-        });
-    next();
-    epi_rows64_t(acc, [&](int m, int n, int t, float v) {
-        if (n < dh) Hout[m * LDH + n] = act_fwd(layer, v + bv[t]);
-    });
-}
-
-// Backward through a hidden layer: Hio <- (dZ W) * act'(Hio)  (in place), K = dk rows of W;
-// A / B hold W's slices 0 and 1 (``prefetch_wt``), ``next`` as above.
-template <typename M, typename Next>
-__device__ __forceinline__ void backward_dz(const M &W, int dk, int dh, const float *dZ, int ldz,
-                                            float *Hio, float *stage, int layer, ColSlice &A,
-                                            ColSlice &B, Next next) {
-    f32x4 acc[5];
-    zero(acc);
-    pipeline2_pre<ColSlice>(
-        (dk + BK - 1) / BK, A, B,
-        [&](ColSlice &w, int s) { w.load(W, dh, dk, s * BK); },
-        [&](const ColSlice &w) { w.store(stage); },
-        [&](int s) {
-            const int k0 = s * BK;
-            mma_rows64<true>(acc, dZ + k0, ldz, stage);
-        });
-    next();
-    epi_rows64(acc, [&](int m, int n, float v) {
-        if (n < dh) Hio[m * LDH + n] = v * act_grad(layer, Hio[m * LDH + n]);
-    });
-}
-
-// W3 held in registers from the layer-3 forward to the dZ2 backward (W_HOLD): the five forward
-// slices RowSlice<160> [n][32s..32s+31] cover W3 once, 50 floats per thread, so the backward's
-// row slices [32j..32j+31][*] are restaged from registers instead of re-read from HBM (the W3
-// re-read was 23 MB of the kernel's 315).  Thread element i of forward slice s is W3[n][32s + c]
-// with n = (tid + 512 i) / 32, c = tid % 32; backward slice j holds rows 32j..32j+31, i.e. the
-// thread's elements i = 2j and 2j + 1 of every forward slice.
-// Measured time-neutral (fwd3 -0.5, dZ2 -1.8 us, fwd2 +3.2 us issuing the 50 hold loads;
-// 240 VGPRs): off by default, kept as the measured alternative (-DW_HOLD=1).
-#ifndef W_HOLD
-#define W_HOLD 0
-#endif
-#if W_HOLD
-struct WHold {
-    RowSlice<160> s[5];
+// forward: B(n, k) = W[n][k0 + k], rows [0, n_rows), as 8-byte pairs (even dh, even offsets)
+struct RowPairs {
+    static constexpr int PER = 160 * BK / 2 / NTHR;   // 5 pairs per thread
+    f32x2 v[PER];
+    int k0_, nr_, K_;
+    template <typename M>
+    __device__ __forceinline__ void load(const M &W, int n_rows, int K, int k0) {
+        k0_ = k0;
+        nr_ = n_rows;
+        K_ = K;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int e = threadIdx.x + i * NTHR;
+            const int r = e / (BK / 2), c = 2 * (e % (BK / 2));
+            v[i] = *reinterpret_cast<const f32x2 *>(
+                W.at(r < n_rows ? r : n_rows - 1, k0 + c < K ? k0 + c : K - 2));
+        }
+    }
+    __device__ __forceinline__ void store(float *S) const {
+        char *pl = reinterpret_cast<char *>(S);
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int e = threadIdx.x + i * NTHR;
+            const int r = e / (BK / 2), c = 2 * (e % (BK / 2));
+            const f32x2 x = (r < nr_ && k0_ + c < K_) ? v[i] : f32x2{0.f, 0.f};
+            bf16x2 h, m, l;
+            split2(x.x, x.y, h, m, l);
+            const uint32_t o = l1_wofs(r, c);
+            *reinterpret_cast<bf16x2 *>(pl + o) = h;
+            *reinterpret_cast<bf16x2 *>(pl + HPL + o) = m;
+            *reinterpret_cast<bf16x2 *>(pl + 2 * HPL + o) = l;
+        }
+    }
 };
 
-template <typename M>
-__device__ __forceinline__ void hold_load(WHold &h, const M &W, int dh) {
+// backward: B(n, k) = W[k0 + k][n] (rows k of W, K = dk), staged transposed into the same planes;
+// a thread holds rows k, k + 1 of one column n (two coalesced scalar loads)
+struct ColPairs {
+    static constexpr int PER = 160 * BK / 2 / NTHR;   // 5
+    float v0[PER], v1[PER];
+    int k0_, nc_, K_;
+    template <typename M>
+    __device__ __forceinline__ void load(const M &W, int n_cols, int K, int k0) {
+        k0_ = k0;
+        nc_ = n_cols;
+        K_ = K;
 #pragma unroll
-    for (int i = 0; i < 5; ++i) h.s[i].load(W, dh, dh, i * BK);
+        for (int i = 0; i < PER; ++i) {
+            const int e = threadIdx.x + i * NTHR;
+            const int n = e % 160, k = k0 + 2 * (e / 160);
+            const int nn = n < n_cols ? n : n_cols - 1;
+            v0[i] = *W.at(k < K ? k : K - 1, nn);
+            v1[i] = *W.at(k + 1 < K ? k + 1 : K - 1, nn);
+        }
+    }
+    __device__ __forceinline__ void store(float *S) const {
+        char *pl = reinterpret_cast<char *>(S);
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int e = threadIdx.x + i * NTHR;
+            const int n = e % 160, kl = 2 * (e / 160), k = k0_ + kl;
+            const bool ok = n < nc_;
+            bf16x2 h, m, l;
+            split2(ok && k < K_ ? v0[i] : 0.f, ok && k + 1 < K_ ? v1[i] : 0.f, h, m, l);
+            const uint32_t o = l1_wofs(n, kl);
+            *reinterpret_cast<bf16x2 *>(pl + o) = h;
+            *reinterpret_cast<bf16x2 *>(pl + HPL + o) = m;
+            *reinterpret_cast<bf16x2 *>(pl + 2 * HPL + o) = l;
+        }
+    }
+};
+
+__device__ __forceinline__ bf16x8 cat8(const bf16x4 &a, const bf16x4 &b) {
+    return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
-// forward layer from a held W (all five slices already in registers)
-template <typename M>
-__device__ __forceinline__ void forward_hidden_held(const M &bias, int dh, const float *Hin,
-                                                    float *Hout, float *stage, int layer,
-                                                    const WHold &h) {
-    f32x4 acc[5];
+// split 8 consecutive fp32 values (two float4) into their three bf16x8 planes
+__device__ __forceinline__ void split8(const f32x4 &x0, const f32x4 &x1, bf16x8 &h, bf16x8 &m,
+                                       bf16x8 &l) {
+    bf16x4 h0, m0, l0, h1, m1, l1;
+    split4(x0, h0, m0, l0);
+    split4(x1, h1, m1, l1);
+    h = cat8(h0, h1);
+    m = cat8(m0, m1);
+    l = cat8(l0, l1);
+}
+
+// One K slice of the [64 x 160] output on the bf16 cores: acc/sml[t] += A[m][0..31] B[n][0..31]
+// for this wave's M-tile (w & 3) and N-tiles 5 (w >> 2) + t (epi_rows64's C/D map).  A is fp32
+// [m][lda] in LDS (16-byte aligned rows), B the three staged planes.
+__device__ __forceinline__ void mma_x6_rows64(f32x4 (&acc)[5], f32x4 (&sml)[5], const float *A,
+                                              int lda, const float *Bp) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int m = (wave & 3) * 16 + (lane & 15), q = lane >> 4;
+    const char *pl = reinterpret_cast<const char *>(Bp);
+    const f32x4 *ar = reinterpret_cast<const f32x4 *>(A + m * lda + 8 * q);
+    bf16x8 ah, am, al;
+    split8(ar[0], ar[1], ah, am, al);
+#pragma unroll
+    for (int t = 0; t < 5; ++t) {
+        const uint32_t ob = l1_wofs((wave >> 2) * 80 + 16 * t + (lane & 15), 8 * q);
+        const bf16x8 bh = *reinterpret_cast<const bf16x8 *>(pl + ob);
+        const bf16x8 bm = *reinterpret_cast<const bf16x8 *>(pl + HPL + ob);
+        const bf16x8 bl = *reinterpret_cast<const bf16x8 *>(pl + 2 * HPL + ob);
+        mfma_x6(ah, am, al, bh, bm, bl, acc[t], sml[t]);
+    }
+}
+
+// Whole-matrix register sets for the hidden phases : every K slice of a hidden weight
+// (dh <= 160 -> five slices, 10 floats per thread each) is requested at once, and each set is
+// re-issued with the NEXT phase's slice of the same index as soon as its own slice is in LDS
+// ("rolling"): the next phase's weights are in flight during this phase's remaining MFMAs and
+// epilogue, so a phase waits one HBM latency at most instead of one per pair of slices (the
+// two-slice pipeline was latency-bound: the same phases without MFMAs took 6-9 us of 10-12).
+// Five slices run whatever dh is (slices past dh stage zeros: exact zero products), so every
+// load and store is unconditional and the waits before the stores stay counted.
+constexpr int NSL = 5;
+static_assert(NSL * BK >= 152, "five K slices cover dh <= 152");
+template <typename Set, typename M>
+__device__ __forceinline__ void load_all_w(Set (&w)[NSL], const M &W, int dh) {
+#pragma unroll
+    for (int s = 0; s < NSL; ++s) w[s].load(W, dh, dh, s * BK);
+}
+template <typename Set, typename M>
+__device__ __forceinline__ void load_all_wt(Set (&w)[NSL], const M &W, int dk, int dh) {
+#pragma unroll
+    for (int s = 0; s < NSL; ++s) w[s].load(W, dh, dk, s * BK);
+}
+
+// Forward hidden layer from a whole-matrix set: roll(s) runs right after slice s is stored (it
+// re-issues w[s] with the next phase's slice s, or does nothing).
+// X6: W slices staged as bf16 planes (RowPairs) and the MFMAs on the bf16 cores; else fp32
+// [n][k] slices (RowSlice) on the fp32 MFMA.
+template <bool X6, typename M, typename Set, typename Roll>
+__device__ __forceinline__ void forward_hidden_all(const M &bias, int dh, const float *Hin,
+                                                   float *Hout, float *stage, int layer,
+                                                   Set (&w)[NSL], Roll roll) {
+    f32x4 acc[5], sml[5];
     zero(acc);
+    zero(sml);
     float bv[5];
     load_bias5(bias, dh, bv);
 #pragma unroll
-    for (int sl = 0; sl < 5; ++sl) {
-        if (sl * BK < dh) {
-            h.s[sl].store(stage);
-            __syncthreads();
-            mma_rows64<false>(acc, Hin + sl * BK, LDH, stage);
-            __syncthreads();
-        }
+    for (int s = 0; s < NSL; ++s) {
+        w[s].store(stage);
+        __syncthreads();
+        roll(s);
+        if constexpr (X6) mma_x6_rows64(acc, sml, Hin + s * BK, LDH, stage);
+        else mma_rows64<false>(acc, Hin + s * BK, LDH, stage);
+        __syncthreads();
+    }
+    if constexpr (X6) {
+#pragma unroll
+        for (int t = 0; t < 5; ++t) acc[t] += sml[t];
     }
     epi_rows64_t(acc, [&](int m, int n, int t, float v) {
         if (n < dh) Hout[m * LDH + n] = act_fwd(layer, v + bv[t]);
     });
 }
 
-// backward through a hidden layer from the held W: row slice j restaged [k][n] (ColSlice layout)
-__device__ __forceinline__ void backward_dz_held(int dh, const float *dZ, int ldz, float *Hio,
-                                                 float *stage, int layer, const WHold &h) {
-    f32x4 acc[5];
+// Backward through a hidden layer from a whole-matrix set of W^T slices (K = dk <= 160 rows)
+// X6: W^T slices staged as transposed bf16 planes (ColPairs); else fp32 [k][n] (ColSlice)
+template <bool X6, typename Set, typename Roll>
+__device__ __forceinline__ void backward_dz_all(int dh, const float *dZ, int ldz, float *Hio,
+                                                float *stage, int layer, Set (&w)[NSL],
+                                                Roll roll) {
+    f32x4 acc[5], sml[5];
     zero(acc);
-    const int tid = threadIdx.x, c = tid % BK;
+    zero(sml);
 #pragma unroll
-    for (int j = 0; j < 5; ++j) {
-        if (j * BK < dh) {
+    for (int s = 0; s < NSL; ++s) {
+        w[s].store(stage);
+        __syncthreads();
+        roll(s);
+        if constexpr (X6) mma_x6_rows64(acc, sml, dZ + s * BK, ldz, stage);
+        else mma_rows64<true>(acc, dZ + s * BK, ldz, stage);
+        __syncthreads();
+    }
+    if constexpr (X6) {
 #pragma unroll
-            for (int s = 0; s < 5; ++s)
-#pragma unroll
-                for (int q = 0; q < 2; ++q) {
-                    const int i = 2 * j + q;
-                    const int n = (tid + i * NTHR) / BK;     // W row (the backward's K)
-                    const int k = s * BK + c;                // W column (the backward's N)
-                    stage[(n - j * BK) * LDT + k] = (n < dh && k < dh) ? h.s[s].v[i] : 0.f;
-                }
-            __syncthreads();
-            mma_rows64<true>(acc, dZ + j * BK, ldz, stage);
-            __syncthreads();
-        }
+        for (int t = 0; t < 5; ++t) acc[t] += sml[t];
     }
     epi_rows64(acc, [&](int m, int n, float v) {
         if (n < dh) Hio[m * LDH + n] = v * act_grad(layer, Hio[m * LDH + n]);
     });
 }
-#endif
+
+// dZ3 = (dZ4 W4) * elu'(H3) in place: K = dout <= BK, so one W4^T slice (A, issued during the
+// layer-3 forward); next() runs after the MFMAs, before the epilogue.
+template <typename Next>
+__device__ __forceinline__ void backward_dz_one(int dh, const float *dZ, int ldz, float *Hio,
+                                                float *stage, int layer, const ColSlice &A,
+                                                Next next) {
+    f32x4 acc[5];
+    zero(acc);
+    A.store(stage);
+    __syncthreads();
+    mma_rows64<true>(acc, dZ, ldz, stage);
+    __syncthreads();
+    next();
+    epi_rows64(acc, [&](int m, int n, float v) {
+        if (n < dh) Hio[m * LDH + n] = v * act_grad(layer, Hio[m * LDH + n]);
+    });
+}
 
 // Weight gradient of a hidden layer: dW[i][j] = sum_b dZ[b][i] Hin[b][j] (both LDS-resident,
 // [64][LDH]), i, j < dh, straight into G; bias gradient db[i] = sum_b dZ[b][i] from Hin's ones
@@ -650,8 +693,10 @@ struct MlpArgs {
 #define STAMP(i) \
     if (p.stamps && threadIdx.x == 0) p.stamps[(int64_t)blockIdx.x * 16 + (i)] = wall_clock64()
 
-// L1X6: layer 1 on the bf16 matrix cores with the exact 3-way split (bf16x6, above); false =
-// fp32 MFMA (DLAMD_MLP_L1=fp32, a measurement knob)
+// L1X6: layer 1, dW1 and the hidden forward / dZ GEMMs on the bf16 matrix cores with the exact
+// 3-way split (bf16x6, above; the hidden dW tiles stay on the fp32 MFMA: a per-fragment split of
+// both batch-strided operands measured no faster); false = everything on the fp32 MFMA
+// (DLAMD_MLP_L1=fp32, a measurement knob)
 template <bool TILED, bool L1X6>
 __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -686,8 +731,13 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
     __syncthreads();
     if (tid < MB) H1[tid * LDH + dh] = 1.f;   // ones column: db2 in dW2's MFMAs
 
-    RowSlice<160> wa, wb;   // a forward phase's first two W slices, requested one phase early
-    ColSlice ta, tb;        // the same for the backward phases
+    // a forward phase's whole W, requested during the phase before, and the same for the
+    // backward phases' W^T: bf16-plane pair sets (X6) or fp32 slices
+    using WSet = std::conditional_t<L1X6, RowPairs, RowSlice<160>>;
+    using TSet = std::conditional_t<L1X6, ColPairs, ColSlice>;
+    WSet w5[NSL];
+    TSet t5[NSL];
+    ColSlice ta;            // dZ3's W4^T slice (K = dout)
     // ---- layer 1: H1 = relu(x W1^T + b1), K = din from HBM: x and W1 slices double-buffered in
     // LDS (the H2/H3 space, free until layer 2), the next two register-prefetched
     if constexpr (L1X6) {
@@ -816,7 +866,7 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
                 }
             }
         }
-        prefetch_w(wa, wb, mat(Xr, o_w2, dh), dh);   // layer 2's first slices
+        load_all_w(w5, mat(Xr, o_w2, dh), dh);   // layer 2's weights
         __syncthreads();   // every consumer is done with the images before H2/H3 are written
     } else {
         f32x4 acc[5];
@@ -851,7 +901,7 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
                 mma_rows64<false>(acc, H2 + buf * IMG, LDS1, H2 + buf * IMG + MB * LDS1);
 #endif
             });
-        prefetch_w(wa, wb, mat(Xr, o_w2, dh), dh);   // layer 2's first slices
+        load_all_w(w5, mat(Xr, o_w2, dh), dh);   // layer 2's weights
         epi_rows64_t(acc, [&](int m, int n, int t, float v) {
             if (n < dh) H1[m * LDH + n] = act_fwd(0, v + bv[t]);
         });
@@ -862,14 +912,8 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
     }
     __syncthreads();
     STAMP(1);
-#if W_HOLD
-    WHold w3h;   // W3 from HBM once, for the layer-3 forward and the dZ2 backward
-    forward_hidden(mat(Xr, o_w2, dh), mat(Xr, o_b2, 0), dh, H1, H2, stage, 1, wa, wb,
-                   [&] { hold_load(w3h, mat(Xr, o_w3, dh), dh); });
-#else
-    forward_hidden(mat(Xr, o_w2, dh), mat(Xr, o_b2, 0), dh, H1, H2, stage, 1, wa, wb,
-                   [&] { prefetch_w(wa, wb, mat(Xr, o_w3, dh), dh); });
-#endif
+    forward_hidden_all<L1X6>(mat(Xr, o_b2, 0), dh, H1, H2, stage, 1, w5,
+                       [&](int sl) { w5[sl].load(mat(Xr, o_w3, dh), dh, dh, sl * BK); });
     __syncthreads();
     STAMP(2);
     // the logits' operands from HBM (W4 image values, b4, this wave's labels), issued now so they
@@ -886,13 +930,9 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
     int lab[MB / 8];
 #pragma unroll
     for (int i = 0; i < MB / 8; ++i) lab[i] = p.labels[(int64_t)a * p.s_lab + wave + 8 * i];
-#if W_HOLD
-    prefetch_wt(ta, tb, mat(Xr, o_w4, dh), dout, dh);
-    forward_hidden_held(mat(Xr, o_b3, 0), dh, H2, H3, stage, 2, w3h);
-#else
-    forward_hidden(mat(Xr, o_w3, dh), mat(Xr, o_b3, 0), dh, H2, H3, stage, 2, wa, wb,
-                   [&] { prefetch_wt(ta, tb, mat(Xr, o_w4, dh), dout, dh); });
-#endif
+    forward_hidden_all<L1X6>(mat(Xr, o_b3, 0), dh, H2, H3, stage, 2, w5, [&](int sl) {
+        if (sl == NSL - 1) ta.load(mat(Xr, o_w4, dh), dh, dout, 0);   // dZ3's W4^T (dout <= 16)
+    });
     STAMP(3);
     // ---- logits Z = H3 W4^T + b4 (waves 0-3, one 16 x 16 tile each), W4 image [16][LDW4]
 #pragma unroll
@@ -960,30 +1000,21 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
     }
     __syncthreads();
     // ---- dZ3 = (dZ4 W4) * elu'(H3) in place, K = dout
-#if W_HOLD
-    backward_dz(mat(Xr, o_w4, dh), dout, dh, Zs, LDZ, H3, stage, 2, ta, tb,
-                [&] { prefetch_wt(ta, tb, mat(Xr, o_w2, dh), dh, dh); });   // for dZ1
-#else
-    backward_dz(mat(Xr, o_w4, dh), dout, dh, Zs, LDZ, H3, stage, 2, ta, tb,
-                [&] { prefetch_wt(ta, tb, mat(Xr, o_w3, dh), dh, dh); });
-#endif
+    backward_dz_one(dh, Zs, LDZ, H3, stage, 2, ta,   // dZ2's W3^T lands during dW3
+                    [&] { load_all_wt(t5, mat(Xr, o_w3, dh), dh, dh); });
     __syncthreads();
     STAMP(5);
     weight_grad_hidden(H3, H2, dh, mat(Gr, o_w3, dh), mat(Gr, o_b3, 0));
     __syncthreads();
     STAMP(6);
-#if W_HOLD
-    backward_dz_held(dh, H3, LDH, H2, stage, 1, w3h);                         // dZ2 into H2
-#else
-    backward_dz(mat(Xr, o_w3, dh), dh, dh, H3, LDH, H2, stage, 1, ta, tb,     // dZ2 into H2
-                [&] { prefetch_wt(ta, tb, mat(Xr, o_w2, dh), dh, dh); });
-#endif
+    backward_dz_all<L1X6>(dh, H3, LDH, H2, stage, 1, t5,    // dZ2 into H2; dZ1's W2^T rolls in
+                    [&](int sl) { t5[sl].load(mat(Xr, o_w2, dh), dh, dh, sl * BK); });
     __syncthreads();
     STAMP(7);
     weight_grad_hidden(H2, H1, dh, mat(Gr, o_w2, dh), mat(Gr, o_b2, 0));
     __syncthreads();
     STAMP(8);
-    backward_dz(mat(Xr, o_w2, dh), dh, dh, H2, LDH, H1, stage, 0, ta, tb, [] {});  // dZ1 into H1
+    backward_dz_all<L1X6>(dh, H2, LDH, H1, stage, 0, t5, [](int) {});   // dZ1 into H1
     __syncthreads();
     STAMP(9);
     // ---- dW1 = dZ1^T x [dh x din], K = the 64 batch rows.
@@ -1146,7 +1177,7 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
 }  // namespace
 
 int mlp_fused_supported(int batch, int din, int dh, int dout) {
-    return batch == MB && din > 0 && din % 4 == 0 && dh > 0 && dh <= 152 && dout > 0 &&
+    return batch == MB && din > 0 && din % 4 == 0 && dh > 0 && dh <= 152 && dh % 2 == 0 && dout > 0 &&
            dout <= 16;
 }
 

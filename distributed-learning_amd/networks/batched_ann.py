@@ -20,7 +20,7 @@ from .ann_model import ANNModel
 
 def fused_supported(batch, input_dim, hidden_dim, output_dim):
     """Shapes the one-launch kernel (dl_mlp_grad, csrc/mlp_fused.hip) covers."""
-    return batch == 64 and input_dim % 4 == 0 and 0 < hidden_dim <= 152 and 0 < output_dim <= 16
+    return batch == 64 and input_dim % 4 == 0 and 0 < hidden_dim <= 152 and hidden_dim % 2 == 0 and 0 < output_dim <= 16
 
 
 class BatchedANN:

@@ -478,7 +478,7 @@ int dl_xent_grad(const float *Z, int64_t sZ, const int32_t *y, int64_t sY, float
  * agent's forward (Linear-ReLU-Linear-Tanh-Linear-ELU-Linear), torch.nn.CrossEntropyLoss (mean)
  * and backward, one workgroup per agent with its activations resident in LDS.  Replaces the
  * 11-launch dl_bgemm sequence for the shapes it supports (batch == 64, input_dim % 4 == 0,
- * hidden_dim <= 152, output_dim <= 16); other shapes return DL_ERR_UNSUPPORTED and the caller
+ * even hidden_dim <= 152, output_dim <= 16); other shapes return DL_ERR_UNSUPPORTED and the caller
  * uses dl_bgemm.
  *   X [n_agents, ldx]: parameter rows in the Mixer flatten order (mixer.py:68-69: fc1.weight,
  *     fc1.bias, fc2.weight, fc2.bias, fc3.weight, fc3.bias, fc4.weight, fc4.bias);

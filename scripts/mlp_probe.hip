@@ -26,7 +26,10 @@ hipError_t allow_full_lds(const void *k) {
 int main(int argc, char **argv) {
     // argv[1] == "fp32": layer 1 and dW1 on the fp32 MFMA (default: the bf16x6 split)
     const bool x6 = !(argc > 1 && argv[1][0] == 'f');
-    auto kern = x6 ? dl::mlp_fused_kernel<false, true> : dl::mlp_fused_kernel<false, false>;
+    // argv[2] == "tiled": X and G in the engine's column-tiled layout (T = 64 for 256 agents)
+    const bool tiled = argc > 2 && argv[2][0] == 't';
+    auto kern = tiled ? (x6 ? dl::mlp_fused_kernel<true, true> : dl::mlp_fused_kernel<true, false>)
+                      : (x6 ? dl::mlp_fused_kernel<false, true> : dl::mlp_fused_kernel<false, false>);
     const int N = 256, B = 64, din = 784, dh = 150, dout = 10;
     const long P = (long)dh * din + dh + 2 * (dh * dh + dh) + dout * dh + dout;
     const long ld = (P + 63) / 64 * 64;
@@ -50,7 +53,9 @@ int main(int argc, char **argv) {
     CHECK(hipMemcpy(D, hd.data(), hd.size() * 4, hipMemcpyHostToDevice));
     CHECK(hipMemcpy(Y, hl.data(), hl.size() * 4, hipMemcpyHostToDevice));
     CHECK(dl::allow_full_lds(reinterpret_cast<const void *>(kern)));
-    dl::MlpArgs p{X, ld, D, (long)B * din, Y, B, G, ld, L, din, dh, dout, 0, 0, st};
+    // tiled: T = 64 -> tsh 6, tile stride N * 64 floats (ld is a multiple of 64: whole tiles)
+    dl::MlpArgs p{X, ld, D, (long)B * din, Y, B, G, ld, L, din, dh, dout, tiled ? 6 : 0,
+                  tiled ? (long)N * 64 : 0, st};
     int rate_khz = 0;
     CHECK(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, 0));
     const char *names[] = {"layer1 fwd", "fwd2", "fwd3", "logits+xent", "dW4+db4+dZ3", "dW3",

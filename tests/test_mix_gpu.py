@@ -112,6 +112,21 @@ def test_mix_shapes_bit_exact(cuda, n, P, deg, sgd):
         assert np.all(dsq == 0) and dmax == 0.0
 
 
+@pytest.mark.parametrize("sgd", [False, True])
+def test_row_major_ragged_last_pass(cuda, sgd):
+    """Row-major tiles whose last pass is ragged (256 agents: 515 tiles of 128 columns on the
+    balanced grid) and a guarded 5-column tail behind them: bits and deviations as the oracle's."""
+    n, P = 256, 515 * 128 + 5
+    rng = np.random.default_rng(11)
+    csr = graph_csr(n, 4, seed=3)
+    X = rng.standard_normal((n, P), dtype=np.float32)
+    G = rng.standard_normal((n, P), dtype=np.float32) if sgd else None
+    Y, dsq, dmax, mean = run_round(csr, X, G, 0.05, dev=True, cuda=cuda)
+    want = cref.mix_round(X, csr.rowptr, csr.col, csr.w, G=G, lr=0.05)
+    assert np.array_equal(bits(Y), bits(want))
+    check_dev(Y, dsq, dmax, mean)
+
+
 def test_regular_graph_skips_rowptr(cuda):
     from distributed_learning_amd.graph import Csr
     E = eng_mod()

@@ -206,10 +206,11 @@ def kernel_name(plan, sgd, dev, n_src):
     need = -(-n_src // (1024 // c))
     kv = 2 if need <= 2 else 4 if need <= 4 else 8
     b = lambda v: "true" if v else "false"  # noqa: E731
-    return f"mix_tile_kernel<{c}, {kv}, {b(sgd)}, {b(dev)}, true, false, true>"
+    # prefix of the instantiation (the trailing RD / LAG parameters are the defaults)
+    return f"mix_tile_kernel<{c}, {kv}, {b(sgd)}, {b(dev)}, true, false, true, 0, false>"
 
 
-def traffic_from_profile(kname, path=os.path.join(ROOT, "profiles", "r08", "summary.json")):
+def traffic_from_profile(kname, path=os.path.join(ROOT, "profiles", "r09", "summary.json")):
     """HBM bytes per launch of this kernel from the committed rocprofv3 PMC summary
     (FETCH_SIZE x 2 + WRITE_SIZE, gfx950 correction), or None if it was not profiled."""
     try:
@@ -399,8 +400,8 @@ def run_c3(args, dev, rank, world):
     gbs = mix_bytes / (mix_ms / 1e3) / 1e9
     if rank != 0:
         return
-    # HBM bytes per launch from the committed PMC passes of this workload (profiles/r08/c3)
-    c3_path = os.path.join(ROOT, "profiles", "r08", "c3", "summary.json")
+    # HBM bytes per launch from the committed PMC passes of this workload (profiles/r09/c3)
+    c3_path = os.path.join(ROOT, "profiles", "r09", "c3", "summary.json")
     c3_grad_traffic, c3_src = (traffic_from_profile("mlp_fused_kernel", c3_path)
                                if ann.path == "fused" and args.c3_layout == "rows"
                                else (None, None))
@@ -412,10 +413,10 @@ def run_c3(args, dev, rank, world):
                  "kernel": ("mlp_fused_kernel" if ann.path == "fused" else
                             "dl_bgemm x11 + dl_xent_grad") + " (per-step HIP-event time)",
                  "flops_per_launch": flops, "launch_ms": grad_ms,
-                 "arithmetic": "fp32 GEMMs: hidden layers on the fp32 MFMA; layer 1 and dW1 on the "
+                 "arithmetic": "fp32 GEMMs: layer 1, dW1 and the hidden forward / dZ GEMMs on the "
                                "bf16 matrix cores as exact 3-way bf16 splits (six products, "
-                               "csrc/mlp_fused.hip); achieved counts the fp32 FLOPs, peak is the "
-                               "fp32 MFMA peak"}
+                               "csrc/mlp_fused.hip), the hidden dW tiles and the head on the fp32 "
+                               "MFMA; achieved counts the fp32 FLOPs, peak is the fp32 MFMA peak"}
     mix_roof = {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": gbs / HBM_PEAK_GBS, "traffic": c3_mix_traffic,
                 "traffic_source": c3_src if c3_mix_traffic else None,

@@ -912,6 +912,9 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
     }
     __syncthreads();
     STAMP(1);
+#if MLP_PROBE_MODE == 12   // measurement only: layer 1 alone (PMC of its traffic)
+    return;
+#endif
     forward_hidden_all<L1X6>(mat(Xr, o_b2, 0), dh, H1, H2, stage, 1, w5,
                        [&](int sl) { w5[sl].load(mat(Xr, o_w3, dh), dh, dh, sl * BK); });
     __syncthreads();

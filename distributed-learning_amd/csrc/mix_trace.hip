@@ -24,6 +24,26 @@ namespace dl {
 namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// (lo, hi) += w * v on v's (x, y) / (z, w) halves: each v_pk_mul_f32 / v_pk_add_f32 rounds every
+// lane as the scalar ops do, so the fold's bits are those of acc.x = acc.x + w * v.x, ... .  The
+// pairs are the halves of the ds_read_b128 registers.  (Written per component, the deviation's
+// sums let the vectorizer pair (x, z) / (y, w): three moves per neighbour, and each LDS read
+// waited for before the next was issued -- the rows kernel ran 1978 instead of 2520 rounds/s.)
+__device__ __forceinline__ void fold2(f32x2 &lo, f32x2 &hi, float w, const f32x4 &v) {
+    const f32x2 w2 = {w, w};
+    lo = lo + w2 * __builtin_shufflevector(v, v, 0, 1);
+    hi = hi + w2 * __builtin_shufflevector(v, v, 2, 3);
+}
+
+// ||(lo, hi) - (mlo, mhi)||^2 summed as (dx^2 + dy^2) + (dz^2 + dw^2)
+__device__ __forceinline__ float dev2(const f32x2 &lo, const f32x2 &hi, const f32x2 &mlo,
+                                      const f32x2 &mhi) {
+    const f32x2 dl = lo - mlo, dh = hi - mhi;
+    const f32x2 ql = dl * dl, qh = dh * dh;
+    return (ql.x + ql.y) + (qh.x + qh.y);
+}
 
 __device__ __forceinline__ float4 tr_load4(const char *p) {
     const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(p));
@@ -89,20 +109,17 @@ __global__ void __launch_bounds__(kTileThreads) mix_trace_kernel(TileArgs a, int
             wreg[e] = a.w[e];
         }
     }
-    // agent tid's output chunk c: left fold in CSR order from +0.0 (mixer.py:47)
-    auto mix = [&](const float4 *src, int c) {
-        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    // agent tid's output chunk c: left fold in CSR order from +0.0 (mixer.py:47), as pairs
+    auto mix = [&](const float4 *src, int c, f32x2 &lo, f32x2 &hi) {
+        lo = f32x2{0.f, 0.f};
+        hi = f32x2{0.f, 0.f};
         if constexpr (RE > 0) {
             const char *base = reinterpret_cast<const char *>(src + c * N);
+            f32x4 v[RE];
 #pragma unroll
-            for (int e = 0; e < RE; ++e) {
-                const float4 v = *reinterpret_cast<const float4 *>(base + coff[e]);
-                const float w = wreg[e];
-                acc.x = acc.x + w * v.x;
-                acc.y = acc.y + w * v.y;
-                acc.z = acc.z + w * v.z;
-                acc.w = acc.w + w * v.w;
-            }
+            for (int e = 0; e < RE; ++e) v[e] = *reinterpret_cast<const f32x4 *>(base + coff[e]);
+#pragma unroll
+            for (int e = 0; e < RE; ++e) fold2(lo, hi, wreg[e], v[e]);
         } else {
             int e0, e1;
             if (reg) {
@@ -113,16 +130,9 @@ __global__ void __launch_bounds__(kTileThreads) mix_trace_kernel(TileArgs a, int
                 e1 = lrp[tid + 1];
             }
             const float *wr = wshared ? lw - e0 : lw;
-            for (int e = e0; e < e1; ++e) {
-                const float w = wr[e];
-                const float4 v = src[c * N + lcol[e]];
-                acc.x = acc.x + w * v.x;
-                acc.y = acc.y + w * v.y;
-                acc.z = acc.z + w * v.z;
-                acc.w = acc.w + w * v.w;
-            }
+            const f32x4 *sv = reinterpret_cast<const f32x4 *>(src + c * N);
+            for (int e = e0; e < e1; ++e) fold2(lo, hi, wr[e], sv[lcol[e]]);
         }
-        return acc;
     };
     // byte offset of (agent tid, chunk q) in an operand laid out in lc-chunk tiles (lc a power
     // of two; the step index is wave-uniform, so the tile part is scalar arithmetic)
@@ -191,14 +201,14 @@ __global__ void __launch_bounds__(kTileThreads) mix_trace_kernel(TileArgs a, int
                     float d = 0.f;
 #pragma unroll
                     for (int c = 0; c < C; ++c) {
-                        const float4 y = mix(src, c);
+                        f32x2 lo, hi;
+                        mix(src, c, lo, hi);
+                        const float4 y = make_float4(lo.x, lo.y, hi.x, hi.y);
                         if (r + 1 < rounds)
                             dst[c * N + tid] = y;
                         else
                             tr_store4(y, yb + off(a.yts, yrow, q * C + c));
-                        const float dx = y.x - mean[c].x, dy = y.y - mean[c].y;
-                        const float dz = y.z - mean[c].z, dw = y.w - mean[c].w;
-                        d += (dx * dx + dy * dy) + (dz * dz + dw * dw);
+                        d += dev2(lo, hi, f32x2{mean[c].x, mean[c].y}, f32x2{mean[c].z, mean[c].w});
                     }
                     dacc[r] += d;
                 }
@@ -246,19 +256,16 @@ __global__ void __launch_bounds__(kTileThreads) mix_trace_rows_kernel(TileArgs a
 #pragma unroll
         for (int e = 0; e < RE; ++e) coff[k][e] = ((uint32_t)a.col[ag * RE + e] * C + c) * 16u;
     }
-    auto mix = [&](const float4 *src, int k) {
+    // the fold as (x, y) / (z, w) pairs (fold2), the five neighbour reads issued first
+    auto mix = [&](const float4 *src, int k, f32x2 &lo, f32x2 &hi) {
         const char *base = reinterpret_cast<const char *>(src);
-        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        f32x4 v[RE];
 #pragma unroll
-        for (int e = 0; e < RE; ++e) {
-            const float4 v = *reinterpret_cast<const float4 *>(base + coff[k][e]);
-            const float w = wreg[e];
-            acc.x = acc.x + w * v.x;
-            acc.y = acc.y + w * v.y;
-            acc.z = acc.z + w * v.z;
-            acc.w = acc.w + w * v.w;
-        }
-        return acc;
+        for (int e = 0; e < RE; ++e) v[e] = *reinterpret_cast<const f32x4 *>(base + coff[k][e]);
+        lo = f32x2{0.f, 0.f};
+        hi = f32x2{0.f, 0.f};
+#pragma unroll
+        for (int e = 0; e < RE; ++e) fold2(lo, hi, wreg[e], v[e]);
     };
     const int lsh = __builtin_ctz((unsigned)a.lchunks);
     const int64_t lmask = (int64_t)a.lchunks - 1;
@@ -314,6 +321,7 @@ __global__ void __launch_bounds__(kTileThreads) mix_trace_rows_kernel(TileArgs a
         }
         const float n = (float)N;
         mean = make_float4(mean.x / n, mean.y / n, mean.z / n, mean.w / n);
+        const f32x2 mlo = {mean.x, mean.y}, mhi = {mean.z, mean.w};
         if (q + gridDim.x < nsteps) prefetch(q + gridDim.x);   // lands during the rounds
         const float4 *src = img0;
         float4 *dst = img1;
@@ -326,14 +334,14 @@ __global__ void __launch_bounds__(kTileThreads) mix_trace_rows_kernel(TileArgs a
                     const int ag = s + k * SLOTS;
                     float v = 0.f;
                     if (ag < N) {
-                        const float4 y = mix(src, k);
+                        f32x2 lo, hi;
+                        mix(src, k, lo, hi);
+                        const float4 y = make_float4(lo.x, lo.y, hi.x, hi.y);
                         if (r + 1 < rounds)
                             dst[ag * C + c] = y;
                         else
                             tr_store4(y, yb + off(a.yts, (int64_t)ag * a.yrs, q * C + c));
-                        const float dx = y.x - mean.x, dy = y.y - mean.y;
-                        const float dz = y.z - mean.z, dw = y.w - mean.w;
-                        v = (dx * dx + dy * dy) + (dz * dz + dw * dw);
+                        v = dev2(lo, hi, mlo, mhi);
                     }
                     v += quad_xor1(v);   // the agent's 4 chunk lanes (whole wave active)
                     v += quad_xor2(v);

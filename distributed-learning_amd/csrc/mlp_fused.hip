@@ -184,6 +184,19 @@ struct ParMat {
     __device__ __forceinline__ float *at(int r, int c) const { return row.at(off + r * ld + c); }
 };
 
+#ifndef G_NT
+#define G_NT 0
+#endif
+// one gradient value into G (G_NT: non-temporal, so G does not displace X' and the batch in the
+// MALL; measurement knob)
+__device__ __forceinline__ void gstore(float *p, float v) {
+#if G_NT
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
+
 // Store a finished 32 x 32 MFMA tile: register r holds row i0 + (r & 3) + 8 (r >> 2) of this
 // lane's column j (C/D map); every store instruction writes two 128-B runs.  (Issuing these
 // stores interleaved with the next tile's MFMA chain measured slower: dW1 53 -> 64 us.)
@@ -196,7 +209,7 @@ __device__ __forceinline__ void store_tile(const f32x16 &v, int i0, int j, const
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int i = i0 + (r & 3) + 8 * (r >> 2);
-            if (i < rows) *bias.at(0, i) = v[r];
+            if (i < rows) gstore(bias.at(0, i), v[r]);
         }
         return;
     }
@@ -207,17 +220,17 @@ __device__ __forceinline__ void store_tile(const f32x16 &v, int i0, int j, const
             float *p = m.at(i0, j);
             const int ld = m.ld;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) p[((r & 3) + 8 * (r >> 2)) * ld] = v[r];
+            for (int r = 0; r < 16; ++r) gstore(p + ((r & 3) + 8 * (r >> 2)) * ld, v[r]);
         } else {
 #pragma unroll
-            for (int r = 0; r < 16; ++r) *m.at(i0 + (r & 3) + 8 * (r >> 2), j) = v[r];
+            for (int r = 0; r < 16; ++r) gstore(m.at(i0 + (r & 3) + 8 * (r >> 2), j), v[r]);
         }
         return;
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         const int i = i0 + (r & 3) + 8 * (r >> 2);
-        if (i < rows) *m.at(i, j) = v[r];
+        if (i < rows) gstore(m.at(i, j), v[r]);
     }
 }
 
@@ -996,8 +1009,8 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int i = 4 * (lane >> 4) + r;
-                if (i < dout && j < dh) *Gr.at(o_w4 + i * dh + j) = acc[r];
-                if (i < dout && j == dh) *Gr.at(o_b4 + i) = acc[r];   // H3's ones column
+                if (i < dout && j < dh) gstore(Gr.at(o_w4 + i * dh + j), acc[r]);
+                if (i < dout && j == dh) gstore(Gr.at(o_b4 + i), acc[r]);   // H3's ones column
             }
         }
     }

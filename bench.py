@@ -80,8 +80,10 @@ def parse():
                    help="c3: resident layout of X and G (tiled: the fused gradient kernel "
                         "addresses the round's column tiles; measured equal overall)")
     p.add_argument("--batch", type=int, default=64, help="c5: images per agent per step")
-    p.add_argument("--cudnn-benchmark", action="store_true",
-                   help="c5: torch.backends.cudnn.benchmark (MIOpen exhaustive find)")
+    p.add_argument("--cudnn-benchmark", action=argparse.BooleanOptionalAction, default=True,
+                   help="c5: torch.backends.cudnn.benchmark (MIOpen picks the fastest measured "
+                        "solver per shape: 6.90 vs 6.66 steps/s; --no-cudnn-benchmark keeps the "
+                        "default heuristic)")
     p.add_argument("--no-halo-probe", action="store_true",
                    help="N>1: skip the c4 agent-partition (RCCL halo exchange) probe that the "
                         "c2 line carries as its 'c4_halo' object")

@@ -363,24 +363,28 @@ def run_c3(args, dev, rank, world):
     sgd = MLPConsensusSGD(ann, eng, data, labels, lr, deviation=True)
     G = sgd.G
     stream = torch.cuda.current_stream(dev)
-    # phase times: eager steps bracketed by HIP events (kernel time is the same under a graph),
-    # after warmup steps that load every kernel's code object
+    # phase times: n_ev back-to-back launches of each phase between one pair of HIP events on
+    # the launch stream, after warmup steps that load every kernel's code object.  (An event pair
+    # around every eager launch also timed the host's submission gaps: 170-177 us for a kernel
+    # rocprofv3 puts at 154-164 us.)
     for _ in range(max(args.warmup, 2)):
         sgd.step()
-    n_ev = min(args.steps, 20)
-    evs = event_pairs(n_ev, 3)
+    n_ev = max(min(args.steps, 20), 1)
+    e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+    torch.cuda.synchronize()
+    e0.record(stream)
     for i in range(n_ev):
-        evs[i][0].record(stream)
         if eng.layout == "tiled":
             ann.gradients(eng.X, data, labels, G)
         else:
             ann.gradients(eng.X[:, :P], data, labels, G[:, :P])
-        evs[i][1].record(stream)
+    e1.record(stream)
+    for i in range(n_ev):
         eng.round(G=G, lr=lr, deviation=True)
-        evs[i][2].record(stream)
+    e2.record(stream)
     torch.cuda.synchronize()
-    grad_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in evs]))
-    mix_ms = float(np.mean([b.elapsed_time(c) for _, b, c in evs]))
+    grad_ms = e0.elapsed_time(e1) / n_ev
+    mix_ms = e1.elapsed_time(e2) / n_ev
     losses = [sgd.loss.mean()]
     use_graph = not args.no_graph
     if use_graph:
@@ -413,7 +417,8 @@ def run_c3(args, dev, rank, world):
                  "unit": "TFLOP/s", "frac": tflops / FP32_MFMA_PEAK_TFLOPS,
                  "traffic": c3_grad_traffic, "traffic_source": c3_src if c3_grad_traffic else None,
                  "kernel": ("mlp_fused_kernel" if ann.path == "fused" else
-                            "dl_bgemm x11 + dl_xent_grad") + " (per-step HIP-event time)",
+                            "dl_bgemm x11 + dl_xent_grad") + " (HIP events around 20 "
+                           "back-to-back launches)",
                  "flops_per_launch": flops, "launch_ms": grad_ms,
                  "arithmetic": "fp32 GEMMs: layer 1, dW1 and the hidden forward / dZ GEMMs on the "
                                "bf16 matrix cores as exact 3-way bf16 splits (six products, "

@@ -254,6 +254,46 @@ def test_full_size_round_column_slices(cuda):
                                rtol=DEV_RTOL)
 
 
+def test_full_size_c4_torus_column_slices(cuda):
+    """BASELINE config c4 at full size on one GPU (64 x 64 torus, 4096 agents x 2^18 params,
+    best-constant weights, fused local step + deviation, the engine's column-tiled layout):
+    column slices bit-exact against the oracle; size-independent properties of the whole round
+    -- W doubly stochastic, so every column sum of the stepped inputs is preserved (fp64 sums
+    on the device, within fp32 rounding), and the fused deviation equals an fp64 recomputation
+    from the output."""
+    import math
+    from distributed_learning_amd.graph import from_edge_weights, torus_edges
+    E = eng_mod()
+    n, P, lr = 4096, 1 << 18, 1e-3
+    e = torus_edges(64, 64)
+    w = 2.0 / (2.0 - 2.0 * math.cos(2 * math.pi / 64) + 8.0)
+    csr = from_edge_weights(e, [w] * len(e), list(range(n)))
+    g = torch.Generator(device=cuda).manual_seed(4)
+    X = torch.randn(n, P, device=cuda, generator=g)
+    G = torch.randn(n, P, device=cuda, generator=g)
+    eng = E.GossipEngine(csr, P, device=cuda, X=X)
+    plan = eng.plan(deviation=True)
+    assert plan["path"] == 1 and eng.layout == "tiled"
+    eng.round(G=eng.layout_like(G), lr=lr, deviation=True)
+    torch.cuda.synchronize()
+    Y = eng.rows()
+    for c0, c1 in [(0, 2048), (P - 2048, P), (77777, 77777 + 513)]:
+        want = cref.mix_round(X[:, c0:c1].cpu().numpy(), csr.rowptr, csr.col, csr.w,
+                              G=G[:, c0:c1].cpu().numpy(), lr=lr)
+        assert np.array_equal(bits(Y[:, c0:c1].cpu().numpy()), bits(want)), (c0, c1)
+    T = X - np.float32(lr) * G          # the stepped inputs, rounded as the kernel does
+    cs_in, cs_out = T.double().sum(0), Y.double().sum(0)
+    scale = T.double().abs().sum(0)
+    assert float(((cs_out - cs_in).abs() / scale).max()) < 1e-5
+    del T
+    Yd = Y.double()
+    dsq = ((Yd - Yd.mean(0)) ** 2).sum(1)
+    del Yd
+    np.testing.assert_allclose(np.sqrt(eng.dev_sq.cpu().numpy()), np.sqrt(dsq.cpu().numpy()),
+                               rtol=DEV_RTOL)
+    assert float(eng.dev_max.item()) == pytest.approx(float(dsq.max().sqrt()), rel=DEV_RTOL)
+
+
 @pytest.mark.parametrize("layout,P", [("rows", 10 ** 6), ("rows", 10 ** 6 + 3),
                                       ("tiled", 10 ** 6 + 8)])
 def test_full_size_tail_columns(cuda, layout, P):

@@ -10,6 +10,7 @@ import numpy as np
 import pytest
 import torch
 
+from oracle import cref
 from oracle import mixer_ref as M
 from test_mix_gpu import bits
 
@@ -232,3 +233,45 @@ def test_mixer_traced_stop_tie_uses_row_order_mean(cuda):
             models[k].load_state_dict(init[k].state_dict())
         got_n = Mixer(models, topo, logging.getLogger("tie")).mix(times=1, eps=eps)
         assert got_n == want_n, (r, traced[r], ref[r], eps)
+
+
+def test_full_size_c2_gossip_traced_pass(cuda):
+    """BASELINE config c2 as pure gossip at full size (1024 agents x 2^20, random 4-regular
+    graph, best-constant weights): one traced pass of 24 rounds (Mixer.mix(times, eps)'s device
+    path) -- column slices of the final iterate bit-exact against 24 oracle rounds on the slice,
+    the pass input left intact, and every round's max deviation against the fused deviation of
+    24 single-round launches of the same iterates."""
+    from distributed_learning_amd.graph import from_edge_weights, random_regular_edges
+    e = E()
+    n, P, K = 1024, 1 << 20, 24
+    edges = random_regular_edges(4, n, seed=0)
+    csr = from_edge_weights(edges, [0.25] * len(edges))
+    assert csr.doubly_stochastic
+    W = e.DeviceCsr(csr, cuda)
+    g = torch.Generator(device=cuda).manual_seed(2)
+    X = torch.randn(n, P, device=cuda, generator=g)
+    T = 16
+    Xt = e.to_tiled(X, T)
+    Yt = torch.empty_like(Xt)
+    assert e.trace_max_rounds(W, Xt, Yt, tiled=(P, T)) >= K
+    trace = torch.full((K,), -1.0, device=cuda)
+    X0 = Xt.clone()
+    e.mix_rounds_trace(W, Xt, Yt, K, trace, tiled=(P, T))
+    torch.cuda.synchronize()
+    assert torch.equal(Xt, X0)
+    del X0
+    Y = e.from_tiled(Yt, P)
+    for c0, c1 in [(0, 2048), (P - 2048, P), (500001, 500001 + 771)]:
+        Z = X[:, c0:c1].cpu().numpy()
+        for _ in range(K):
+            Z = cref.mix_round(Z, csr.rowptr, csr.col, csr.w)
+        assert np.array_equal(bits(Y[:, c0:c1].cpu().numpy()), bits(Z)), (c0, c1)
+    # the same 24 rounds one launch each, with the single-round kernel's fused deviation
+    eng = e.GossipEngine(csr, P, device=cuda, X=X)
+    ref = []
+    for _ in range(K):
+        eng.round(deviation=True)
+        ref.append(float(eng.dev_max.item()))
+    assert torch.equal(eng.rows(), Y)
+    floor = 8 * np.sqrt(P) * np.finfo(np.float32).eps * float(X.mean(0).abs().max())
+    np.testing.assert_allclose(trace.cpu().numpy(), ref, rtol=1e-5, atol=floor)

@@ -43,8 +43,14 @@ __device__ __forceinline__ const float4 *mm_at(const void *base, uint32_t off) {
 // registers for the whole launch, so a round issues only the RE neighbour reads and one write
 // per output chunk (no CSR reads from LDS).  RE = 0: CSR from LDS.
 // FAST tiles only (every tile full and 16-byte aligned; the column-tiled layout always is).
-template <int C, int KV, bool SGD, bool DEV, int RE>
+// MODE 1 / 2: N == KV * SLOTS (every slot an agent): the image fill and the output stores carry
+// no ragged guard and the store kind is fixed (1 plain, 2 non-temporal).  With guarded stores or
+// a run-time store-kind branch, the compiler's wait-count tracking could not count the stores
+// issued after the prefetch and waited for the previous tile's stores to drain (vmcnt(0))
+// before the image fill of every tile.  MODE 0: guarded, store kind from a.nt_store.
+template <int C, int KV, bool SGD, bool DEV, int RE, int MODE>
 __global__ void __launch_bounds__(kTileThreads) mix_multi_kernel(TileArgs a, int rounds) {
+    constexpr bool FULL = MODE > 0;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int NT = kTileThreads;
     constexpr int SLOTS = NT / C;
@@ -85,7 +91,7 @@ __global__ void __launch_bounds__(kTileThreads) mix_multi_kernel(TileArgs a, int
         const char *gt = SGD ? tile_base(a.g, a.gts, tile_id) : nullptr;
 #pragma unroll
         for (int k = 0; k < KV; ++k) {
-            const bool ok = s + k * SLOTS < Nr;   // ragged last pass re-reads row 0 (L1 hit)
+            const bool ok = FULL || s + k * SLOTS < Nr;   // ragged: re-read row 0 (L1 hit)
             px[k] = mm_nt_load4(mm_at(xt, ok ? ox + k * sx : 16u * c));
             if (SGD) pg[k] = mm_nt_load4(mm_at(gt, ok ? og + k * sg : 16u * c));
         }
@@ -122,7 +128,7 @@ __global__ void __launch_bounds__(kTileThreads) mix_multi_kernel(TileArgs a, int
         for (int e = 0; e < RE; ++e) wreg[e] = a.w[e];
 #pragma unroll
         for (int k = 0; k < KV; ++k) {
-            const int ag = s + k * SLOTS < Nr ? s + k * SLOTS : 0;
+            const int ag = FULL || s + k * SLOTS < Nr ? s + k * SLOTS : 0;
 #pragma unroll
             for (int e = 0; e < RE; ++e)
                 coff[k][e] = ((uint32_t)a.col[ag * RE + e] * C + c) * 16u;
@@ -152,11 +158,13 @@ __global__ void __launch_bounds__(kTileThreads) mix_multi_kernel(TileArgs a, int
 #pragma unroll
     for (int k = 0; k < ND; ++k) dacc[k] = 0.f;
 
+    // The tile loop is rotated: stage (image fill + column mean) of the next tile runs after
+    // this tile's output stores, and its prefetch is issued right after, so every path into
+    // the fill has the same loads-then-stores order and the fill waits only for the loads
+    // (vmcnt(4..7) rather than vmcnt(0), which also drained the previous tile's stores).
     int tile_id = blockIdx.x;
-    if (tile_id < a.n_tiles) prefetch(tile_id);
-    for (; tile_id < a.n_tiles; tile_id += gridDim.x) {
-        asm volatile("" : "+v"(ox), "+v"(og), "+v"(oy));
-        const int nxt = tile_id + gridDim.x;
+    float4 mean = mm_zero4();
+    auto stage = [&]() {
         float4 cst = mm_zero4();
 #pragma unroll
         for (int k = 0; k < KV; ++k) {
@@ -168,7 +176,7 @@ __global__ void __launch_bounds__(kTileThreads) mix_multi_kernel(TileArgs a, int
                 t.z = t.z - a.lr * pg[k].z;
                 t.w = t.w - a.lr * pg[k].w;
             }
-            if (r < Nr) {
+            if (FULL || r < Nr) {
                 img0[r * C + c] = t;
                 if (DEV) {
                     cst.x += t.x;
@@ -189,7 +197,7 @@ __global__ void __launch_bounds__(kTileThreads) mix_multi_kernel(TileArgs a, int
             if ((tid & 63) < C) scratch[(tid >> 6) * C + (tid & 63)] = cst;
         }
         __syncthreads();
-        float4 mean = mm_zero4();
+        mean = mm_zero4();
         if (DEV) {
 #pragma unroll 2   // (fully unrolled, the 16 reads are hoisted: 64 VGPRs at once, spills)
             for (int wv = 0; wv < NT / 64; ++wv) {
@@ -205,14 +213,25 @@ __global__ void __launch_bounds__(kTileThreads) mix_multi_kernel(TileArgs a, int
             mean.z = mean.z / n;
             mean.w = mean.w / n;
         }
-        if (nxt < a.n_tiles) prefetch(nxt);   // lands while this tile's rounds run in LDS
+    };
+    // prefetches past the last tile re-read the last tile instead (unconditional loads keep the
+    // count exact; 64 KB per workgroup per pass)
+    const int last = a.n_tiles - 1;
+    if (tile_id < a.n_tiles) {
+        prefetch(tile_id);
+        stage();
+        prefetch(min(tile_id + (int)gridDim.x, last));
+    }
+    for (; tile_id < a.n_tiles; tile_id += gridDim.x) {
+        asm volatile("" : "+v"(ox), "+v"(og), "+v"(oy));
+        const int nxt = min(tile_id + (int)gridDim.x, last);
         const float4 *src = img0;
         float4 *dst = img1;
         for (int r = 0; r + 1 < rounds; ++r) {
 #pragma unroll
             for (int k = 0; k < KV; ++k) {
                 const int ag = s + k * SLOTS;
-                if (ag < Nr) dst[ag * C + c] = out_row(src, k, ag);
+                if (FULL || ag < Nr) dst[ag * C + c] = out_row(src, k, ag);
                 // one output row at a time: keeps the RE neighbour reads of the next row from
                 // being hoisted above this one's (register pressure at 1024 threads)
                 __builtin_amdgcn_sched_barrier(0);
@@ -226,10 +245,10 @@ __global__ void __launch_bounds__(kTileThreads) mix_multi_kernel(TileArgs a, int
 #pragma unroll
         for (int k = 0; k < KV; ++k) {
             const int ag = s + k * SLOTS;
-            if (ag < Nr) {
+            if (FULL || ag < Nr) {
                 const float4 y = out_row(src, k, ag);
                 float4 *py = const_cast<float4 *>(mm_at(yt, oy + (uint32_t)k * sy));
-                if (a.nt_store)
+                if (MODE == 2 || (MODE == 0 && a.nt_store))
                     mm_nt_store4(y, py);
                 else
                     *py = y;
@@ -251,6 +270,8 @@ __global__ void __launch_bounds__(kTileThreads) mix_multi_kernel(TileArgs a, int
             *reinterpret_cast<float4 *>(a.mean + col0) = mean;
         }
         __syncthreads();   // both images and the scratch are rewritten by the next tile
+        stage();   // the next tile (past the end: a re-read of the last one, then unused)
+        prefetch(min(nxt + (int)gridDim.x, last));   // lands while the next tile's rounds run
     }
     if (DEV) {
 #pragma unroll
@@ -263,14 +284,23 @@ __global__ void __launch_bounds__(kTileThreads) mix_multi_kernel(TileArgs a, int
     }
 }
 
-template <int C, int KV, bool SGD, bool DEV, int RE>
-hipError_t launch_one(const TileArgs &a, int rounds, int grid, int lds, hipStream_t s) {
-    const void *k = reinterpret_cast<const void *>(mix_multi_kernel<C, KV, SGD, DEV, RE>);
+template <int C, int KV, bool SGD, bool DEV, int RE, int MODE>
+hipError_t launch_mode(const TileArgs &a, int rounds, int grid, int lds, hipStream_t s) {
+    const void *k = reinterpret_cast<const void *>(mix_multi_kernel<C, KV, SGD, DEV, RE, MODE>);
     hipError_t e = allow_full_lds(k);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((mix_multi_kernel<C, KV, SGD, DEV, RE>), dim3(grid), dim3(kTileThreads),
-                       lds, s, a, rounds);
+    hipLaunchKernelGGL((mix_multi_kernel<C, KV, SGD, DEV, RE, MODE>), dim3(grid),
+                       dim3(kTileThreads), lds, s, a, rounds);
     return hipGetLastError();
+}
+
+template <int C, int KV, bool SGD, bool DEV, int RE>
+hipError_t launch_one(const TileArgs &a, int rounds, int grid, int lds, hipStream_t s) {
+    // the unguarded variant for the register-CSR graphs whose N fills every slot (c2, c4)
+    if (RE > 0 && a.n_rows == KV * (kTileThreads / C))
+        return a.nt_store ? launch_mode<C, KV, SGD, DEV, RE, RE ? 2 : 0>(a, rounds, grid, lds, s)
+                          : launch_mode<C, KV, SGD, DEV, RE, RE ? 1 : 0>(a, rounds, grid, lds, s);
+    return launch_mode<C, KV, SGD, DEV, RE, 0>(a, rounds, grid, lds, s);
 }
 
 template <int C, int KV, int RE>
@@ -288,8 +318,10 @@ hipError_t launch_kv(const TileArgs &a, int rounds, bool sgd, bool dev, int grid
                      hipStream_t s) {
     // register-cached CSR for the degree-4 regular graphs with shared weights (c2, c4 shapes);
     // the same test as csr_in_registers() on the host, which then reserves no LDS for the CSR
-    if (a.regular == 5 && a.n_w == 5 && KV <= 4)
-        return launch_re<C, KV, 5>(a, rounds, sgd, dev, grid, lds, s);
+    if constexpr (KV <= 4) {
+        if (a.regular == 5 && a.n_w == 5)
+            return launch_re<C, KV, 5>(a, rounds, sgd, dev, grid, lds, s);
+    }
     return launch_re<C, KV, 0>(a, rounds, sgd, dev, grid, lds, s);
 }
 

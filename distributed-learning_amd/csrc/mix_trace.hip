@@ -234,7 +234,13 @@ __global__ void __launch_bounds__(kTileThreads) mix_trace_kernel(TileArgs a, int
 // graph of 1024 agents reaches 51 extra cycles per round-tile, against 335 x 4 planes for the
 // chunk-major images at their best order).  Per round the 4 chunk lanes of an agent add their
 // squared deviations with two quad shuffles; lane c keeps agent s + c * 256's trace in dacc.
-template <int KV, int KR>
+//
+// The pass's last round (the one that stores Y) is peeled out of the round loop and FULL
+// (N == KV * SLOTS, every slot an agent) drops the ragged guards: with the image fill and the
+// output stores conditional, the compiler's wait-count tracking could not count the stores
+// issued after the prefetch, so each tile waited for the previous tile's output stores to drain
+// (vmcnt(0)) before filling the image and issuing the next prefetch (≈1.3 ms per pass at c2).
+template <int KV, int KR, bool FULL>
 __global__ void __launch_bounds__(kTileThreads) mix_trace_rows_kernel(TileArgs a, int rounds) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int C = 4, RE = 5;
@@ -252,7 +258,7 @@ __global__ void __launch_bounds__(kTileThreads) mix_trace_rows_kernel(TileArgs a
     for (int e = 0; e < RE; ++e) wreg[e] = a.w[e];
 #pragma unroll
     for (int k = 0; k < KV; ++k) {
-        const int ag = s + k * SLOTS < N ? s + k * SLOTS : 0;
+        const int ag = FULL || s + k * SLOTS < N ? s + k * SLOTS : 0;
 #pragma unroll
         for (int e = 0; e < RE; ++e) coff[k][e] = ((uint32_t)a.col[ag * RE + e] * C + c) * 16u;
     }
@@ -278,11 +284,12 @@ __global__ void __launch_bounds__(kTileThreads) mix_trace_rows_kernel(TileArgs a
     float dacc[KR];
 #pragma unroll
     for (int r = 0; r < KR; ++r) dacc[r] = 0.f;
+    float dlast = 0.f;   // the last round's (dacc[rounds - 1] stays 0)
     float4 px[KV];
     auto prefetch = [&](int64_t q) {
 #pragma unroll
         for (int k = 0; k < KV; ++k) {
-            const int ag = s + k * SLOTS < N ? s + k * SLOTS : 0;   // ragged: re-read row 0
+            const int ag = FULL || s + k * SLOTS < N ? s + k * SLOTS : 0;   // ragged: row 0
             px[k] = tr_load4(xb + off(a.xts, (int64_t)ag * a.xrs, q * C + c));
         }
     };
@@ -293,7 +300,7 @@ __global__ void __launch_bounds__(kTileThreads) mix_trace_rows_kernel(TileArgs a
 #pragma unroll
         for (int k = 0; k < KV; ++k) {
             const int ag = s + k * SLOTS;
-            if (ag < N) {
+            if (FULL || ag < N) {
                 img0[ag * C + c] = px[k];
                 cs.x += px[k].x;
                 cs.y += px[k].y;
@@ -325,41 +332,46 @@ __global__ void __launch_bounds__(kTileThreads) mix_trace_rows_kernel(TileArgs a
         if (q + gridDim.x < nsteps) prefetch(q + gridDim.x);   // lands during the rounds
         const float4 *src = img0;
         float4 *dst = img1;
+        // one round src -> dst (LDS) or, the pass's last, src -> Y; acc += this lane's agent's
+        // squared deviation
+        auto round = [&](bool last, float &acc) {
+            float own = 0.f;
 #pragma unroll
-        for (int r = 0; r < KR; ++r) {
-            if (r < rounds) {
-                float own = 0.f;
-#pragma unroll
-                for (int k = 0; k < KV; ++k) {
-                    const int ag = s + k * SLOTS;
-                    float v = 0.f;
-                    if (ag < N) {
-                        f32x2 lo, hi;
-                        mix(src, k, lo, hi);
-                        const float4 y = make_float4(lo.x, lo.y, hi.x, hi.y);
-                        if (r + 1 < rounds)
-                            dst[ag * C + c] = y;
-                        else
-                            tr_store4(y, yb + off(a.yts, (int64_t)ag * a.yrs, q * C + c));
-                        v = dev2(lo, hi, mlo, mhi);
-                    }
-                    v += quad_xor1(v);   // the agent's 4 chunk lanes (whole wave active)
-                    v += quad_xor2(v);
-                    own += k == c ? v : 0.f;
+            for (int k = 0; k < KV; ++k) {
+                const int ag = s + k * SLOTS;
+                float v = 0.f;
+                if (FULL || ag < N) {
+                    f32x2 lo, hi;
+                    mix(src, k, lo, hi);
+                    const float4 y = make_float4(lo.x, lo.y, hi.x, hi.y);
+                    if (!last)
+                        dst[ag * C + c] = y;
+                    else
+                        tr_store4(y, yb + off(a.yts, (int64_t)ag * a.yrs, q * C + c));
+                    v = dev2(lo, hi, mlo, mhi);
                 }
-                dacc[r] += own;
-                __syncthreads();   // dst complete before it is read; img0/scratch reuse
-                const float4 *t = src;
-                src = dst;
-                dst = const_cast<float4 *>(t);
+                v += quad_xor1(v);   // the agent's 4 chunk lanes (whole wave active)
+                v += quad_xor2(v);
+                own += k == c ? v : 0.f;
             }
-        }
+            acc += own;
+            __syncthreads();   // dst complete before it is read; img0/scratch reuse
+            const float4 *t = src;
+            src = dst;
+            dst = const_cast<float4 *>(t);
+        };
+#pragma unroll
+        for (int r = 0; r + 1 < KR; ++r)
+            if (r + 1 < rounds) round(false, dacc[r]);
+        round(true, dlast);
     }
     const int mine_ag = s + c * SLOTS;
-    if (c < KV && mine_ag < N) {
+    if (c < KV && (FULL || mine_ag < N)) {
 #pragma unroll
         for (int r = 0; r < KR; ++r)
-            if (r < rounds) a.dev_partial[((int64_t)blockIdx.x * rounds + r) * N + mine_ag] = dacc[r];
+            if (r < rounds)
+                a.dev_partial[((int64_t)blockIdx.x * rounds + r) * N + mine_ag] =
+                    r == rounds - 1 ? dlast : dacc[r];
     }
 }
 
@@ -406,6 +418,22 @@ hipError_t launch_rc(const TileArgs &a, int rounds, int grid, int lds, hipStream
     return hipGetLastError();
 }
 
+template <int KV, int KR>
+hipError_t launch_rows(const TileArgs &a, int rounds, int grid, int lds, hipStream_t s) {
+    const bool full = a.n_rows == KV * (kTileThreads / 4);
+    const void *k = full ? reinterpret_cast<const void *>(mix_trace_rows_kernel<KV, KR, true>)
+                         : reinterpret_cast<const void *>(mix_trace_rows_kernel<KV, KR, false>);
+    hipError_t e = allow_full_lds(k);
+    if (e != hipSuccess) return e;
+    if (full)
+        hipLaunchKernelGGL((mix_trace_rows_kernel<KV, KR, true>), dim3(grid), dim3(kTileThreads),
+                           lds, s, a, rounds);
+    else
+        hipLaunchKernelGGL((mix_trace_rows_kernel<KV, KR, false>), dim3(grid), dim3(kTileThreads),
+                           lds, s, a, rounds);
+    return hipGetLastError();
+}
+
 template <int RE>
 hipError_t launch_re(const TileArgs &a, int chunks, int rounds, int grid, int lds,
                      hipStream_t s) {
@@ -428,18 +456,12 @@ hipError_t launch_mix_trace(const TileArgs &a, int chunks, int rounds, int grid,
     if (trace_uses_rows(a.n_rows, in_regs, chunks)) {
         // agent-major rows (mix_trace_rows_kernel); DLAMD_TRACE_PLANES=1 keeps the chunk-major
         // planes for comparison
-        const void *k = a.n_rows <= 256   ? reinterpret_cast<const void *>(mix_trace_rows_kernel<1, kTraceRounds>)
-                        : a.n_rows <= 512 ? reinterpret_cast<const void *>(mix_trace_rows_kernel<2, kTraceRounds>)
-                                          : reinterpret_cast<const void *>(mix_trace_rows_kernel<4, kRowsTraceRounds>);
-        e = allow_full_lds(k);
-        if (e != hipSuccess) return e;
         if (a.n_rows <= 256)
-            hipLaunchKernelGGL((mix_trace_rows_kernel<1, kTraceRounds>), dim3(grid), dim3(kTileThreads), lds, s, a, rounds);
+            e = launch_rows<1, kTraceRounds>(a, rounds, grid, lds, s);
         else if (a.n_rows <= 512)
-            hipLaunchKernelGGL((mix_trace_rows_kernel<2, kTraceRounds>), dim3(grid), dim3(kTileThreads), lds, s, a, rounds);
+            e = launch_rows<2, kTraceRounds>(a, rounds, grid, lds, s);
         else
-            hipLaunchKernelGGL((mix_trace_rows_kernel<4, kRowsTraceRounds>), dim3(grid), dim3(kTileThreads), lds, s, a, rounds);
-        e = hipGetLastError();
+            e = launch_rows<4, kRowsTraceRounds>(a, rounds, grid, lds, s);
     } else {
         e = in_regs ? launch_re<5>(a, chunks, rounds, grid, lds, s)
                     : launch_re<0>(a, chunks, rounds, grid, lds, s);

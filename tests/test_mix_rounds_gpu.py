@@ -56,6 +56,40 @@ def test_k_rounds_equal_k_launches(cuda, n, P, deg, layout, sgd):
     assert np.array_equal(bits(a.rows().cpu().numpy()), bits(b.rows().cpu().numpy()))
 
 
+@pytest.mark.parametrize("n,P", [(1024, 2048), (4096, 512)])
+@pytest.mark.parametrize("nt", ["0", "1"])
+@pytest.mark.parametrize("dev", [False, True])
+def test_full_slot_variants_both_store_kinds(cuda, monkeypatch, n, P, nt, dev):
+    """N = KV * SLOTS on a degree-4 regular graph (c2's 1024 agents at 4 chunks, c4's 4096 at
+    1): the unguarded mix_multi_kernel instantiations (MODE 1 plain / 2 non-temporal stores,
+    chosen by DLAMD_NT_STORE here, by the output size in production) against K one-round
+    launches with the local step before the first round, and the fused final deviation."""
+    from distributed_learning_amd.graph import best_constant_weight, random_regular_edges, \
+        uniform_weights
+    monkeypatch.setenv("DLAMD_NT_STORE", nt)
+    E = engine()
+    edges = random_regular_edges(4, n, seed=n)
+    csr = uniform_weights(edges, best_constant_weight(edges))
+    assert csr.doubly_stochastic and csr.shared_row_weights
+    rng = np.random.default_rng(n + int(nt))
+    X = rng.standard_normal((n, P), dtype=np.float32)
+    G = rng.standard_normal((n, P), dtype=np.float32)
+    a = E.GossipEngine(csr, P, device=cuda, X=torch.from_numpy(X).to(cuda), layout="tiled")
+    b = E.GossipEngine(csr, P, device=cuda, X=torch.from_numpy(X).to(cuda), layout="tiled")
+    Ga = a.layout_like(torch.from_numpy(G).to(cuda))
+    assert E.rounds_plan(a.W, a.X, a.Y, tiled=(a.P, a.T)) is not None
+    K = 6
+    mean = torch.empty(P, device=cuda)
+    a.rounds(K, G=Ga, lr=0.01, deviation=dev, mean=mean if dev else None)
+    for i in range(K):
+        b.round(G=Ga if i == 0 else None, lr=0.01 if i == 0 else 0.0)
+    torch.cuda.synchronize()
+    Y = a.rows().cpu().numpy()
+    assert np.array_equal(bits(Y), bits(b.rows().cpu().numpy()))
+    if dev:
+        check_dev(Y, a.dev_sq.cpu().numpy(), float(a.dev_max.item()), mean.cpu().numpy())
+
+
 @pytest.mark.parametrize("layout", ["tiled", "rows"])
 def test_final_deviation_doubly_stochastic(cuda, layout):
     from distributed_learning_amd.graph import best_constant_weight, random_regular_edges, \

@@ -54,9 +54,11 @@ def noise_floor(X):
 
 
 # rr4 rows run mix_trace_rows_kernel (4 / 2 / 1 agents per thread at 1024 / 300 / 64 agents,
-# ragged at 300); metropolis rows (irregular) the chunk-major planes kernel
+# ragged at 300; 256, 512 and 1024 agents fill every slot: the unguarded FULL instantiations);
+# metropolis rows (irregular) the chunk-major planes kernel
 CASES = [("rr4", 64, 4096, 0), ("rr4", 1024, 256, 1), ("metro", 50, 1000, 2),
-         ("metro", 7, 4, 3), ("rr4", 16, 65536, 4), ("rr4", 300, 512, 5), ("rr4", 1000, 128, 6)]
+         ("metro", 7, 4, 3), ("rr4", 16, 65536, 4), ("rr4", 300, 512, 5), ("rr4", 1000, 128, 6),
+         ("rr4", 256, 1024, 7), ("rr4", 512, 512, 8)]
 
 
 def make(kind, n, seed):

@@ -1179,7 +1179,7 @@ def run_gossip(args, dev, rank, world):
                      "peak": LDS_PEAK_GBS, "unit": "GB/s",
                      "frac": lds_bytes / (launch_ms / 1e3) / 1e9 / LDS_PEAK_GBS,
                      "traffic": None,
-                     "kernel": ("mix_trace_kernel (+trace_reduce)" if args.trace else
+                     "kernel": ("mix_trace_rows_kernel (+trace_reduce)" if args.trace else
                                 "mix_multi_kernel (+dev_reduce)") + " per-step HIP-event time",
                      "bytes_per_launch": lds_bytes, "launch_ms": launch_ms,
                      "hbm_bytes_per_launch": hbm_bytes,

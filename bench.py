@@ -720,6 +720,7 @@ def run_c4(args, dev, rank, world):
                      "kernel": "per-round HIP-event time (rank 0 local work)",
                      "bytes_per_launch": bytes_per_round, "launch_ms": launch_ms},
         "xgmi": xgmi,
+        "dist": getattr(args, "dist_info", None),
         "overlap_schemes": schemes or None,
         "cpu_baseline": None,
     }
@@ -807,6 +808,7 @@ def run_c2halo(args, dev, rank, world):
                      "traffic": None, "kernel": "per-round HIP-event time (rank 0 local work)",
                      "bytes_per_launch": bytes_per_round, "launch_ms": launch_ms},
         "xgmi": _halo_xgmi(schemes, plan["overlap"], P, launch_ms) if world > 1 else None,
+        "dist": getattr(args, "dist_info", None),
         "overlap_schemes": schemes or None,
         "cpu_baseline": None,
     }
@@ -1191,12 +1193,14 @@ def run_gossip(args, dev, rank, world):
     print(json.dumps(rec), flush=True)
 
 
-def halo_probe(world, backend, steps=20, warmup=3, timeout_s=240, workload="c4"):
+def halo_probe(world, backend, steps=20, warmup=3, timeout_s=240, workload="c4",
+               stderr_lines=40):
     """The agent-partitioned path at this GPU count: bench --workload c4 (64 x 64 torus, 2-D
     blocks, boundary rows exchanged with RCCL send/recv over xGMI each round, overlapped with
     the mix of the previous column chunk) as a CHILD job on the same GPUs, after this job's own
     process group is gone.  It runs as a child under a time limit, so whatever it does, the c2
-    line is still printed.  Returns the child's figures (or its failure)."""
+    line is still printed.  Returns the child's figures, or its failure with the tail of its
+    stderr (``stderr_tail``)."""
     import signal
     import socket
     import subprocess
@@ -1213,24 +1217,58 @@ def halo_probe(world, backend, steps=20, warmup=3, timeout_s=240, workload="c4")
            os.path.join(ROOT, "bench.py"), "--workload", workload, "--gpus", str(world),
            "--steps", str(steps), "--warmup", str(warmup), "--dist-backend", backend]
     t0 = time.perf_counter()
-    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, env=env,
-                         start_new_session=True, text=True)
-    try:
-        out, _ = p.communicate(timeout=timeout_s)
-    except subprocess.TimeoutExpired:
-        os.killpg(p.pid, signal.SIGKILL)
-        p.wait()
-        return {"status": f"timeout after {timeout_s} s"}
-    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
-    if p.returncode != 0 or not lines:
-        return {"status": f"exit {p.returncode}"}
+    # the child's stderr goes to a file, so a failing or hung run leaves its traceback tail in
+    # this line (the driver's one multi-GPU chance is otherwise undiagnosable from the record)
+    import tempfile
+    with tempfile.TemporaryFile("w+") as errf:
+        p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=errf, env=env,
+                             start_new_session=True, text=True)
+        try:
+            out, _ = p.communicate(timeout=timeout_s)
+            status = None
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
+            out, _ = p.communicate()
+            status = f"timeout after {timeout_s} s"
+        errf.seek(0)
+        err = errf.read()
+    lines = [ln for ln in (out or "").splitlines() if ln.startswith("{")]
+    if status is None and (p.returncode != 0 or not lines):
+        status = f"exit {p.returncode}"
+    if status is not None:
+        errl = err.splitlines()
+        tail = errl[-stderr_lines:]
+        # torchrun ends with its own failure summary: keep the first rank traceback as well
+        tb = next((i for i, ln in enumerate(errl) if ln.startswith("Traceback")), None)
+        first_tb = "\n".join(errl[tb:tb + stderr_lines]) if tb is not None else ""
+        return {"status": status, "cmd": " ".join(cmd[2:]), "wall_s": time.perf_counter() - t0,
+                "stderr_first_traceback": first_tb[-6000:],
+                "stderr_tail": "\n".join(tail)[-6000:],
+                "stdout_tail": "\n".join((out or "").splitlines()[-5:])[-2000:]}
     r = json.loads(lines[-1])
     return {"status": "ok", "metric": r["metric"], "value": r["value"], "unit": r["unit"],
             "scaling": r["scaling"], "ms_per_step": r["ms_per_step"], "steps": r["steps"],
             "parallelism": r["config"]["parallelism"], "plan": r["config"]["plan"],
             "hbm": {k: r["roofline"][k] for k in ("achieved", "peak", "frac", "launch_ms")},
             "xgmi": r["xgmi"], "overlap_schemes": r.get("overlap_schemes"),
-            "partition_report": r.get("partition_report"), "wall_s": time.perf_counter() - t0}
+            "partition_report": r.get("partition_report"), "dist": r.get("dist"),
+            "wall_s": time.perf_counter() - t0}
+
+
+def dist_info(args, world):
+    """What the process group saw (for the driver's one multi-GPU record): backend, world size,
+    RCCL version, visible devices."""
+    info = {"world_size_env": world, "backend": args.dist_backend if world > 1 else None,
+            "visible_devices": torch.cuda.device_count()}
+    if world > 1:
+        import torch.distributed as dist
+        info["world_size_pg"] = dist.get_world_size()
+    try:
+        v = torch.cuda.nccl.version()
+        info["rccl_version"] = ".".join(map(str, v)) if isinstance(v, tuple) else str(v)
+    except Exception as e:   # noqa: BLE001 -- diagnostics only
+        info["rccl_version"] = f"unavailable ({type(e).__name__})"
+    return info
 
 
 def main():
@@ -1250,6 +1288,7 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(args.dist_backend)
+    args.dist_info = dist_info(args, world)
 
     if args.workload in ("c1", "c2-gossip", "c2-halo", "c3", "c4", "c4-gather", "c5"):
         {"c1": run_c1, "c2-gossip": run_gossip, "c2-halo": run_c2halo, "c3": run_c3,
@@ -1374,6 +1413,7 @@ def main():
             "cpu_baseline": cpu,
             "final_max_deviation": dev_max,
             "fdla_weights": fdla,
+            "dist": args.dist_info,
         }
     if world > 1:
         dist.barrier()

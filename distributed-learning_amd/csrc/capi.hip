@@ -867,7 +867,11 @@ int dl_mix_round(const dl_mix_args *args, void *workspace, size_t ws_bytes, dl_s
         return fail(DL_ERR_WORKSPACE, "dl_mix_round: deviation outputs need a 16-byte aligned "
                                       "workspace of dl_mix_workspace_bytes()");
     const bool sgd = args->g != nullptr;
-    if (pl.pub.path == 4 && !t.vec) {   // the register-CSR kernel is FAST-only: gather instead
+    if (pl.pub.path == 4 && !t.vec) {   // the register-CSR kernel is FAST-only
+        // the gather kernel reads row-major operands only: column-tiled ones are refused as on
+        // path 1, row-major ones take the gather path
+        if (t.tiled)
+            return fail(DL_ERR_INVALID, "dl_mix_round: tiled operands must be 16-byte aligned");
         pl.pub.path = 2;
     }
     if (pl.pub.path == 1 || pl.pub.path == 4) {

@@ -138,9 +138,11 @@ class DeviceIterates:
         a.sum_f32 = 1 if d and all(v.f32 for v in nbrs) else 0
         a.keep, a.eps, a.conv_eps = float(keep), float(eps), float(conv_eps)
         a.parity = self._parity
-        self._parity ^= 1
         _lib.check(self._lib.dl_async_update(ctypes.byref(a), ctypes.byref(self._verdict),
                                              self._stream()), "dl_async_update")
+        # flipped only once the step ran: a call refused by the argument checks launches no
+        # kernel, so the other parity's flag word was not zeroed for the next step
+        self._parity ^= 1
         self.updates += 1
         return Iterate(self, out, False, y.shape, y.scalar), bool(self._verdict.value)
 

@@ -166,6 +166,9 @@ class RankPlan:
     # [n_interior, n_local) boundary rows (they read halo rows).  -1: not in that order.
     n_deep: int = -1
     n_interior: int = -1
+    # every column of the GLOBAL W sums to 1 (taken from the global Csr in halo_plans): the
+    # lagged deviation's sum(W t) = sum(t) needs it, and one rank cannot see it from its rows
+    doubly_stochastic: bool = False
 
     @property
     def n_local(self):
@@ -239,7 +242,8 @@ def halo_plans(csr: Csr, parts):
                         n_src=len(p) + off)
         send_to = {q: pos[np.asarray(sorted(need[q][r]), np.int64)]
                    for q in range(world) if need[q][r]}
-        plans.append(RankPlan(r, np.asarray(p), local_csr, halo_from, send_to, halo_offset))
+        plans.append(RankPlan(r, np.asarray(p), local_csr, halo_from, send_to, halo_offset,
+                              doubly_stochastic=bool(csr.doubly_stochastic)))
     return plans
 
 
@@ -457,7 +461,7 @@ class HaloShard:
     """One rank's agent block with halo exchange (row-major X[n_local, P])."""
 
     def __init__(self, plan: RankPlan, n_params, device, transport, chunk_cols=None,
-                 n_agents_total=None, ops=None, doubly_stochastic=True, overlap="chunks"):
+                 n_agents_total=None, ops=None, doubly_stochastic=None, overlap="chunks"):
         """overlap="chunks": the columns are processed in chunks, the exchange of chunk j+1 in
         flight while chunk j is mixed.  overlap="split" (a boundary-last plan from
         split_halo_plans): ONE exchange of every column per round, in flight while the interior
@@ -487,9 +491,11 @@ class HaloShard:
         self.Y = staggered_zeros((plan.n_local, self.P), 1, self.device)
         self._bufs = {}
         self.mean_prev = None      # global column mean of X (lagged deviation), once known
-        # the lagged deviation needs sum(W t) = sum(t): W doubly stochastic over ALL agents
-        # (column sums of the global W are not visible to one rank; the caller states it)
-        self.doubly_stochastic = bool(doubly_stochastic)
+        # the lagged deviation needs sum(W t) = sum(t): W doubly stochastic over ALL agents.
+        # One rank cannot see the global column sums, so halo_plans records them on the plan;
+        # an explicit argument may only narrow that (False), never assert it.
+        ds = bool(plan.doubly_stochastic)
+        self.doubly_stochastic = ds if doubly_stochastic is None else (ds and bool(doubly_stochastic))
 
     def _buffers(self, slot, width):
         """Send/halo buffers of one pipeline slot; chunks alternate between two slots so the
@@ -541,6 +547,7 @@ class HaloShard:
         if deviation:
             if self.plan.n_halo == 0 or not self.doubly_stochastic:
                 dev = self.deviation()
+                self.mean_prev = None
                 self._mix_all(chunks, G, lr, None)
                 return dev
             if self.mean_prev is None:
@@ -554,6 +561,9 @@ class HaloShard:
         else:
             self._mix_all(chunks, G, lr, lag)
         if lag is None:
+            # a round that does not publish its column sums leaves mean_prev stale (the local
+            # step moved the mean): the next lagged round recomputes it
+            self.mean_prev = None
             return None
         dev_sq = parts.sum(0)
         self.transport.all_reduce_(colsum, "sum")
@@ -561,6 +571,11 @@ class HaloShard:
         dev_max = torch.sqrt(dev_sq.max()).reshape(1)
         self.transport.all_reduce_(dev_max, "max")
         return dev_sq, dev_max
+
+    def reset_deviation_lag(self):
+        """Forget the lagged mean.  Callers that write ``X`` directly (loading new parameters)
+        must call this before the next ``round(deviation=True)``."""
+        self.mean_prev = None
 
     def _mix_all(self, chunks, G, lr, lag):
         def post(j):

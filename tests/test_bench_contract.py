@@ -43,3 +43,20 @@ def test_driver_command_line_parses(bench, monkeypatch):
         monkeypatch.setattr("sys.argv", argv)
         p = bench.parse()
         assert p.gpus >= 1 and p.steps >= 1 and p.warmup >= 0
+
+
+def test_halo_probe_failure_carries_child_stderr(bench):
+    """A failing child run (here: 2 gloo ranks of bench --workload c4 on a host with no GPU, which
+    die in torch.cuda.set_device) comes back with its traceback tail in the record, so a failed
+    multi-GPU probe in the driver's one scaling run is diagnosable from the JSON line alone."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("needs a host without a GPU for the child to fail")
+    rec = bench.halo_probe(2, "gloo", steps=1, warmup=0, timeout_s=240)
+    assert rec["status"].startswith("exit"), rec
+    assert "Error" in rec["stderr_tail"], rec
+    # the rank's own traceback, not only torchrun's summary
+    assert rec["stderr_first_traceback"].startswith("Traceback"), rec
+    assert "set_device" in rec["stderr_first_traceback"] or "cuda" in \
+        rec["stderr_first_traceback"].lower(), rec
+    assert "bench.py" in rec["cmd"]

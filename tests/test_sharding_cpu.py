@@ -235,3 +235,58 @@ def test_lds_slot_order_native_matches_objective():
     with pytest.raises(ValueError, match="chunks"):
         _lib.check(lib.dl_lds_slot_order(2, 4, col.ctypes.data, 3, 10, 0, out.ctypes.data,
                                          conf.ctypes.data), "dl_lds_slot_order")
+
+
+def test_plan_records_global_doubly_stochastic():
+    """RankPlan.doubly_stochastic comes from the GLOBAL W (one rank's rows cannot show its column
+    sums); HaloShard takes it from the plan and an explicit True cannot override a False."""
+    from shard_oracle_ops import OracleOps
+    csr = torus_csr(4, 4)
+    parts = sharding.torus_block_partition(4, 4, 2)
+    assert all(p.doubly_stochastic for p in sharding.halo_plans(csr, parts))
+    w = csr.w.copy()
+    w[0] += 0.01            # row 0 / some column no longer sums to 1
+    bad = type(csr)(csr.rowptr, csr.col, w)
+    plans = sharding.halo_plans(bad, parts)
+    assert not any(p.doubly_stochastic for p in plans)
+    tr = sharding.LocalTransport(2)
+    sh = sharding.HaloShard(plans[0], 4, "cpu", tr.endpoint(0), n_agents_total=16,
+                            ops=OracleOps(), doubly_stochastic=True)
+    assert not sh.doubly_stochastic
+
+
+def test_lagged_mean_cleared_by_unlagged_rounds():
+    """A round without the lagged deviation (or a direct write of X) leaves no stale mean_prev:
+    the next lagged round returns the exact deviation of its input iterate."""
+    import threading
+    from shard_oracle_ops import OracleOps
+    csr = torus_csr(4, 4)
+    parts = sharding.torus_block_partition(4, 4, 2)
+    plans = sharding.halo_plans(csr, parts)
+    rng = np.random.default_rng(5)
+    P = 6
+    X = rng.standard_normal((16, P), dtype=np.float32)
+    G = rng.standard_normal((16, P), dtype=np.float32)
+    tr = sharding.LocalTransport(2)
+    out = {}
+
+    def run(r):
+        sh = sharding.HaloShard(plans[r], P, "cpu", tr.endpoint(r), n_agents_total=16,
+                                ops=OracleOps())
+        sh.X = torch.from_numpy(X[plans[r].local].copy())
+        Gl = torch.from_numpy(G[plans[r].local].copy())
+        sh.round(G=Gl, lr=0.1, deviation=True)      # sets mean_prev
+        assert sh.mean_prev is not None
+        sh.round(G=Gl, lr=0.1, deviation=False)     # moves the mean (local step)
+        assert sh.mean_prev is None
+        ref = sh.deviation()
+        got = sh.round(G=Gl, lr=0.1, deviation=True)
+        out[r] = (ref[0].numpy(), got[0].numpy(), float(ref[1]), float(got[1]))
+
+    ts = [threading.Thread(target=run, args=(r,)) for r in range(2)]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    for r in range(2):
+        ref_sq, got_sq, ref_max, got_max = out[r]
+        np.testing.assert_allclose(got_sq, ref_sq, rtol=1e-5)
+        assert abs(got_max - ref_max) <= 1e-5 * ref_max

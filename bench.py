@@ -57,8 +57,11 @@ def parse():
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--workload", default="c2",
-                   choices=["c1", "c2", "c2-mix", "c2-gossip", "c2-halo", "c3", "c4", "c4-gather",
+                   choices=["c1", "c2", "c2-mix", "c2-gossip", "c2-halo", "c3", "c4", "c4-gather", "c4-ba",
                             "c5"])
+    p.add_argument("--layout", default="auto", choices=["auto", "rows", "tiled"],
+                   help="c2-gossip: resident layout of X (rows = the Mixer drop-in's row-major "
+                        "flattened models)")
     p.add_argument("--graph", default="rr4", choices=["rr4", "circ4", "torus"],
                    help="c2-gossip: agent graph (circ4 = conflict-free control)")
     p.add_argument("--relabel", type=int, default=2_000_000,
@@ -495,10 +498,31 @@ def run_gather(args, dev, rank, world):
     (local step + mix + deviation) per step.  The per-entry CSR does not fit LDS beside a column
     tile of every agent, so the product path is the register-CSR tile kernel (plan path 4,
     column-tiled layout, fused deviation) -- ``value`` and ``roofline``.  The general gather
-    kernel (path 2: neighbour rows from L2/MALL, two-pass deviation), which irregular graphs of
-    this size still take, is timed on the same graph as ``gather`` (forced).  N>1: replicas."""
-    from distributed_learning_amd import engine
-    csr, n = per_edge_torus(64, 64)
+    kernel (path 2: neighbour rows from L2/MALL, two-pass deviation) is timed on the same graph
+    as ``gather`` (forced).  N>1: replicas.
+
+    ``--workload c4-ba``: the same on an IRREGULAR graph of the same size -- Barabasi-Albert
+    (m = 2, seed 1) with Metropolis weights, the reference-run fixture B's construction at 4096
+    agents (rows of 3 to 172 entries, 20,472 entries): plan path 5, each row's first 3 entries in
+    registers and the other 8,184 in LDS behind the tile."""
+    from distributed_learning_amd import engine, graph
+    if args.workload == "c4-ba":
+        csr = graph.barabasi_albert_metropolis(4096, 2, 1)
+        n = csr.n_rows
+        kname = "mix_tile_kernel<1, 4, true, true, true, false, true, 3, false, true>"
+        gname = ("c4-ba: Barabasi-Albert m=2 (seed 1), Metropolis weights, 4096 agents, fused "
+                 "local step + mix + deviation")
+        kdesc = "mix_tile_kernel register head + LDS tail (+dev_reduce), HIP-event time"
+        metric = "consensus rounds/sec, 4096 agents x 2^18 fp32 params, irregular graph"
+        prof_dir = os.path.join(ROOT, "profiles", "r10", "ba")
+    else:
+        csr, n = per_edge_torus(64, 64)
+        kname = "mix_tile_kernel<1, 4, true, true, true, false, true, 5>"
+        gname = ("c4-gather: 64x64 torus, per-edge weights (best constant x U[0.9, 1.1]), fused "
+                 "local step + mix + deviation")
+        kdesc = "mix_tile_kernel register-CSR (+dev_reduce), HIP-event time"
+        metric = "consensus rounds/sec, 4096 agents x 2^18 fp32 params, per-edge weights"
+        prof_dir = os.path.join(ROOT, "profiles", "r07", "peredge")
     P, lr = 1 << 18, 1e-3
     gen = torch.Generator(device=dev).manual_seed(1000 + rank)
     stream = torch.cuda.current_stream(dev)
@@ -536,29 +560,27 @@ def run_gather(args, dev, rank, world):
     g_mix = timed(lambda: engine.mix_round(W, X, Y, G=Gr, lr=lr, workspace=ws))
     del os.environ["DLAMD_FORCE_GATHER"]
     bytes_per_round = 12 * n * P
-    prof = os.path.join(ROOT, "profiles", "r07", "peredge", "summary.json")
-    traffic, src = traffic_from_profile("mix_tile_kernel<1, 4, true, true, true, false, true, 5>",
-                                        prof)
+    prof = os.path.join(prof_dir, "summary.json")
+    traffic, src = traffic_from_profile(kname, prof)
     g_traffic, g_src = traffic_from_profile("mix_gather_kernel", prof)
     achieved = bytes_per_round / (launch_ms / 1e3) / 1e9
     g_achieved = bytes_per_round / (g_mix[1] / 1e3) / 1e9
     if rank == 0:
         print(json.dumps({
-            "metric": "consensus rounds/sec, 4096 agents x 2^18 fp32 params, per-edge weights",
+            "metric": metric,
             "value": world * args.steps / elapsed, "unit": "rounds/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic X, G ~ N(0,1) resident in HBM",
-            "config": {"workload": "c4-gather: 64x64 torus, per-edge weights (best constant "
-                                   "x U[0.9, 1.1]), fused local step + mix + deviation",
-                       "agents": n, "params": P, "plan": plan,
+            "config": {"workload": gname, "agents": n, "params": P, "nnz": csr.nnz,
+                       "max_row_nnz": int(np.diff(csr.rowptr).max()), "plan": plan,
                        "parallelism": f"{world} independent replicas" if world > 1
                        else "single GPU"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_source": src,
-                         "kernel": "mix_tile_kernel register-CSR (+dev_reduce), HIP-event time",
+                         "kernel": kdesc, "kernel_instance": kname,
                          "bytes_per_launch": bytes_per_round, "launch_ms": launch_ms},
             "gather": {"plan": gplan, "rounds_per_s_with_deviation": 1e3 / g_round[1],
                        "round_ms_with_deviation": g_round[1], "mix_launch_ms": g_mix[1],
@@ -1096,7 +1118,7 @@ def run_gossip(args, dev, rank, world):
         conflicts = {"before": c0, "after": c1, "search_s": time.perf_counter() - t0}
         log(f"c2-gossip: LDS slot order, bank conflicts {c0} -> {c1}")
     eng = engine.GossipEngine(csr, P, device=dev, X=torch.randn(n, P, device=dev, generator=g),
-                              order=order)
+                              order=order, layout=args.layout)
     stream = torch.cuda.current_stream(dev)
     evs = event_pairs(args.steps, 2)
     if args.trace:
@@ -1106,7 +1128,8 @@ def run_gossip(args, dev, rank, world):
         if kmax < 1:
             raise SystemExit("c2-gossip --trace: the traced kernel does not fit this graph")
         K = min(K, kmax)
-        plan = {"kernel": "mix_trace_kernel", "max_rounds_per_pass": kmax}
+        plan = {"kernel": "mix_trace_wide_kernel" if n > 1024 else "mix_trace_rows_kernel",
+                "max_rounds_per_pass": kmax, "layout": eng.layout}
         trace = torch.empty(K, dtype=torch.float32, device=dev)
         last = []
 
@@ -1154,7 +1177,8 @@ def run_gossip(args, dev, rank, world):
     rounds_per_s = world * args.steps * K / elapsed
     rec = {
         "metric": "consensus rounds/sec, pure gossip averaging (Mixer.mix(times=K)), "
-                  "1024 agents x 1M fp32 params",
+                  + (f"1024 agents x 1M fp32 params" if (n, P) == (1024, 1 << 20)
+                     else f"{n} agents x {P} fp32 params"),
         "value": rounds_per_s,
         "unit": "rounds/s",
         "n_gpus": world,
@@ -1181,7 +1205,7 @@ def run_gossip(args, dev, rank, world):
                      "peak": LDS_PEAK_GBS, "unit": "GB/s",
                      "frac": lds_bytes / (launch_ms / 1e3) / 1e9 / LDS_PEAK_GBS,
                      "traffic": None,
-                     "kernel": ("mix_trace_rows_kernel (+trace_reduce)" if args.trace else
+                     "kernel": (f"{plan['kernel']} (+trace_reduce)" if args.trace else
                                 "mix_multi_kernel (+dev_reduce)") + " per-step HIP-event time",
                      "bytes_per_launch": lds_bytes, "launch_ms": launch_ms,
                      "hbm_bytes_per_launch": hbm_bytes,
@@ -1290,9 +1314,9 @@ def main():
             dist.init_process_group(args.dist_backend)
     args.dist_info = dist_info(args, world)
 
-    if args.workload in ("c1", "c2-gossip", "c2-halo", "c3", "c4", "c4-gather", "c5"):
+    if args.workload in ("c1", "c2-gossip", "c2-halo", "c3", "c4", "c4-gather", "c4-ba", "c5"):
         {"c1": run_c1, "c2-gossip": run_gossip, "c2-halo": run_c2halo, "c3": run_c3,
-         "c4": run_c4, "c4-gather": run_gather, "c5": run_c5}[args.workload](args, dev, rank,
+         "c4": run_c4, "c4-gather": run_gather, "c4-ba": run_gather, "c5": run_c5}[args.workload](args, dev, rank,
                                                                               world)
         if world > 1:
             dist.destroy_process_group()

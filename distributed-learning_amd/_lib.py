@@ -24,7 +24,7 @@ _i32, _i64, _f32, _f64, _sz = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ct
 class DlCsr(ctypes.Structure):
     _fields_ = [("row_ptr", _vp), ("col", _vp), ("w", _vp), ("n_rows", _i32), ("nnz", _i32),
                 ("uniform_row_nnz", _i32), ("doubly_stochastic", _i32),
-                ("shared_row_weights", _i32)]
+                ("shared_row_weights", _i32), ("min_row_nnz", _i32)]
 
 
 class DlMixArgs(ctypes.Structure):
@@ -110,6 +110,8 @@ SIGNATURES = {
     "dl_mix_plan_query": (_i32, [ctypes.POINTER(DlMixArgs), ctypes.POINTER(DlMixPlan)]),
     "dl_mix_plan_shape": (_i32, [_i32, _i32, _i64, _i32, _i32, _i32, _i32, _i32,
                                  ctypes.POINTER(DlMixPlan)]),
+    "dl_mix_plan_csr": (_i32, [ctypes.POINTER(DlCsr), _i32, _i64, _i32, _i32,
+                               ctypes.POINTER(DlMixPlan)]),
     "dl_mix_round": (_i32, [ctypes.POINTER(DlMixArgs), _vp, _sz, _vp]),
     "dl_mix_rounds_plan": (_i32, [ctypes.POINTER(DlMixArgs), ctypes.POINTER(DlMixPlan)]),
     "dl_mix_rounds_plan_shape": (_i32, [_i32, _i64, _i32, _i32, _i32, _i32, _i32, _i32,
@@ -142,7 +144,7 @@ SIGNATURES = {
     "dl_lds_slot_order": (_i32, [_i32, _i32, _vp, _i32, _i64, ctypes.c_uint64, _vp, _vp]),
 }
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 _lib = None
 
 

@@ -82,6 +82,7 @@ struct Plan {
     int chunks;
     bool dev;
     uint32_t csr_off, scratch_off;
+    int head;   // path 5: CSR entries per row in registers (the rest in LDS)
 };
 
 // Workgroups per CU the tile kernel may use (LDS permitting): 2 unless DLAMD_WG_PER_CU=1
@@ -114,27 +115,57 @@ int next_pow2_chunks(int64_t n_params) {
     return c;
 }
 
+// LDS bytes of the register-head + LDS-tail tile kernel (path 5) for R rows at c chunks, or 0
+// when it does not apply: the nnz - head * R tail entries (6 B each: fp32 weight, u16 row)
+// behind the tile and the mean scratch; the tail's u16 row map (setup only) must fit the tile
+// area.
+int64_t reg_tail_lds(const dl_csr &W, int32_t R, int c, bool want_dev, int *head_out) {
+    const int head = dl::reg_head_rows(W.min_row_nnz);
+    if (W.uniform_row_nnz == 5 || !dl::reg_tail_supported(c, R, head, 0)) return 0;
+    const int64_t ntail = (int64_t)W.nnz - (int64_t)head * R;
+    if (ntail < 0 || ntail > 65535) return 0;
+    const int64_t tile = (int64_t)R * c * 16;
+    const int64_t scratch = want_dev ? (int64_t)(dl::kTileThreads / 64) * c * 16 : 0;
+    const int64_t lds = tile + scratch + ((6 * ntail + 15) & ~(int64_t)15);
+    if (tile > 65536 || lds > dl::kLdsBytes || 2 * ntail > tile) return 0;
+    if (head_out) *head_out = head;
+    return lds;
+}
+
 // Tile width (float4 chunks) for the column-tiled layout: the widest power of two whose tile
 // of all R rows is <= 64 KiB and fits LDS beside the CSR.  Measured on MI355X:
 // 64-KiB tiles stream at 5.7-5.85 TB/s for N = 256..1024, 128-KiB tiles at 5.0-5.6 TB/s
 // depending on the box.  0 = no tiled configuration fits.
-int choose_tiled_chunks(int32_t R, uint32_t csr, bool want_dev, int32_t regular = 0) {
-    if (csr == 0 || R > 65535) return 0;
-    for (int c = dl::kMaxChunks; c >= 1; c >>= 1) {
-        if ((int64_t)R * c > (int64_t)dl::kRowsPerThread * dl::kTileThreads) continue;
-        const int64_t tile = (int64_t)R * c * 16;
-        if (tile > 65536 && c > 1) continue;
-        const int64_t scratch = want_dev ? (int64_t)(dl::kTileThreads / 64) * c * 16 : 0;
-        if (tile + csr + scratch <= dl::kLdsBytes) return c;
+// DLAMD_FORCE_REG=1 (tests only): the register-CSR kernels (paths 4 / 5) wherever they apply,
+// so the reference's small fixtures pin them too
+bool force_reg_env() {
+    const char *f = getenv("DLAMD_FORCE_REG");
+    const char *g = getenv("DLAMD_FORCE_GATHER");
+    return f && f[0] == '1' && !(g && g[0] == '1');
+}
+
+int choose_tiled_chunks(const dl_csr &W, int32_t R, uint32_t csr, bool want_dev) {
+    if (R > 65535) return 0;
+    const bool reg_any = dl::reg_csr_supported(1, R, W.uniform_row_nnz, 0) ||
+                         reg_tail_lds(W, R, 1, want_dev, nullptr) > 0;
+    if (force_reg_env() && reg_any) return 1;
+    if (csr > 0) {
+        for (int c = dl::kMaxChunks; c >= 1; c >>= 1) {
+            if ((int64_t)R * c > (int64_t)dl::kRowsPerThread * dl::kTileThreads) continue;
+            const int64_t tile = (int64_t)R * c * 16;
+            if (tile > 65536 && c > 1) continue;
+            const int64_t scratch = want_dev ? (int64_t)(dl::kTileThreads / 64) * c * 16 : 0;
+            if (tile + csr + scratch <= dl::kLdsBytes) return c;
+        }
     }
-    // the CSR does not fit beside any tile: the register-CSR kernel needs LDS for the tile only
-    for (int c = 1; c >= 1; c >>= 1) {
-        const int64_t tile = (int64_t)R * c * 16;
-        const int64_t scratch = want_dev ? (int64_t)(dl::kTileThreads / 64) * c * 16 : 0;
-        if (dl::reg_csr_supported(c, R, regular, 0) && tile <= 65536 &&
-            tile + scratch <= dl::kLdsBytes)
-            return c;
-    }
+    // the CSR does not fit beside any tile: the register-CSR kernels need LDS for the tile (and
+    // path 5 for the CSR entries past each row's register head)
+    const int64_t tile = (int64_t)R * 16;
+    const int64_t scratch = want_dev ? (int64_t)(dl::kTileThreads / 64) * 16 : 0;
+    if (dl::reg_csr_supported(1, R, W.uniform_row_nnz, 0) && tile <= 65536 &&
+        tile + scratch <= dl::kLdsBytes)
+        return 1;
+    if (reg_tail_lds(W, R, 1, want_dev, nullptr) > 0) return 1;
     return 0;
 }
 
@@ -143,29 +174,38 @@ inline int32_t local_src(const dl_mix_args *a) {
     return a->n_local_src > 0 ? a->n_local_src : a->W.n_rows;
 }
 
-// Register-CSR plan (path 4) for c chunks, or false when it does not apply.
+// Register-CSR plan for c chunks -- path 4 (regular, 5 entries per row, all in registers) or
+// path 5 (rows of >= min_row_nnz entries: register head + LDS tail) -- or false when neither
+// applies.
 bool plan_reg(const dl_mix_args *a, int c, bool want_dev, Plan *pl) {
     const int32_t R = a->W.n_rows;
-    if (a->n_halo > 0 || local_src(a) != R ||
-        !dl::reg_csr_supported(c, R, a->W.uniform_row_nnz, 0))
-        return false;
+    if (a->n_halo > 0 || local_src(a) != R) return false;
     const int64_t tile = (int64_t)R * c * 16;
     const int64_t scratch = want_dev ? (int64_t)(dl::kTileThreads / 64) * c * 16 : 0;
-    if (tile + scratch > dl::kLdsBytes) return false;
+    int head = 0;
+    int64_t lds = 0;
+    if (dl::reg_csr_supported(c, R, a->W.uniform_row_nnz, 0)) {
+        lds = tile + scratch;
+        if (lds > dl::kLdsBytes) return false;
+    } else {
+        lds = reg_tail_lds(a->W, R, c, want_dev, &head);
+        if (lds == 0) return false;
+    }
     const int64_t T = 4 * c;
     const int64_t n_tiles = (a->n_params + T - 1) / T;
     if (n_tiles > 0x7fffffff) return false;
-    int bpc = (int)(dl::kLdsBytes / (tile + scratch));
+    int bpc = (int)(dl::kLdsBytes / lds);
     if (bpc > wg_per_cu_cap()) bpc = wg_per_cu_cap();
-    pl->pub.path = 4;
+    pl->pub.path = head > 0 ? 5 : 4;
     pl->pub.tile_cols = (int32_t)T;
     pl->pub.grid = (int32_t)balanced_grid(
         n_tiles, (int64_t)device_cus() * bpc * (a->tile_cols > 0 ? grid_mult() : 1));
-    pl->pub.lds_bytes = (int32_t)(tile + scratch);
+    pl->pub.lds_bytes = (int32_t)lds;
     pl->pub.n_tiles = (int32_t)n_tiles;
-    pl->pub.regular = 1;
+    pl->pub.regular = head > 0 ? 0 : 1;
     pl->chunks = c;
-    pl->csr_off = (uint32_t)tile;
+    pl->head = head;
+    pl->csr_off = (uint32_t)(tile + scratch);   // path 5: the LDS tail
     pl->scratch_off = (uint32_t)tile;
     return true;
 }
@@ -187,15 +227,19 @@ int plan_mix(const dl_mix_args *a, Plan *pl) {
         const int m = atoi(mc);
         while (m >= 1 && cmax > m) cmax >>= 1;
     }
-    // DLAMD_FORCE_GATHER=1 (tests only) forces the general gather kernel
+    // DLAMD_FORCE_GATHER=1 (tests only) forces the general gather kernel; DLAMD_FORCE_REG=1
+    // (tests only) the register-CSR kernels (paths 4 / 5) wherever they apply, so the reference's
+    // small fixtures pin them too
     const char *force = getenv("DLAMD_FORCE_GATHER");
     const bool force_gather = force && force[0] == '1';
+    const bool force_reg = force_reg_env();
     if (a->tile_cols > 0) {  // column-tiled layout: the tile width is fixed by the data
         const int c = a->tile_cols / 4;
         const int64_t tile = (int64_t)R * c * 16;
         const int64_t scratch = want_dev ? (int64_t)(dl::kTileThreads / 64) * c * 16 : 0;
         const int64_t lds = tile + csr + scratch;
-        if ((csr == 0 || lds > dl::kLdsBytes) && R <= 65535 && plan_reg(a, c, want_dev, pl))
+        if ((csr == 0 || lds > dl::kLdsBytes || force_reg) && R <= 65535 &&
+            plan_reg(a, c, want_dev, pl))
             return DL_OK;
         if (csr == 0 || R > 65535 || (int64_t)R * c > (int64_t)dl::kRowsPerThread * dl::kTileThreads ||
             lds > dl::kLdsBytes)
@@ -222,6 +266,8 @@ int plan_mix(const dl_mix_args *a, Plan *pl) {
         pl->scratch_off = (uint32_t)(tile + csr);
         return DL_OK;
     }
+    if (force_reg && R <= 65535 && a->n_params % 4 == 0 && plan_reg(a, 1, want_dev, pl))
+        return DL_OK;
     if (csr > 0 && R <= 65535 && !force_gather) {
         for (int c = cmax; c >= 1; c >>= 1) {
             if ((int64_t)R * c > (int64_t)dl::kRowsPerThread * dl::kTileThreads) continue;
@@ -302,6 +348,8 @@ int check_mix_args(const dl_mix_args *a) {
         return fail(DL_ERR_INVALID, "dl_mix_round: uniform_row_nnz * n_rows != nnz");
     if (W.shared_row_weights && W.uniform_row_nnz <= 0)
         return fail(DL_ERR_INVALID, "dl_mix_round: shared_row_weights needs uniform_row_nnz > 0");
+    if (W.min_row_nnz < 0 || (int64_t)W.min_row_nnz * W.n_rows > W.nnz)
+        return fail(DL_ERR_INVALID, "dl_mix_round: min_row_nnz * n_rows > nnz");
     const bool halo_round = a->n_halo > 0 || part;
     if ((a->mean_prev || a->colsum_out) && !halo_round)
         return fail(DL_ERR_INVALID, "dl_mix_round: mean_prev / colsum_out are for halo rounds "
@@ -506,9 +554,11 @@ int plan_trace(const dl_mix_args *a, TracePlan *tp) {
                                         "doubly stochastic W (mean(W x) = mean(x))");
     if (a->g)
         return fail(DL_ERR_UNSUPPORTED, "dl_mix_rounds_trace: no local step (g must be NULL)");
-    if (N < 2 || N > dl::kTileThreads)
-        return fail(DL_ERR_UNSUPPORTED, "dl_mix_rounds_trace: needs 2..%d agents (one per "
-                                        "thread), got %d", dl::kTileThreads, N);
+    // one agent per thread up to 1024 agents; above, mix_trace_wide_kernel (one column chunk per
+    // step, up to 4 agents per thread; the CSR in registers above 2048 agents)
+    if (N < 2 || N > 4 * dl::kTileThreads)
+        return fail(DL_ERR_UNSUPPORTED, "dl_mix_rounds_trace: needs 2..%d agents, got %d",
+                    4 * dl::kTileThreads, N);
     if (a->n_params % 4)
         return fail(DL_ERR_UNSUPPORTED, "dl_mix_rounds_trace: n_params must be a multiple of 4");
     const int reg = a->W.uniform_row_nnz > 0 ? 1 : 0;
@@ -517,11 +567,16 @@ int plan_trace(const dl_mix_args *a, TracePlan *tp) {
     const uint32_t csr = in_regs ? 0u : dl::csr_lds_bytes(N, a->W.nnz, reg, n_w);
     if (!in_regs && csr == 0)
         return fail(DL_ERR_UNSUPPORTED, "dl_mix_rounds_trace: CSR too large");
+    const bool wide = N > dl::kTileThreads;
+    if (wide && !in_regs && N > 2 * dl::kTileThreads)
+        return fail(DL_ERR_UNSUPPORTED, "dl_mix_rounds_trace: above %d agents the traced pass "
+                                        "keeps the CSR in registers (regular degree-4 graphs with "
+                                        "shared weights)", 2 * dl::kTileThreads);
     const int64_t nq = a->n_params / 4;
     const int64_t lc = a->tile_cols > 0 ? a->tile_cols / 4 : 0;   // 0: row-major
     // widest chunk count whose two images fit LDS (a round then does C outputs per thread)
     tp->chunks = 0;
-    for (int c = 4; c >= 1; c >>= 1) {
+    for (int c = wide ? 1 : 4; c >= 1; c >>= 1) {
         const uint32_t img = 2u * (uint32_t)N * 16u * (uint32_t)c;
         const uint32_t scr = (uint32_t)align_up(img + csr);
         const uint32_t lds = scr + (dl::kTileThreads / 64) * 16u * (uint32_t)c;
@@ -812,33 +867,27 @@ int dl_mix_rounds_plan_shape(int32_t n_rows, int64_t n_params, int32_t nnz,
     return DL_OK;
 }
 
-int dl_mix_plan_shape(int32_t n_rows, int32_t n_halo, int64_t n_params, int32_t nnz,
-                      int32_t uniform_row_nnz, int32_t shared_row_weights, int32_t deviation,
-                      int32_t tile_cols, dl_mix_plan *plan) {
-    g_err.clear();
-    if (!plan || n_rows <= 0 || n_halo < 0 || n_params <= 0 || nnz < 0 || tile_cols < -1)
-        return fail(DL_ERR_INVALID, "dl_mix_plan_shape: bad arguments");
+namespace {
+int plan_from_csr(const dl_csr &W, int32_t n_halo, int64_t n_params, int32_t deviation,
+                  int32_t tile_cols, dl_mix_plan *plan, const char *who) {
+    if (!plan || W.n_rows <= 0 || n_halo < 0 || n_params <= 0 || W.nnz < 0 || tile_cols < -1 ||
+        W.min_row_nnz < 0)
+        return fail(DL_ERR_INVALID, "%s: bad arguments", who);
     dl_mix_args a{};
-    a.W.n_rows = n_rows;
-    a.W.nnz = nnz;
-    a.W.uniform_row_nnz = uniform_row_nnz;
-    a.W.shared_row_weights = uniform_row_nnz > 0 ? shared_row_weights : 0;
+    a.W = W;
+    a.W.shared_row_weights = W.uniform_row_nnz > 0 ? W.shared_row_weights : 0;
     a.n_halo = n_halo;
     a.n_params = n_params;
     float dummy;
     if (deviation) a.dev_max = &dummy;
     if (tile_cols == -1) {  // pick the column-tiled width (no halo rows in that layout)
-        const int reg = uniform_row_nnz > 0 ? 1 : 0;
-        const int32_t n_w = (reg && a.W.shared_row_weights) ? uniform_row_nnz : nnz;
-        const int c = n_halo == 0 ? choose_tiled_chunks(n_rows, dl::csr_lds_bytes(
-                                                                    n_rows, nnz, reg, n_w),
-                                                        deviation != 0, uniform_row_nnz)
+        const int reg = W.uniform_row_nnz > 0 ? 1 : 0;
+        const int32_t n_w = (reg && a.W.shared_row_weights) ? W.uniform_row_nnz : W.nnz;
+        const int c = n_halo == 0 ? choose_tiled_chunks(a.W, W.n_rows,
+                                                        dl::csr_lds_bytes(W.n_rows, W.nnz, reg, n_w),
+                                                        deviation != 0)
                                   : 0;
-        if (c == 0) {  // not tileable: report the row-major plan
-            tile_cols = 0;
-        } else {
-            tile_cols = 4 * c;
-        }
+        tile_cols = 4 * c;   // 0: not tileable, report the row-major plan
     }
     a.tile_cols = tile_cols;
     Plan pl;
@@ -846,6 +895,27 @@ int dl_mix_plan_shape(int32_t n_rows, int32_t n_halo, int64_t n_params, int32_t 
     if (rc) return rc;
     *plan = pl.pub;
     return DL_OK;
+}
+}  // namespace
+
+int dl_mix_plan_shape(int32_t n_rows, int32_t n_halo, int64_t n_params, int32_t nnz,
+                      int32_t uniform_row_nnz, int32_t shared_row_weights, int32_t deviation,
+                      int32_t tile_cols, dl_mix_plan *plan) {
+    g_err.clear();
+    dl_csr W{};
+    W.n_rows = n_rows;
+    W.nnz = nnz;
+    W.uniform_row_nnz = uniform_row_nnz;
+    W.shared_row_weights = shared_row_weights;
+    W.min_row_nnz = uniform_row_nnz > 0 ? uniform_row_nnz : 0;
+    return plan_from_csr(W, n_halo, n_params, deviation, tile_cols, plan, "dl_mix_plan_shape");
+}
+
+int dl_mix_plan_csr(const dl_csr *W, int32_t n_halo, int64_t n_params, int32_t deviation,
+                    int32_t tile_cols, dl_mix_plan *plan) {
+    g_err.clear();
+    if (!W) return fail(DL_ERR_INVALID, "dl_mix_plan_csr: W is NULL");
+    return plan_from_csr(*W, n_halo, n_params, deviation, tile_cols, plan, "dl_mix_plan_csr");
 }
 
 int dl_mix_round(const dl_mix_args *args, void *workspace, size_t ws_bytes, dl_stream_t stream) {
@@ -867,17 +937,17 @@ int dl_mix_round(const dl_mix_args *args, void *workspace, size_t ws_bytes, dl_s
         return fail(DL_ERR_WORKSPACE, "dl_mix_round: deviation outputs need a 16-byte aligned "
                                       "workspace of dl_mix_workspace_bytes()");
     const bool sgd = args->g != nullptr;
-    if (pl.pub.path == 4 && !t.vec) {   // the register-CSR kernel is FAST-only
+    if ((pl.pub.path == 4 || pl.pub.path == 5) && !t.vec) {   // register-CSR: FAST-only
         // the gather kernel reads row-major operands only: column-tiled ones are refused as on
         // path 1, row-major ones take the gather path
         if (t.tiled)
             return fail(DL_ERR_INVALID, "dl_mix_round: tiled operands must be 16-byte aligned");
         pl.pub.path = 2;
     }
-    if (pl.pub.path == 1 || pl.pub.path == 4) {
+    if (pl.pub.path == 1 || pl.pub.path == 4 || pl.pub.path == 5) {
         // full tiles on the branch-free float4 kernel, the ragged tail tile (and unaligned
         // operands) on the guarded one; each launch writes its own deviation partial rows
-        const bool reg_csr = pl.pub.path == 4;
+        const bool reg_csr = pl.pub.path == 4 || pl.pub.path == 5;
         const int64_t T = pl.pub.tile_cols;
         if (t.tiled) {
             if (!t.vec)
@@ -911,7 +981,7 @@ int dl_mix_round(const dl_mix_args *args, void *workspace, size_t ws_bytes, dl_s
             t.n_tiles = (int32_t)n_full;
             t.col_base = 0;
             t.dev_partial = partial;
-            hipError_t e = reg_csr ? dl::launch_mix_tile_reg(t, pl.chunks, sgd, pl.dev,
+            hipError_t e = reg_csr ? dl::launch_mix_tile_reg(t, pl.chunks, pl.head, sgd, pl.dev,
                                                              grid_full, lds, s)
                                    : dl::launch_mix_tile(t, pl.chunks, sgd, pl.dev, true,
                                                          grid_full, lds, true, s);

@@ -81,8 +81,13 @@ hipError_t launch_mix_gather(const TileArgs &a, bool sgd, hipStream_t s);
 // Tile kernel with the CSR in registers (regular graphs of 5 entries per row whose CSR does not
 // fit LDS beside the tile): FAST path only, no halo, chunks 1, <= 4 rows per thread.
 bool reg_csr_supported(int chunks, int n_rows, int regular, int n_halo);
-hipError_t launch_mix_tile_reg(const TileArgs &a, int chunks, bool sgd, bool dev, int grid,
-                               int lds, hipStream_t s);
+// ... and its irregular form: every row has >= min_row_nnz entries; the first reg_head_rows()
+// of each row in registers, the remaining nnz - head * n_rows entries in LDS (8 B each)
+int reg_head_rows(int min_row_nnz);   // 5, 3, 2 or 0 (no register head)
+bool reg_tail_supported(int chunks, int n_rows, int head, int n_halo);
+// head 0: the regular register-CSR kernel (path 4); head > 0: head + LDS tail (path 5)
+hipError_t launch_mix_tile_reg(const TileArgs &a, int chunks, int head, bool sgd, bool dev,
+                               int grid, int lds, hipStream_t s);
 // rows per thread (KV) the FAST tile kernels use for n_src rows at `chunks` float4 per row
 int tile_passes(int chunks, int n_src, bool fast);
 // K rounds of mixing on LDS-resident tiles (mix_multi.hip); FAST tiles only, no halo rows
@@ -94,6 +99,14 @@ constexpr int kTraceRounds = 32;   // rounds per traced pass (per-round deviatio
 // mix_trace_rows_kernel at 4 agents per thread keeps 4 agents' CSR offsets and prefetch
 // registers: its trace depth is capped so the per-round deviations fit VGPRs (122, no spills)
 constexpr int kRowsTraceRounds = 24;
+// mix_trace_wide_kernel (1024 < N <= 4096 agents, one chunk per step, KV = 2 or 4 agents per
+// thread) keeps every agent's per-round deviation of the pass in registers (KV x rounds VGPRs):
+// 16 rounds per pass at KV = 2, 8 at KV = 4 (12 spilled 20-30 VGPRs there)
+constexpr int kWideTraceRounds2 = 16;
+constexpr int kWideTraceRounds4 = 8;
+inline int wide_trace_rounds(int n_rows) {
+    return n_rows > 2 * kTileThreads ? kWideTraceRounds4 : kWideTraceRounds2;
+}
 // the agent-major traced kernel serves register-cached regular graphs at C = 4;
 // DLAMD_TRACE_PLANES=1 keeps the chunk-major planes kernel (comparison runs)
 inline bool trace_uses_rows(int n_rows, bool in_regs, int chunks) {
@@ -101,6 +114,7 @@ inline bool trace_uses_rows(int n_rows, bool in_regs, int chunks) {
            std::getenv("DLAMD_TRACE_PLANES") == nullptr;
 }
 inline int trace_max_rounds(int n_rows, bool in_regs, int chunks) {
+    if (n_rows > kTileThreads) return wide_trace_rounds(n_rows);
     return trace_uses_rows(n_rows, in_regs, chunks) && n_rows > kTileThreads / 2 ? kRowsTraceRounds
                                                                                   : kTraceRounds;
 }

@@ -126,8 +126,13 @@ __device__ __forceinline__ float4 *at(float *base, uint32_t off) {
 //        (the deviation of the previous round's iterate against its all-reduced global mean) and
 //        this rank's column sums of the stepped inputs t into colsum_out -- all-reduced over the
 //        ranks, the numerator of the next mean_prev (sum(W t) = sum(t): W doubly stochastic).
+// RAG  : (with RD > 0) an irregular graph whose every row has >= RD entries (dl_csr.min_row_nnz):
+//        each row's first RD entries in registers as above, the rest ("tail", nnz - RD*n_rows
+//        entries) staged once per workgroup in LDS behind the tile, fp32 weights then u16 row
+//        indices (6 B per entry); row r's tail is [rowptr[r] - RD*r, rowptr[r+1] - RD*(r+1)).  The fold runs the
+//        register head, then the tail, in CSR order: still the reference's left fold.
 template <int C, int KV, bool SGD, bool DEV, bool MIX, bool HALO, bool FAST, int RD = 0,
-          bool LAG = false>
+          bool LAG = false, bool RAG = false>
 __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float4 *tile = reinterpret_cast<float4 *>(smem);
@@ -153,19 +158,52 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
     constexpr int NRC = RD > 0 ? KV * RD : 1;
     float rw[NRC];
     uint32_t ri[(NRC + 1) / 2];
+    // RAG: per pass, this row's tail in LDS: start (low 16 bits) and length (high 16 bits)
+    uint32_t rdesc[RAG ? KV : 1];
+    const int ntail = RAG ? nnz - RD * Nr : 0;
+    float *ltw = reinterpret_cast<float *>(smem + a.csr_off);
+    uint16_t *ltc = reinterpret_cast<uint16_t *>(smem + a.csr_off + 4u * (uint32_t)ntail);
     if (RD > 0) {
 #pragma unroll
         for (int i = 0; i < (NRC + 1) / 2; ++i) ri[i] = 0u;
 #pragma unroll
         for (int k = 0; k < KV; ++k) {
             const int r = s + k * SLOTS;
+            const int rr = r < Nr ? r : 0;
+            const int e0 = RAG ? a.rowptr[rr] : rr * RD;
 #pragma unroll
             for (int e = 0; e < RD; ++e) {
                 const int j = k * RD + e;
-                const int idx = (r < Nr ? r : 0) * RD + e;
+                const int idx = e0 + e;
                 rw[j] = a.w[idx];
                 ri[j >> 1] |= ((uint32_t)a.col[idx] * C + c) << (16 * (j & 1));
             }
+            if (RAG) {
+                const int e1 = a.rowptr[rr + 1];
+                rdesc[k] = r < Nr ? (uint32_t)(e0 - RD * rr) | ((uint32_t)(e1 - e0 - RD) << 16)
+                                  : 0u;
+            }
+        }
+        if (RAG) {
+            // stage the tail: first a row id per tail slot (u16, in the tile area, which the
+            // first tile's staging overwrites only after the barrier below), then every thread
+            // copies tail slots t = tid, tid + NT, ... -- coalesced loads whatever the degrees
+            uint16_t *trow = reinterpret_cast<uint16_t *>(smem);
+#pragma unroll
+            for (int k = 0; k < KV; ++k) {
+                const uint32_t t0 = rdesc[k] & 0xffffu, tn = rdesc[k] >> 16;
+                for (uint32_t t = 0; t < tn; ++t) trow[t0 + t] = (uint16_t)(s + k * SLOTS);
+            }
+            __syncthreads();
+            for (int t = tid; t < ntail; t += NT) {
+                const int r = trow[t];
+                const int e = t + RD * (r + 1);
+                const float we = a.w[e];
+                const int ce = a.col[e];
+                ltw[t] = we;
+                ltc[t] = (uint16_t)(ce * C + c);
+            }
+            __syncthreads();
         }
     } else if (MIX) {
         for (int i = tid; i < a.n_w; i += NT) lw[i] = a.w[i];
@@ -297,6 +335,34 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
                 idx = k == kk ? ri[j >> 1] >> (16 * (j & 1)) : idx;
             }
             axpy4(acc, w, tile[idx & 0xffffu]);
+        }
+        if (RAG) {   // the row's entries past the register head, from LDS, in CSR order
+            uint32_t d = rdesc[0];
+#pragma unroll
+            for (int kk = 1; kk < (RAG ? KV : 1); ++kk) d = k == kk ? rdesc[kk] : d;
+            // TU entries per step with their reads issued first: a hub row's tail (169
+            // entries on the c4-ba graph) is one lane's serial chain, and read-then-fold per
+            // entry exposed two dependent LDS latencies each (4.5 ms per round, LDS-bound)
+            uint32_t t = d & 0xffffu;
+            const uint32_t t1 = t + (d >> 16);
+            // (one at a five-entry head: beside its 30 head registers even two per step spill
+            // 84 VGPRs in the local-step + deviation instantiation)
+            constexpr int TU = RD >= 5 ? 1 : 4;
+            if constexpr (TU > 1) for (; t + TU <= t1; t += TU) {
+                float w4[TU];
+                uint32_t c4[TU];
+#pragma unroll
+                for (int u = 0; u < TU; ++u) {
+                    w4[u] = ltw[t + u];
+                    c4[u] = ltc[t + u];
+                }
+                float4 v4[TU];
+#pragma unroll
+                for (int u = 0; u < TU; ++u) v4[u] = tile[c4[u]];
+#pragma unroll
+                for (int u = 0; u < TU; ++u) axpy4(acc, w4[u], v4[u]);
+            }
+            for (; t < t1; ++t) axpy4(acc, ltw[t], tile[ltc[t]]);
         }
         return acc;
     };
@@ -618,9 +684,9 @@ __global__ void __launch_bounds__(1024) stream_triad_tile_kernel(const float4 *_
 }
 
 template <int C, int KV, bool SGD, bool DEV, bool MIX, bool HALO, bool FAST, int RD = 0,
-          bool LAG = false>
+          bool LAG = false, bool RAG = false>
 hipError_t launch_one(const TileArgs &a, int grid, int lds, hipStream_t s) {
-    auto k = mix_tile_kernel<C, KV, SGD, DEV, MIX, HALO, FAST, RD, LAG>;
+    auto k = mix_tile_kernel<C, KV, SGD, DEV, MIX, HALO, FAST, RD, LAG, RAG>;
     hipError_t e = allow_full_lds(reinterpret_cast<const void *>(k));
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k, dim3(grid), dim3(kTileThreads), lds, s, a);
@@ -662,28 +728,54 @@ int tile_passes(int chunks, int n_src, bool fast) {
     return need <= 2 ? 2 : need <= 4 ? 4 : 8;
 }
 
-// Register-CSR tile kernels: regular graphs of 5 entries per row (degree 4 + self), FAST path,
-// no halo rows, C = 1 (T = 4 columns), KV in {2, 4} rows per thread, i.e. up to 4096 agents.
-// (C = 2 at KV = 4 spills; at KV = 2 -- 1024 agents -- the CSR always fits LDS.)
-template <int KV>
+// Register-CSR tile kernels, FAST path, no halo rows, C = 1 (T = 4 columns), KV in {2, 4} rows
+// per thread, i.e. up to 4096 agents.  (C = 2 at KV = 4 spills; at KV = 2 -- 1024 agents -- a
+// CSR that fits a 5-entry register head fits LDS too.)
+//   head == 0: regular graphs of 5 entries per row, the whole CSR in registers (path 4);
+//   head  > 0: rows of >= head entries, the first `head` in registers, the rest in LDS (path 5).
+template <int KV, int RD, bool RAG>
 hipError_t launch_reg_kv(const TileArgs &a, bool sgd, bool dev, int grid, int lds, hipStream_t s) {
     if (sgd)
-        return dev ? launch_one<1, KV, true, true, true, false, true, 5>(a, grid, lds, s)
-                   : launch_one<1, KV, true, false, true, false, true, 5>(a, grid, lds, s);
-    return dev ? launch_one<1, KV, false, true, true, false, true, 5>(a, grid, lds, s)
-               : launch_one<1, KV, false, false, true, false, true, 5>(a, grid, lds, s);
+        return dev ? launch_one<1, KV, true, true, true, false, true, RD, false, RAG>(a, grid, lds, s)
+                   : launch_one<1, KV, true, false, true, false, true, RD, false, RAG>(a, grid, lds, s);
+    return dev ? launch_one<1, KV, false, true, true, false, true, RD, false, RAG>(a, grid, lds, s)
+               : launch_one<1, KV, false, false, true, false, true, RD, false, RAG>(a, grid, lds, s);
+}
+
+template <int RD, bool RAG>
+hipError_t launch_reg(const TileArgs &a, bool sgd, bool dev, int grid, int lds, hipStream_t s) {
+    return tile_passes(1, a.n_src, true) <= 2 ? launch_reg_kv<2, RD, RAG>(a, sgd, dev, grid, lds, s)
+                                              : launch_reg_kv<4, RD, RAG>(a, sgd, dev, grid, lds, s);
 }
 
 bool reg_csr_supported(int chunks, int n_rows, int regular, int n_halo) {
     return regular == 5 && n_halo == 0 && chunks == 1 && tile_passes(chunks, n_rows, true) <= 4;
 }
 
-hipError_t launch_mix_tile_reg(const TileArgs &a, int chunks, bool sgd, bool dev, int grid,
-                               int lds, hipStream_t s) {
-    if (!reg_csr_supported(chunks, a.n_rows, a.regular, a.n_src - a.n_rows))
+int reg_head_rows(int min_row_nnz) {
+    return min_row_nnz >= 5 ? 5 : min_row_nnz >= 3 ? 3 : min_row_nnz >= 2 ? 2 : 0;
+}
+
+bool reg_tail_supported(int chunks, int n_rows, int head, int n_halo) {
+    return head > 0 && n_halo == 0 && chunks == 1 && tile_passes(chunks, n_rows, true) <= 4;
+}
+
+hipError_t launch_mix_tile_reg(const TileArgs &a, int chunks, int head, bool sgd, bool dev,
+                               int grid, int lds, hipStream_t s) {
+    if (head == 0) {
+        if (!reg_csr_supported(chunks, a.n_rows, a.regular, a.n_src - a.n_rows))
+            return hipErrorInvalidValue;
+        return launch_reg<5, false>(a, sgd, dev, grid, lds, s);
+    }
+    if (!reg_tail_supported(chunks, a.n_rows, head, a.n_src - a.n_rows) ||
+        a.nnz < head * a.n_rows)
         return hipErrorInvalidValue;
-    return tile_passes(chunks, a.n_src, true) <= 2 ? launch_reg_kv<2>(a, sgd, dev, grid, lds, s)
-                                                   : launch_reg_kv<4>(a, sgd, dev, grid, lds, s);
+    switch (head) {
+        case 5: return launch_reg<5, true>(a, sgd, dev, grid, lds, s);
+        case 3: return launch_reg<3, true>(a, sgd, dev, grid, lds, s);
+        case 2: return launch_reg<2, true>(a, sgd, dev, grid, lds, s);
+        default: return hipErrorInvalidValue;
+    }
 }
 
 hipError_t launch_mix_tile(const TileArgs &a, int chunks, bool sgd, bool dev, bool mix, int grid,

@@ -375,6 +375,177 @@ __global__ void __launch_bounds__(kTileThreads) mix_trace_rows_kernel(TileArgs a
     }
 }
 
+// Wide variant: 1024 < N <= 4096 agents (the c4 torus) at C = 1 (T = 4 columns per step), KV =
+// ceil(N / 1024) agents per thread (s + k * 1024), every lane its agents' only chunk.  Two images
+// of 4096 agents are 128 KiB, so the CSR stays in registers (RE = 5, shared weights, as in
+// mix_multi_kernel) or, for up to 2048 agents, in LDS (RE = 0).  The per-round squared
+// deviations of a thread's KV agents live in registers for the whole pass (dacc[KV][KR]), which
+// caps a pass at KR rounds; the last round, which stores Y, is peeled as in the rows kernel.
+template <int KV, int KR, int RE, bool FULL>
+__global__ void __launch_bounds__(kTileThreads) mix_trace_wide_kernel(TileArgs a, int rounds) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int SLOTS = kTileThreads;
+    const int tid = threadIdx.x;
+    const int s = tid;
+    const int N = a.n_rows;
+    float4 *img0 = reinterpret_cast<float4 *>(smem);
+    float4 *img1 = img0 + N;
+    float4 *scratch = reinterpret_cast<float4 *>(smem + a.scratch_off);   // [16]
+    float *lw = reinterpret_cast<float *>(smem + a.csr_off);
+    uint16_t *lcol = reinterpret_cast<uint16_t *>(smem + a.csr_off + 4u * (uint32_t)a.n_w);
+    uint16_t *lrp = lcol + a.nnz;
+    const int reg = a.regular;
+    const bool wshared = a.n_w != a.nnz;
+    if constexpr (RE == 0) {
+        for (int i = tid; i < a.n_w; i += kTileThreads) lw[i] = a.w[i];
+        for (int i = tid; i < a.nnz; i += kTileThreads) lcol[i] = (uint16_t)a.col[i];
+        if (!reg)
+            for (int i = tid; i <= N; i += kTileThreads) lrp[i] = (uint16_t)a.rowptr[i];
+    }
+    uint32_t coff[KV][RE > 0 ? RE : 1];
+    float wreg[RE > 0 ? RE : 1];
+    if constexpr (RE > 0) {
+#pragma unroll
+        for (int e = 0; e < RE; ++e) wreg[e] = a.w[e];
+#pragma unroll
+        for (int k = 0; k < KV; ++k) {
+            const int ag = FULL || s + k * SLOTS < N ? s + k * SLOTS : 0;
+#pragma unroll
+            for (int e = 0; e < RE; ++e) coff[k][e] = (uint32_t)a.col[ag * RE + e] * 16u;
+        }
+    }
+    // agent s + k * SLOTS's output from an image: left fold in CSR order from +0.0, as pairs
+    auto mix = [&](const float4 *src, int k, f32x2 &lo, f32x2 &hi) {
+        lo = f32x2{0.f, 0.f};
+        hi = f32x2{0.f, 0.f};
+        if constexpr (RE > 0) {
+            const char *base = reinterpret_cast<const char *>(src);
+            f32x4 v[RE];
+#pragma unroll
+            for (int e = 0; e < RE; ++e) v[e] = *reinterpret_cast<const f32x4 *>(base + coff[k][e]);
+#pragma unroll
+            for (int e = 0; e < RE; ++e) fold2(lo, hi, wreg[e], v[e]);
+        } else {
+            const int ag = s + k * SLOTS;
+            int e0, e1;
+            if (reg) {
+                e0 = ag * reg;
+                e1 = e0 + reg;
+            } else {
+                e0 = lrp[ag];
+                e1 = lrp[ag + 1];
+            }
+            const float *wr = wshared ? lw - e0 : lw;
+            const f32x4 *sv = reinterpret_cast<const f32x4 *>(src);
+            for (int e = e0; e < e1; ++e) fold2(lo, hi, wr[e], sv[lcol[e]]);
+        }
+    };
+    const int lsh = __builtin_ctz((unsigned)a.lchunks);
+    const int64_t lmask = (int64_t)a.lchunks - 1;
+    auto off = [&](int64_t ts, int64_t row, int64_t q) {
+        return (q >> lsh) * ts + row + (q & lmask) * 16;
+    };
+    const char *xb = reinterpret_cast<const char *>(a.x);
+    char *yb = reinterpret_cast<char *>(a.y);
+    const int64_t nsteps = a.n_tiles;
+    float dacc[KV][KR];
+#pragma unroll
+    for (int k = 0; k < KV; ++k)
+#pragma unroll
+        for (int r = 0; r < KR; ++r) dacc[k][r] = 0.f;
+    float dlast[KV];   // the last round's (dacc[.][rounds - 1] stays 0)
+#pragma unroll
+    for (int k = 0; k < KV; ++k) dlast[k] = 0.f;
+    float4 px[KV];
+    auto prefetch = [&](int64_t q) {
+#pragma unroll
+        for (int k = 0; k < KV; ++k) {
+            const int ag = FULL || s + k * SLOTS < N ? s + k * SLOTS : 0;   // ragged: row 0
+            px[k] = tr_load4(xb + off(a.xts, (int64_t)ag * a.xrs, q));
+        }
+    };
+    int64_t q = blockIdx.x;
+    if (q < nsteps) prefetch(q);
+    if (RE == 0) __syncthreads();   // CSR staged
+    for (; q < nsteps; q += gridDim.x) {
+        float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int k = 0; k < KV; ++k) {
+            const int ag = s + k * SLOTS;
+            if (FULL || ag < N) {
+                img0[ag] = px[k];
+                cs.x += px[k].x;
+                cs.y += px[k].y;
+                cs.z += px[k].z;
+                cs.w += px[k].w;
+            }
+        }
+#pragma unroll
+        for (int m = 1; m < 64; m <<= 1) {
+            cs.x += __shfl_xor(cs.x, m);
+            cs.y += __shfl_xor(cs.y, m);
+            cs.z += __shfl_xor(cs.z, m);
+            cs.w += __shfl_xor(cs.w, m);
+        }
+        if ((tid & 63) == 0) scratch[tid >> 6] = cs;
+        __syncthreads();
+        float4 mean = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 2
+        for (int wv = 0; wv < kTileThreads / 64; ++wv) {
+            const float4 p = scratch[wv];
+            mean.x += p.x;
+            mean.y += p.y;
+            mean.z += p.z;
+            mean.w += p.w;
+        }
+        const float n = (float)N;
+        mean = make_float4(mean.x / n, mean.y / n, mean.z / n, mean.w / n);
+        const f32x2 mlo = {mean.x, mean.y}, mhi = {mean.z, mean.w};
+        if (q + gridDim.x < nsteps) prefetch(q + gridDim.x);   // lands during the rounds
+        const float4 *src = img0;
+        float4 *dst = img1;
+        // one round src -> dst (LDS) or, the pass's last, src -> Y; acc[k] += agent k's squared
+        // deviation
+        auto round = [&](bool last, auto &&acc_of) {
+#pragma unroll
+            for (int k = 0; k < KV; ++k) {
+                const int ag = s + k * SLOTS;
+                if (FULL || ag < N) {
+                    f32x2 lo, hi;
+                    mix(src, k, lo, hi);
+                    const float4 y = make_float4(lo.x, lo.y, hi.x, hi.y);
+                    if (!last)
+                        dst[ag] = y;
+                    else
+                        tr_store4(y, yb + off(a.yts, (int64_t)ag * a.yrs, q));
+                    acc_of(k) += dev2(lo, hi, mlo, mhi);
+                }
+                // one output at a time (register pressure at 1024 threads, as mix_multi_kernel)
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            __syncthreads();   // dst complete before it is read; img0/scratch reuse
+            const float4 *t = src;
+            src = dst;
+            dst = const_cast<float4 *>(t);
+        };
+#pragma unroll
+        for (int r = 0; r + 1 < KR; ++r)
+            if (r + 1 < rounds) round(false, [&](int k) -> float & { return dacc[k][r]; });
+        round(true, [&](int k) -> float & { return dlast[k]; });
+    }
+#pragma unroll
+    for (int k = 0; k < KV; ++k) {
+        const int ag = s + k * SLOTS;
+        if (FULL || ag < N) {
+#pragma unroll
+            for (int r = 0; r < KR; ++r)
+                if (r < rounds)
+                    a.dev_partial[((int64_t)blockIdx.x * rounds + r) * N + ag] =
+                        r == rounds - 1 ? dlast[k] : dacc[k][r];
+        }
+    }
+}
+
 // out[r] = max_a sqrt(sum_b partial[b][r][a]) (fp64 sum in workgroup order, then float, as
 // dev_reduce's dev_sq); one workgroup per round.
 __global__ void __launch_bounds__(1024) trace_reduce_kernel(const float *__restrict__ partial,
@@ -445,6 +616,23 @@ hipError_t launch_re(const TileArgs &a, int chunks, int rounds, int grid, int ld
     }
 }
 
+template <int KV, int RE>
+hipError_t launch_wide(const TileArgs &a, int rounds, int grid, int lds, hipStream_t s) {
+    constexpr int KR = KV > 2 ? kWideTraceRounds4 : kWideTraceRounds2;
+    const bool full = a.n_rows == KV * kTileThreads;
+    const void *k = full ? reinterpret_cast<const void *>(mix_trace_wide_kernel<KV, KR, RE, true>)
+                         : reinterpret_cast<const void *>(mix_trace_wide_kernel<KV, KR, RE, false>);
+    hipError_t e = allow_full_lds(k);
+    if (e != hipSuccess) return e;
+    if (full)
+        hipLaunchKernelGGL((mix_trace_wide_kernel<KV, KR, RE, true>), dim3(grid),
+                           dim3(kTileThreads), lds, s, a, rounds);
+    else
+        hipLaunchKernelGGL((mix_trace_wide_kernel<KV, KR, RE, false>), dim3(grid),
+                           dim3(kTileThreads), lds, s, a, rounds);
+    return hipGetLastError();
+}
+
 }  // namespace
 
 hipError_t launch_mix_trace(const TileArgs &a, int chunks, int rounds, int grid, int lds,
@@ -453,7 +641,15 @@ hipError_t launch_mix_trace(const TileArgs &a, int chunks, int rounds, int grid,
     if (rounds < 1 || rounds > trace_max_rounds(a.n_rows, in_regs, chunks))
         return hipErrorInvalidValue;
     hipError_t e;
-    if (trace_uses_rows(a.n_rows, in_regs, chunks)) {
+    if (a.n_rows > kTileThreads) {   // the wide kernel: C = 1, KV agents per thread
+        if (chunks != 1 || a.lchunks < 1 || (!in_regs && a.n_rows > 2 * kTileThreads))
+            return hipErrorInvalidValue;
+        if (a.n_rows <= 2 * kTileThreads)
+            e = in_regs ? launch_wide<2, 5>(a, rounds, grid, lds, s)
+                        : launch_wide<2, 0>(a, rounds, grid, lds, s);
+        else
+            e = launch_wide<4, 5>(a, rounds, grid, lds, s);
+    } else if (trace_uses_rows(a.n_rows, in_regs, chunks)) {
         // agent-major rows (mix_trace_rows_kernel); DLAMD_TRACE_PLANES=1 keeps the chunk-major
         // planes for comparison
         if (a.n_rows <= 256)

@@ -34,11 +34,12 @@ class DeviceCsr:
         self.uniform_row_nnz = csr.uniform_row_nnz
         self.doubly_stochastic = int(csr.doubly_stochastic)
         self.shared_row_weights = int(csr.shared_row_weights)
+        self.min_row_nnz = csr.min_row_nnz
 
     def c_struct(self):
         return _lib.DlCsr(_lib.ptr(self.rowptr), _lib.ptr(self.col), _lib.ptr(self.w),
                           self.n_rows, self.nnz, self.uniform_row_nnz, self.doubly_stochastic,
-                          self.shared_row_weights)
+                          self.shared_row_weights, self.min_row_nnz)
 
 
 def _ld(t):
@@ -57,14 +58,15 @@ def _check(t, name, rows, cols, device):
 
 
 def plan_shape(W: DeviceCsr, n_params, deviation=True, tile_cols=0):
-    """dl_mix_plan_shape: the kernel configuration for these sizes (no tensors needed).
-    tile_cols: 0 row-major, > 0 column-tiled of that width, -1 choose the tiled width."""
+    """dl_mix_plan_csr: the kernel configuration for this graph's sizes and flags (no tensors
+    needed).  tile_cols: 0 row-major, > 0 column-tiled of that width, -1 choose the tiled width."""
     lib = _lib.load()
     plan = _lib.DlMixPlan()
-    _lib.check(lib.dl_mix_plan_shape(W.n_rows, W.n_src - W.n_rows, int(n_params), W.nnz,
-                                     W.uniform_row_nnz, W.shared_row_weights,
-                                     int(bool(deviation)), int(tile_cols), ctypes.byref(plan)),
-               "dl_mix_plan_shape")
+    w = _lib.DlCsr(None, None, None, W.n_rows, W.nnz, W.uniform_row_nnz, W.doubly_stochastic,
+                   W.shared_row_weights, W.min_row_nnz)   # sizes and flags only
+    _lib.check(lib.dl_mix_plan_csr(ctypes.byref(w), W.n_src - W.n_rows, int(n_params),
+                                   int(bool(deviation)), int(tile_cols), ctypes.byref(plan)),
+               "dl_mix_plan_csr")
     return {f: getattr(plan, f) for f, _ in plan._fields_}
 
 
@@ -421,14 +423,26 @@ class GossipEngine:
     """
 
     def __init__(self, csr: Csr, n_params, device="cuda", X=None, layout="auto", tile_cols=None,
-                 order=None):
+                 order="auto"):
         """order (optional, ``graph.lds_slot_order``): order[slot] = agent, the row order of the
         resident matrices.  ``load_rows`` / ``layout_like`` / ``rows`` take and return agent
-        order; ``dev_sq`` is per slot (``agent_dev_sq()`` in agent order)."""
+        order; ``dev_sq`` is per slot (``agent_dev_sq()`` in agent order).  "auto": the agents
+        by descending row length (``graph.row_length_order``) when the round runs the
+        register-head + LDS-tail kernel (plan path 5, irregular graphs of thousands of agents),
+        else agent order (None)."""
         self.device = torch.device(device)
         if self.device.type == "cuda" and self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
         self.order = None
+        if isinstance(order, str):
+            if order != "auto":
+                raise ValueError("order must be a permutation, None or 'auto'")
+            order = None
+            tc = 0 if layout == "rows" else (int(tile_cols) if tile_cols else -1)
+            if plan_shape(DeviceCsr(csr, self.device), int(n_params), deviation=True,
+                          tile_cols=tc)["path"] == 5:
+                from .graph import row_length_order
+                order = row_length_order(csr)
         if order is not None:
             from .graph import permuted
             order = np.asarray(order, np.int64)
@@ -440,7 +454,7 @@ class GossipEngine:
         self.n, self.P = csr.n_rows, int(n_params)
         plan = plan_shape(self.W, self.P, deviation=True,
                           tile_cols=int(tile_cols) if tile_cols else -1)
-        tiled_ok = plan["path"] in (1, 4) and plan["tile_cols"] >= 4 and self.W.n_src == self.n
+        tiled_ok = plan["path"] in (1, 4, 5) and plan["tile_cols"] >= 4 and self.W.n_src == self.n
         if layout == "auto":
             layout = "tiled" if tiled_ok else "rows"
         if layout == "tiled" and not tiled_ok:

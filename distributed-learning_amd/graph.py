@@ -61,6 +61,13 @@ class Csr:
         return int(d[0]) if len(d) and d[0] > 0 and np.all(d == d[0]) else 0
 
     @property
+    def min_row_nnz(self):
+        """Fewest entries of any row (dl_csr.min_row_nnz): a register head of that many entries
+        per row is exact for every row (plan path 5)."""
+        d = np.diff(self.rowptr)
+        return int(d.min()) if len(d) else 0
+
+    @property
     def shared_row_weights(self):
         """Regular graph whose rows all carry row 0's fp32 weight sequence (bit for bit)."""
         d = self.uniform_row_nnz
@@ -209,6 +216,26 @@ def random_regular_edges(d, n, seed):
     """Edge list of ``networkx.random_regular_graph(d, n, seed)`` (bench config c2)."""
     import networkx as nx
     return [(int(u), int(v)) for u, v in nx.random_regular_graph(d, n, seed=seed).edges()]
+
+
+def barabasi_albert_metropolis(n, m, seed):
+    """networkx.barabasi_albert_graph(n, m, seed) with Metropolis weights 1/(1 + max(d_i, d_j)),
+    each row's self weight first, then the neighbours in adjacency order -- the construction of
+    the reference-run fixture B (tests/golden/make_golden.py).  Irregular (hub rows of ~m*sqrt(n)
+    entries), symmetric, doubly stochastic."""
+    import networkx as nx
+    g = nx.barabasi_albert_graph(n, m, seed=seed)
+    deg = dict(g.degree())
+    rowptr, col, w = [0], [], []
+    for i in range(n):
+        nb = list(g.adj[i])
+        ws = [1.0 / (1.0 + max(deg[i], deg[j])) for j in nb]
+        col.append(i)
+        w.append(1.0 - sum(ws))
+        col.extend(nb)
+        w.extend(ws)
+        rowptr.append(len(col))
+    return Csr(rowptr, col, w, keys=list(range(n)))
 
 
 def torus_edges(rows, cols):
@@ -369,6 +396,15 @@ def lds_slot_order_native(csr, chunks, moves=4_000_000, seed=0):
     _lib.check(lib.dl_lds_slot_order(n, d, col.ctypes.data, int(chunks), int(moves), int(seed),
                                      order.ctypes.data, conf.ctypes.data), "dl_lds_slot_order")
     return order.astype(np.int64), int(conf[0]), int(conf[1])
+
+
+def row_length_order(csr):
+    """Agents by descending CSR row length (stable): order[slot] = agent.  The register-head +
+    LDS-tail tile kernel (plan path 5) mixes rows s + k * 1024 in lane s of pass k, and a wave
+    runs each pass for as long as its longest tail; with the rows in this order the 64 rows of a
+    wave-pass have similar lengths (Barabasi-Albert 4096 agents: 628 -> 271 tail steps per tile,
+    summed over wave-passes).  Every row keeps its entry order, so the bits do not change."""
+    return np.argsort(-np.diff(csr.rowptr), kind="stable")
 
 
 def permuted(csr, order):

@@ -10,7 +10,8 @@ trace of max deviations.  Otherwise each round is one
 ``dl_mix_round`` launch (the reference's ``_mix_params_once`` fold, :43-49, bit-identical in
 fp32), and when ``eps`` is given the same launch also produces the per-agent deviation
 (:51-66) so the stop test costs one 4-byte readback per round -- or, when the graph fits the
-traced multi-round kernel (<= 1024 agents, doubly stochastic W), K rounds run in one HBM pass
+traced multi-round kernel (<= 1024 agents, or up to 4096 of a register-cached regular graph;
+doubly stochastic W), K rounds run in one HBM pass
 that also returns their K per-round max deviations (``dl_mix_rounds_trace``), and the stop
 round is found on the host.  With ``eps=None`` the ``times``
 rounds have nothing in between, so they run as ONE ``dl_mix_rounds`` pass (every round on
@@ -159,6 +160,11 @@ class Mixer(object):
     # re-evaluated with the row-order two-pass deviation (dl_column_sum, as dl_mix_until does).
     _TIE_RTOL = 2e-5
 
+    # above this many agents the traced pass (mix_trace_wide_kernel: one 4-column chunk per step)
+    # runs on a column-tiled copy of X: a row-major step reads a 16-byte segment of every row
+    # (c4 torus, 4096 x 2^18: 486 rounds/s row-major against 2179 tiled, profiles/r10/trace4096)
+    _TRACE_TILED_ABOVE = 1024
+
     def _mix_traced(self, W, X, times, eps):
         """mixer.py:27-32 with eps set, in passes of K rounds (dl_mix_rounds_trace): each pass
         runs K rounds in one HBM pass and returns the K per-round max deviations, which are
@@ -167,12 +173,17 @@ class Mixer(object):
         row-order mean (``_TIE_RTOL``).  When the stop round falls inside a pass, that many
         rounds are re-run from the pass's input (left intact).  Returns (X, times_done,
         stopped); stopped is False, with nothing done, when the traced kernel does not fit (the
-        caller's round loop takes over)."""
+        caller's round loop takes over).  Above ``_TRACE_TILED_ABOVE`` agents the passes run on
+        a column-tiled copy of X (one conversion each way per call)."""
         P = X.shape[1]
         Pp = -(-P // 64) * 64
         cur = torch.nn.functional.pad(X, (0, Pp - P)) if Pp != P else X
+        tiled = None
+        if W.n_rows > self._TRACE_TILED_ABOVE:
+            tiled = (Pp, 4)
+            cur = _engine.to_tiled(cur, 4)
         nxt = torch.empty_like(cur)
-        K = min(_engine.trace_max_rounds(W, cur, nxt), self._TRACE_MAX_ROUNDS)
+        K = min(_engine.trace_max_rounds(W, cur, nxt, tiled=tiled), self._TRACE_MAX_ROUNDS)
         if K < min(self._TRACE_MIN_ROUNDS, self._TRACE_MAX_ROUNDS):
             return X, 0, False
         trace = torch.empty(K, dtype=torch.float32, device=X.device)
@@ -180,18 +191,18 @@ class Mixer(object):
         done = 0
         floor = None
         while True:
-            _engine.mix_rounds_trace(W, cur, nxt, K, trace, workspace=ws)
+            _engine.mix_rounds_trace(W, cur, nxt, K, trace, workspace=ws, tiled=tiled)
             stop_at = None
             for i, d in enumerate(trace.tolist()):
                 max_dev = np.float32(d)
                 gap = abs(float(max_dev) - float(eps))
                 if gap <= 0.1 * abs(float(eps)):
                     if floor is None:   # mean(W^k x) = mean(x): one column sum per call
-                        mean = _engine.column_sum(cur[:, :P]) / cur.shape[0]
+                        mean = _engine.column_sum(X) / X.shape[0]
                         floor = 8.0 * np.sqrt(P) * float(np.finfo(np.float32).eps) * \
                             float(mean.abs().max().item())
                     if gap <= self._TIE_RTOL * abs(float(eps)) + floor:
-                        max_dev = self._recheck_deviation(W, cur, i + 1, P)
+                        max_dev = self._recheck_deviation(W, cur, i + 1, P, tiled)
                 self.logger.debug('Mixer calculate max deviation= {}'.format(max_dev))
                 if max_dev < eps and done + i + 1 >= times:
                     stop_at = i + 1
@@ -201,24 +212,28 @@ class Mixer(object):
                 done += K
                 continue
             if stop_at < K:   # the same rounds again from the pass's input (bit-identical)
-                nxt = self._rounds_from(W, cur, stop_at, ws)
-            return nxt[:, :P], done + stop_at, True
+                nxt = self._rounds_from(W, cur, stop_at, ws, tiled)
+            out = _engine.from_tiled(nxt, Pp) if tiled else nxt
+            return out[:, :P], done + stop_at, True
 
-    def _rounds_from(self, W, src, k, ws):
+    def _rounds_from(self, W, src, k, ws, tiled=None):
         """The iterate k rounds after ``src`` (bit-identical to k single rounds), src intact."""
         out = torch.empty_like(src)
-        if _engine.mix_rounds(W, src, out, k, workspace=ws):
+        if _engine.mix_rounds(W, src, out, k, workspace=ws, tiled=tiled):
             return out
         bufs, a = (out, torch.empty_like(src)), src
         for j in range(k):
-            _engine.mix_round(W, a, bufs[j % 2], workspace=ws)
+            _engine.mix_round(W, a, bufs[j % 2], workspace=ws, tiled=tiled)
             a = bufs[j % 2]
         return a
 
-    def _recheck_deviation(self, W, src, k, P):
+    def _recheck_deviation(self, W, src, k, P, tiled=None):
         """max_a ||x_a - mean|| of the iterate k rounds after src, with numpy's row-order column
         mean (mixer.py:61: dl_column_sum, then the division in fp32)."""
-        Z = self._rounds_from(W, src, k, self._wspace())[:, :P]
+        Z = self._rounds_from(W, src, k, self._wspace(), tiled)
+        if tiled:
+            Z = _engine.from_tiled(Z, tiled[0])
+        Z = Z[:, :P]
         mean = _engine.column_sum(Z) / Z.shape[0]
         _, dmax = _engine.deviation(Z, mean_in=mean, workspace=self._wspace())
         return np.float32(dmax.item())

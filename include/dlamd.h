@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define DLAMD_ABI_VERSION 5
+#define DLAMD_ABI_VERSION 6
 
 typedef void *dl_stream_t; /* hipStream_t; NULL = the legacy default stream */
 
@@ -83,6 +83,15 @@ typedef struct dl_csr {
                                    regular graph).  The LDS kernel then stages d weights instead
                                    of nnz, which fits ~2x more agents per tile.  w is still the
                                    full [nnz] array.  0 = per-entry weights. */
+    int32_t min_row_nnz; /* (ABI 6) > 0 promises every row has at least this many entries (any
+                            graph with a self weight per row: >= 1; Barabasi-Albert m = 2 with
+                            self weights: 3).  When the CSR does not fit LDS beside a tile of all
+                            agents (thousands of agents, per-edge weights), the tile kernel then
+                            keeps each row's first min(min_row_nnz, 5) entries in registers and
+                            only the remaining nnz - head * n_rows entries in LDS (plan path 5)
+                            instead of taking the gather path.  Checked: min_row_nnz * n_rows <=
+                            nnz; a wrong promise gives wrong (never out-of-bounds) results.
+                            0 = unknown. */
 } dl_csr;
 
 typedef struct dl_mix_args {
@@ -135,7 +144,9 @@ typedef struct dl_mix_plan {
     int32_t path;       /* 1 = LDS tile kernel (all agents x T columns per tile), 2 = gather kernel,
                            3 = multi-round LDS kernel (dl_mix_rounds), 4 = tile kernel with the
                            CSR in registers (regular graphs of 5 entries per row whose CSR does
-                           not fit LDS beside the tile) */
+                           not fit LDS beside the tile), 5 = tile kernel with each row's first
+                           entries in registers and the rest in LDS (irregular graphs with
+                           W.min_row_nnz >= 2 whose CSR does not fit LDS beside the tile) */
     int32_t tile_cols;  /* T: columns per tile (path 1) */
     int32_t grid;       /* workgroups launched */
     int32_t lds_bytes;  /* dynamic LDS per workgroup */
@@ -154,6 +165,11 @@ size_t dl_mix_workspace_bytes(int32_t n_rows, int32_t n_halo, int64_t n_params);
 int dl_mix_plan_shape(int32_t n_rows, int32_t n_halo, int64_t n_params, int32_t nnz,
                       int32_t uniform_row_nnz, int32_t shared_row_weights, int32_t deviation,
                       int32_t tile_cols, dl_mix_plan *plan);
+/* (ABI 6) The same from a CSR descriptor (only its sizes and flags are read, pointers may be
+ * NULL): min_row_nnz included, which dl_mix_plan_shape cannot express (it assumes
+ * uniform_row_nnz). */
+int dl_mix_plan_csr(const dl_csr *W, int32_t n_halo, int64_t n_params, int32_t deviation,
+                    int32_t tile_cols, dl_mix_plan *plan);
 int dl_mix_plan_query(const dl_mix_args *args, dl_mix_plan *plan);
 int dl_mix_round(const dl_mix_args *args, void *workspace, size_t ws_bytes, dl_stream_t stream);
 

@@ -1,0 +1,197 @@
+"""Plan path 5: irregular graphs of thousands of agents whose CSR does not fit LDS beside a column
+tile of every agent (per-edge weights: 4 B weight + 2 B id per entry).  The tile kernel keeps
+each row's first min(min_row_nnz, 5) CSR entries in registers and stages only the rest in LDS
+(fp32 weight + u16 row per entry), so the round still streams X, G and X' once instead of taking the gather
+kernel.  The reference's Mixer takes any dict-of-dicts topology (utils/consensus_simple/
+mixer.py:43-49); the fold order is the row's CSR order, head then tail, so the result is the
+reference's left fold bit for bit."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import cref
+
+pytestmark = pytest.mark.gpu
+
+
+def bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+
+def eng_mod():
+    from distributed_learning_amd import engine
+    return engine
+
+
+def check_dev(Y, dev_sq, dev_max, mean=None):
+    want = cref.deviation_sq(Y)
+    m = cref.column_mean(Y)
+    floor = 8 * np.sqrt(Y.shape[1]) * np.finfo(np.float32).eps * np.abs(m).max()
+    d_got, d_want = np.sqrt(dev_sq), np.sqrt(want)
+    assert np.all(np.abs(d_got - d_want) <= 1e-5 * d_want + floor)
+    assert abs(dev_max - d_want.max()) <= 1e-5 * d_want.max() + floor
+    if mean is not None:
+        np.testing.assert_allclose(mean, m, rtol=1e-5, atol=1e-6 * np.abs(m).max())
+
+
+def ba(n, m, seed):
+    from distributed_learning_amd.graph import barabasi_albert_metropolis
+    return barabasi_albert_metropolis(n, m, seed)
+
+
+def dense_irregular(n, lo, hi, seed, row_stochastic=False):
+    """Every agent on a ring (degree 2) plus random extra neighbours up to degree lo..hi,
+    Metropolis weights (or, row_stochastic, random positive weights normalised per row: W is
+    then not doubly stochastic and the fused deviation takes its second LDS pass)."""
+    from distributed_learning_amd.graph import Csr
+    rng = np.random.default_rng(seed)
+    adj = [set() for _ in range(n)]
+    for i in range(n):
+        adj[i].add((i + 1) % n)
+        adj[(i + 1) % n].add(i)
+    target = rng.integers(lo, hi + 1, n)
+    for i in range(n):
+        while len(adj[i]) < target[i]:
+            j = int(rng.integers(n))
+            if j != i:
+                adj[i].add(j)
+                adj[j].add(i)
+    rowptr, col, w = [0], [], []
+    for i in range(n):
+        nb = sorted(adj[i], key=lambda j: (j * 7919 + i) % n)   # not sorted by id
+        if row_stochastic:
+            ws = list(rng.uniform(0.5, 1.5, len(nb) + 1))
+            tot = sum(ws)
+            ws = [x / tot for x in ws]
+            pos = int(rng.integers(len(nb) + 1))   # the self entry anywhere in the row
+            ids = nb[:pos] + [i] + nb[pos:]
+        else:
+            mw = [1.0 / (1.0 + max(len(adj[i]), len(adj[j]))) for j in nb]
+            ids, ws = [i] + nb, [1.0 - sum(mw)] + mw
+        col.extend(ids)
+        w.extend(ws)
+        rowptr.append(len(col))
+    return Csr(rowptr, col, w, keys=list(range(n)))
+
+
+CASES = {
+    # name: (graph builder, register head the planner must pick, forced)
+    "ba2_4096": (lambda: ba(4096, 2, 1), 3, False),   # the fixture-B construction at c4 scale
+    # a tree (leaves have 2 entries); its CSR (72 KiB) fits LDS beside the tile, so path 5 is
+    # forced (DLAMD_FORCE_REG=1) to cover the 2-entry head
+    "ba1_4096": (lambda: ba(4096, 1, 2), 2, True),
+    "deg5to9_4096": (lambda: dense_irregular(4096, 4, 8, 3), 5, False),
+    "deg9to12_2048": (lambda: dense_irregular(2048, 8, 11, 4), 5, False),   # 2 rows per thread
+    "ba2_3001": (lambda: ba(3001, 2, 5), 3, True),    # ragged last row pass (forced: fits LDS)
+}
+
+
+@pytest.mark.parametrize("layout", ["tiled", "rows"])
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_register_head_lds_tail(cuda, monkeypatch, case, layout):
+    """Fused local step + mix + deviation through path 5: bit-exact with the oracle's CSR-order
+    fold, deviation within 1e-5; the forced gather kernel gives the same bits."""
+    E = eng_mod()
+    build, head, forced = CASES[case]
+    if forced:
+        monkeypatch.setenv("DLAMD_FORCE_REG", "1")
+    csr = build()
+    n = csr.n_rows
+    assert not csr.uniform_row_nnz and csr.min_row_nnz >= head
+    P = 1024 + 32
+    rng = np.random.default_rng(n + head)
+    X = rng.standard_normal((n, P), dtype=np.float32)
+    G = rng.standard_normal((n, P), dtype=np.float32)
+    want = cref.mix_round(X, csr.rowptr, csr.col, csr.w, G=G, lr=0.02)
+    eng = E.GossipEngine(csr, P, device=cuda, X=torch.from_numpy(X).to(cuda), layout=layout)
+    plan = eng.plan()
+    assert plan["path"] == 5 and plan["tile_cols"] == 4, plan
+    assert plan["lds_bytes"] >= n * 16 + 6 * (csr.nnz - head * n)
+    mean = torch.empty(P, device=cuda)
+    eng.round(G=eng.layout_like(torch.from_numpy(G).to(cuda)), lr=0.02, deviation=True, mean=mean)
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(eng.rows().cpu().numpy()), bits(want))
+    check_dev(want, eng.agent_dev_sq().cpu().numpy(), float(eng.dev_max.item()),
+              mean.cpu().numpy())
+    # plain mix (no local step, no deviation) through the same path, rows in agent order
+    # instead of the engine's default row-length order: the same bits
+    eng2 = E.GossipEngine(csr, P, device=cuda, X=torch.from_numpy(X).to(cuda), layout=layout,
+                          order=None)
+    assert eng2.plan()["path"] == 5 and eng2.order is None
+    eng2.round()
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(eng2.rows().cpu().numpy()),
+                          bits(cref.mix_round(X, csr.rowptr, csr.col, csr.w)))
+    if layout == "rows" and case == "ba2_4096":
+        monkeypatch.setenv("DLAMD_FORCE_GATHER", "1")
+        W = E.DeviceCsr(csr, cuda)
+        assert E.plan_shape(W, P)["path"] == 2
+        Y = torch.empty(n, P, device=cuda)
+        E.mix_round(W, torch.from_numpy(X).to(cuda), Y, G=torch.from_numpy(G).to(cuda), lr=0.02)
+        torch.cuda.synchronize()
+        assert np.array_equal(bits(Y.cpu().numpy()), bits(want))
+
+
+def test_row_stochastic_two_pass_deviation(cuda):
+    """A W that is row- but not column-stochastic, the self entry at varying row positions: the
+    fused deviation cannot take the mean from the inputs and re-mixes the tile in a second LDS
+    pass (head + tail again); same bits, exact-mean deviation."""
+    E = eng_mod()
+    csr = dense_irregular(4096, 4, 9, 7, row_stochastic=True)
+    assert not csr.doubly_stochastic and csr.min_row_nnz >= 5
+    P = 512
+    rng = np.random.default_rng(11)
+    X = rng.standard_normal((4096, P), dtype=np.float32)
+    eng = E.GossipEngine(csr, P, device=cuda, X=torch.from_numpy(X).to(cuda))
+    assert eng.plan()["path"] == 5
+    mean = torch.empty(P, device=cuda)
+    eng.round(deviation=True, mean=mean)
+    torch.cuda.synchronize()
+    want = cref.mix_round(X, csr.rowptr, csr.col, csr.w)
+    assert np.array_equal(bits(eng.rows().cpu().numpy()), bits(want))
+    check_dev(want, eng.agent_dev_sq().cpu().numpy(), float(eng.dev_max.item()),
+              mean.cpu().numpy())
+
+
+@pytest.mark.parametrize("rounds", [1, 10])
+def test_reference_fixture_b_through_path5(cuda, golden, monkeypatch, rounds):
+    """The reference-run fixture B (Barabasi-Albert 64 agents, Metropolis weights, string keys,
+    `Mixer._mix_params_once` snapshots) forced through the register-head + LDS-tail kernel
+    (DLAMD_FORCE_REG=1; at 64 agents the CSR would fit LDS): bit-identical after 1 and 10
+    rounds.  Fixture A (random 4-regular, uniform weights) likewise through path 4."""
+    from distributed_learning_amd.graph import Csr
+    E = eng_mod()
+    d = golden("mix_rr4_n64.npz")
+    monkeypatch.setenv("DLAMD_FORCE_REG", "1")
+    for tag, path in (("b", 5), ("a", 4)):
+        csr = Csr(d[f"{tag}_rowptr"], d[f"{tag}_cols"], d[f"{tag}_w"])
+        X0 = d[f"{tag}_X0"]
+        for layout in ("tiled", "rows"):
+            eng = E.GossipEngine(csr, X0.shape[1], device=cuda,
+                                 X=torch.from_numpy(X0).to(cuda), layout=layout)
+            assert eng.plan()["path"] == path, (tag, layout, eng.plan())
+            for _ in range(rounds):
+                eng.round()
+            torch.cuda.synchronize()
+            assert np.array_equal(bits(eng.rows().cpu().numpy()), bits(d[f"{tag}_X{rounds}"])), \
+                (tag, layout)
+
+
+def test_plan_csr_reports_path5_and_refuses_bad_promise(cuda):
+    """dl_mix_plan_csr sees min_row_nnz (dl_mix_plan_shape assumes uniform rows and reports the
+    gather path for the same sizes); a min_row_nnz above nnz / n_rows is refused."""
+    import ctypes
+    from distributed_learning_amd import _lib
+    E = eng_mod()
+    csr = ba(4096, 2, 1)
+    W = E.DeviceCsr(csr, cuda)
+    assert E.plan_shape(W, 1 << 18, tile_cols=-1)["path"] == 5
+    lib = _lib.load()
+    pl = _lib.DlMixPlan()
+    _lib.check(lib.dl_mix_plan_shape(4096, 0, 1 << 18, csr.nnz, 0, 0, 1, 0, ctypes.byref(pl)),
+               "plan")
+    assert pl.path == 2
+    W.min_row_nnz = csr.nnz // 4096 + 1
+    with pytest.raises(Exception):
+        Y = torch.empty(4096, 64, device=cuda)
+        E.mix_round(W, torch.zeros(4096, 64, device=cuda), Y)

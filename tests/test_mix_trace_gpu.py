@@ -53,16 +53,32 @@ def noise_floor(X):
     return 8 * np.sqrt(X.shape[1]) * np.finfo(np.float32).eps * np.abs(X.mean(axis=0)).max()
 
 
+def torus_csr(side):
+    from distributed_learning_amd.graph import (best_constant_weight, from_edge_weights,
+                                                torus_edges)
+    edges = torus_edges(side, side)
+    n = side * side
+    w = best_constant_weight(edges, list(range(n)))
+    return from_edge_weights(edges, [w] * len(edges), list(range(n)))
+
+
 # rr4 rows run mix_trace_rows_kernel (4 / 2 / 1 agents per thread at 1024 / 300 / 64 agents,
 # ragged at 300; 256, 512 and 1024 agents fill every slot: the unguarded FULL instantiations);
-# metropolis rows (irregular) the chunk-major planes kernel
+# metropolis rows (irregular) the chunk-major planes kernel.  Above 1024 agents the wide kernel
+# (one column chunk per step, 2 or 4 agents per thread): rr4 2048 (FULL, CSR in registers), rr4
+# 3000 (ragged, 4 per thread), the c4 torus (4096, FULL), sparse Metropolis 1500 (CSR in LDS)
 CASES = [("rr4", 64, 4096, 0), ("rr4", 1024, 256, 1), ("metro", 50, 1000, 2),
          ("metro", 7, 4, 3), ("rr4", 16, 65536, 4), ("rr4", 300, 512, 5), ("rr4", 1000, 128, 6),
-         ("rr4", 256, 1024, 7), ("rr4", 512, 512, 8)]
+         ("rr4", 256, 1024, 7), ("rr4", 512, 512, 8), ("rr4", 2048, 256, 9),
+         ("rr4", 3000, 128, 10), ("torus", 4096, 256, 11), ("metro_sparse", 1500, 192, 12)]
 
 
 def make(kind, n, seed):
-    return rr_csr(n, seed) if kind == "rr4" else metropolis_csr(n, 0.1, seed)
+    if kind == "rr4":
+        return rr_csr(n, seed)
+    if kind == "torus":
+        return torus_csr(int(round(n ** 0.5)))
+    return metropolis_csr(n, 3.0 / n if kind == "metro_sparse" else 0.1, seed)
 
 
 @pytest.mark.parametrize("kind,n,P,seed", CASES)
@@ -127,8 +143,13 @@ def test_trace_plan_rejects_unsupported(cuda):
     Y = torch.empty_like(X)
     # random directed neighbours: not doubly stochastic -> the round loop takes over
     assert e.trace_max_rounds(e.DeviceCsr(graph_csr(8, 3, seed=0), cuda), X, Y) == 0
-    big = torch.randn(2048, 64, device=cuda)
-    assert e.trace_max_rounds(e.DeviceCsr(rr_csr(2048, 0), cuda), big, torch.empty_like(big)) == 0
+    big = torch.randn(4100, 64, device=cuda)       # above 4096 agents
+    assert e.trace_max_rounds(e.DeviceCsr(rr_csr(4100, 0), cuda), big, torch.empty_like(big)) == 0
+    # above 2048 agents the CSR must be register-cached (regular degree 4, shared weights)
+    mid = torch.randn(3000, 64, device=cuda)
+    assert e.trace_max_rounds(e.DeviceCsr(metropolis_csr(3000, 1.0 / 3000, 1), cuda), mid,
+                              torch.empty_like(mid)) == 0
+    assert e.trace_max_rounds(e.DeviceCsr(rr_csr(3000, 0), cuda), mid, torch.empty_like(mid)) == 8
     W = e.DeviceCsr(rr_csr(8, 0), cuda)
     k = e.trace_max_rounds(W, X, Y)
     with pytest.raises(ValueError, match="rounds must be"):
@@ -277,3 +298,76 @@ def test_full_size_c2_gossip_traced_pass(cuda):
     assert torch.equal(eng.rows(), Y)
     floor = 8 * np.sqrt(P) * np.finfo(np.float32).eps * float(X.mean(0).abs().max())
     np.testing.assert_allclose(trace.cpu().numpy(), ref, rtol=1e-5, atol=floor)
+
+
+def test_full_size_c4_gossip_traced_pass(cuda):
+    """BASELINE config c4 (64 x 64 torus, 4096 agents x 2^18, best-constant weights) as
+    Mixer.mix(times, eps)'s device path: one traced pass of 8 rounds through the wide kernel
+    (column-tiled T = 4, 4 agents per thread, CSR in registers) -- column slices bit-exact
+    against 8 oracle rounds, the input intact, and every round's max deviation against the fused
+    deviation of 8 single-round launches."""
+    e = E()
+    n, P, K = 4096, 1 << 18, 8
+    csr = torus_csr(64)
+    W = e.DeviceCsr(csr, cuda)
+    g = torch.Generator(device=cuda).manual_seed(4)
+    X = torch.randn(n, P, device=cuda, generator=g)
+    T = 4
+    Xt = e.to_tiled(X, T)
+    Yt = torch.empty_like(Xt)
+    assert e.trace_max_rounds(W, Xt, Yt, tiled=(P, T)) == K
+    trace = torch.full((K,), -1.0, device=cuda)
+    X0 = Xt.clone()
+    e.mix_rounds_trace(W, Xt, Yt, K, trace, tiled=(P, T))
+    torch.cuda.synchronize()
+    assert torch.equal(Xt, X0)
+    del X0
+    Y = e.from_tiled(Yt, P)
+    for c0, c1 in [(0, 512), (P - 512, P), (100001, 100001 + 303)]:
+        Z = X[:, c0:c1].cpu().numpy()
+        for _ in range(K):
+            Z = cref.mix_round(Z, csr.rowptr, csr.col, csr.w)
+        assert np.array_equal(bits(Y[:, c0:c1].cpu().numpy()), bits(Z)), (c0, c1)
+    eng = e.GossipEngine(csr, P, device=cuda, X=X)
+    ref = []
+    for _ in range(K):
+        eng.round(deviation=True)
+        ref.append(float(eng.dev_max.item()))
+    assert torch.equal(eng.rows(), Y)
+    floor = 8 * np.sqrt(P) * np.finfo(np.float32).eps * float(X.mean(0).abs().max())
+    np.testing.assert_allclose(trace.cpu().numpy(), ref, rtol=1e-5, atol=floor)
+
+
+@pytest.mark.parametrize("times,eps", [(1, 2e-1), (20, 1e-1), (3, 5e-1)])
+def test_mixer_traced_path_4096_agents(cuda, monkeypatch, times, eps):
+    """Mixer.mix(times, eps) over the c4 torus (4096 models) takes traced passes of 8 rounds
+    through the wide kernel: the reference loop's round count and bits, one debug line per
+    evaluation (stops inside the first pass, and in later passes)."""
+    from distributed_learning_amd import engine
+    from distributed_learning_amd.utils.consensus_simple import Mixer
+    calls = []
+    real = engine.mix_rounds_trace
+    monkeypatch.setattr(engine, "mix_rounds_trace",
+                        lambda *a, **k: (calls.append(a[3]), real(*a, **k))[1])
+    log = logging.getLogger("traced4096")
+    log.setLevel(logging.DEBUG)
+    h = _Rec()
+    log.addHandler(h)
+    torch.manual_seed(2)
+    csr = torus_csr(64)
+    n = csr.n_rows
+    topo = {i: {int(csr.col[e]): float(csr.w[e]) for e in range(csr.rowptr[i], csr.rowptr[i + 1])}
+            for i in range(n)}
+    models = {i: torch.nn.Linear(24, 8).to(cuda) for i in range(n)}
+    X0 = np.stack([torch.cat([p.data.reshape(-1) for p in models[i].parameters()]).cpu().numpy()
+                   for i in range(n)])
+    rp, cl, w = M.topology_to_csr(topo)
+    want, want_n = M.mixer_mix(X0, rp, cl, w, times=times, eps=eps)
+    assert Mixer(models, topo, log).mix(times=times, eps=eps) == want_n
+    assert calls and set(calls) == {8}, calls
+    got = np.stack([torch.cat([p.data.reshape(-1) for p in models[i].parameters()]).cpu().numpy()
+                    for i in range(n)])
+    assert np.array_equal(bits(got), bits(want))
+    devs = [ln for ln in h.lines if ln.startswith("Mixer calculate max deviation")]
+    assert len(devs) == want_n + 1
+    log.removeHandler(h)

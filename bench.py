@@ -59,6 +59,11 @@ def parse():
     p.add_argument("--workload", default="c2",
                    choices=["c1", "c2", "c2-mix", "c2-gossip", "c2-halo", "c3", "c4", "c4-gather", "c4-ba",
                             "c5"])
+    p.add_argument("--irregular", default="ba2", choices=["ba2", "ba1", "deg"],
+                   help="c4-ba: Barabasi-Albert m=2 (the headline), m=1, or a hub-free random "
+                        "graph of degree 2..6 (graph.random_irregular_metropolis)")
+    p.add_argument("--order", default="auto", choices=["auto", "agents"],
+                   help="c4-ba: engine row order (auto = by row length for plan path 5)")
     p.add_argument("--layout", default="auto", choices=["auto", "rows", "tiled"],
                    help="c2-gossip: resident layout of X (rows = the Mixer drop-in's row-major "
                         "flattened models)")
@@ -504,14 +509,20 @@ def run_gather(args, dev, rank, world):
     ``--workload c4-ba``: the same on an IRREGULAR graph of the same size -- Barabasi-Albert
     (m = 2, seed 1) with Metropolis weights, the reference-run fixture B's construction at 4096
     agents (rows of 3 to 172 entries, 20,472 entries): plan path 5, each row's first 3 entries in
-    registers and the other 8,184 in LDS behind the tile."""
+    registers and the other 8,184 in LDS behind the tile as 8-byte {weight, row} pairs, rows
+    in the engine's row-length order (``--order agents`` keeps agent order)."""
     from distributed_learning_amd import engine, graph
     if args.workload == "c4-ba":
-        csr = graph.barabasi_albert_metropolis(4096, 2, 1)
+        if args.irregular == "deg":
+            csr = graph.random_irregular_metropolis(4096, 2, 6, 1)
+        else:
+            csr = graph.barabasi_albert_metropolis(4096, 2 if args.irregular == "ba2" else 1, 1)
         n = csr.n_rows
-        kname = "mix_tile_kernel<1, 4, true, true, true, false, true, 3, false, true>"
-        gname = ("c4-ba: Barabasi-Albert m=2 (seed 1), Metropolis weights, 4096 agents, fused "
-                 "local step + mix + deviation")
+        kname = "mix_tile_kernel<1, 4, true, true, true, false, true, 3, false, 2>"
+        gname = ({"ba2": "c4-ba: Barabasi-Albert m=2 (seed 1)", "ba1": "c4-ba: Barabasi-Albert "
+                  "m=1 (seed 1)", "deg": "c4-ba --irregular deg: ring + random degree 2..6"}
+                 [args.irregular] + ", Metropolis weights, 4096 agents, fused local step + mix "
+                 "+ deviation")
         kdesc = "mix_tile_kernel register head + LDS tail (+dev_reduce), HIP-event time"
         metric = "consensus rounds/sec, 4096 agents x 2^18 fp32 params, irregular graph"
         prof_dir = os.path.join(ROOT, "profiles", "r10", "ba")
@@ -540,7 +551,8 @@ def run_gather(args, dev, rank, world):
         return elapsed, float(np.mean([a.elapsed_time(b) for a, b, *_ in evs]))
 
     # product path: register-CSR tile kernel, tiled layout, fused deviation
-    eng = engine.GossipEngine(csr, P, device=dev, X=torch.randn(n, P, device=dev, generator=gen))
+    eng = engine.GossipEngine(csr, P, device=dev, X=torch.randn(n, P, device=dev, generator=gen),
+                              order="auto" if args.order == "auto" else None)
     G = eng.layout_like(torch.randn(n, P, device=dev, generator=gen))
     plan = eng.plan(deviation=True)
     elapsed, launch_ms = timed(lambda: eng.round(G=G, lr=lr, deviation=True))

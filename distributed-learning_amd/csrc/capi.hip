@@ -82,7 +82,8 @@ struct Plan {
     int chunks;
     bool dev;
     uint32_t csr_off, scratch_off;
-    int head;   // path 5: CSR entries per row in registers (the rest in LDS)
+    int head;       // path 5: CSR entries per row in registers (the rest in LDS)
+    int tail_fmt;   // path 5: LDS tail entries of 8 B (2) or 6 B (1)
 };
 
 // Workgroups per CU the tile kernel may use (LDS permitting): 2 unless DLAMD_WG_PER_CU=1
@@ -116,26 +117,29 @@ int next_pow2_chunks(int64_t n_params) {
 }
 
 // LDS bytes of the register-head + LDS-tail tile kernel (path 5) for R rows at c chunks, or 0
-// when it does not apply: the nnz - head * R tail entries (6 B each: fp32 weight, u16 row)
-// behind the tile and the mean scratch; the tail's u16 row map (setup only) must fit the tile
-// area.
-int64_t reg_tail_lds(const dl_csr &W, int32_t R, int c, bool want_dev, int *head_out) {
+// when it does not apply: the nnz - head * R tail entries behind the tile and the mean scratch,
+// 8 B per entry ({weight, row} pairs, *fmt = 2) when that fits, else 6 B (weights + u16 rows,
+// *fmt = 1; the only form at a 5-entry head, whose registers leave no room for the pairs'
+// unrolled loop); the tail's u16 row map (setup only) must fit the tile area.
+int64_t reg_tail_lds(const dl_csr &W, int32_t R, int c, bool want_dev, int *head_out,
+                     int *fmt_out = nullptr) {
     const int head = dl::reg_head_rows(W.min_row_nnz);
     if (W.uniform_row_nnz == 5 || !dl::reg_tail_supported(c, R, head, 0)) return 0;
     const int64_t ntail = (int64_t)W.nnz - (int64_t)head * R;
     if (ntail < 0 || ntail > 65535) return 0;
     const int64_t tile = (int64_t)R * c * 16;
     const int64_t scratch = want_dev ? (int64_t)(dl::kTileThreads / 64) * c * 16 : 0;
-    const int64_t lds = tile + scratch + ((6 * ntail + 15) & ~(int64_t)15);
-    if (tile > 65536 || lds > dl::kLdsBytes || 2 * ntail > tile) return 0;
-    if (head_out) *head_out = head;
-    return lds;
+    if (tile > 65536 || 2 * ntail > tile) return 0;
+    for (int fmt = head < 5 ? 2 : 1; fmt >= 1; --fmt) {
+        const int64_t lds = tile + scratch + (((fmt == 2 ? 8 : 6) * ntail + 15) & ~(int64_t)15);
+        if (lds > dl::kLdsBytes) continue;
+        if (head_out) *head_out = head;
+        if (fmt_out) *fmt_out = fmt;
+        return lds;
+    }
+    return 0;
 }
 
-// Tile width (float4 chunks) for the column-tiled layout: the widest power of two whose tile
-// of all R rows is <= 64 KiB and fits LDS beside the CSR.  Measured on MI355X:
-// 64-KiB tiles stream at 5.7-5.85 TB/s for N = 256..1024, 128-KiB tiles at 5.0-5.6 TB/s
-// depending on the box.  0 = no tiled configuration fits.
 // DLAMD_FORCE_REG=1 (tests only): the register-CSR kernels (paths 4 / 5) wherever they apply,
 // so the reference's small fixtures pin them too
 bool force_reg_env() {
@@ -188,7 +192,7 @@ bool plan_reg(const dl_mix_args *a, int c, bool want_dev, Plan *pl) {
         lds = tile + scratch;
         if (lds > dl::kLdsBytes) return false;
     } else {
-        lds = reg_tail_lds(a->W, R, c, want_dev, &head);
+        lds = reg_tail_lds(a->W, R, c, want_dev, &head, &pl->tail_fmt);
         if (lds == 0) return false;
     }
     const int64_t T = 4 * c;
@@ -981,8 +985,8 @@ int dl_mix_round(const dl_mix_args *args, void *workspace, size_t ws_bytes, dl_s
             t.n_tiles = (int32_t)n_full;
             t.col_base = 0;
             t.dev_partial = partial;
-            hipError_t e = reg_csr ? dl::launch_mix_tile_reg(t, pl.chunks, pl.head, sgd, pl.dev,
-                                                             grid_full, lds, s)
+            hipError_t e = reg_csr ? dl::launch_mix_tile_reg(t, pl.chunks, pl.head, pl.tail_fmt,
+                                                             sgd, pl.dev, grid_full, lds, s)
                                    : dl::launch_mix_tile(t, pl.chunks, sgd, pl.dev, true,
                                                          grid_full, lds, true, s);
             if (e != hipSuccess) return hip_fail(e, "mix_tile_kernel launch");

@@ -85,9 +85,10 @@ bool reg_csr_supported(int chunks, int n_rows, int regular, int n_halo);
 // of each row in registers, the remaining nnz - head * n_rows entries in LDS (8 B each)
 int reg_head_rows(int min_row_nnz);   // 5, 3, 2 or 0 (no register head)
 bool reg_tail_supported(int chunks, int n_rows, int head, int n_halo);
-// head 0: the regular register-CSR kernel (path 4); head > 0: head + LDS tail (path 5)
-hipError_t launch_mix_tile_reg(const TileArgs &a, int chunks, int head, bool sgd, bool dev,
-                               int grid, int lds, hipStream_t s);
+// head 0: the regular register-CSR kernel (path 4); head > 0: head + LDS tail (path 5), the
+// tail as {weight, row} pairs of 8 B (tail_fmt 2, heads < 5) or weights + u16 rows (1: 6 B)
+hipError_t launch_mix_tile_reg(const TileArgs &a, int chunks, int head, int tail_fmt, bool sgd,
+                               bool dev, int grid, int lds, hipStream_t s);
 // rows per thread (KV) the FAST tile kernels use for n_src rows at `chunks` float4 per row
 int tile_passes(int chunks, int n_src, bool fast);
 // K rounds of mixing on LDS-resident tiles (mix_multi.hip); FAST tiles only, no halo rows

@@ -128,12 +128,15 @@ __device__ __forceinline__ float4 *at(float *base, uint32_t off) {
 //        ranks, the numerator of the next mean_prev (sum(W t) = sum(t): W doubly stochastic).
 // RAG  : (with RD > 0) an irregular graph whose every row has >= RD entries (dl_csr.min_row_nnz):
 //        each row's first RD entries in registers as above, the rest ("tail", nnz - RD*n_rows
-//        entries) staged once per workgroup in LDS behind the tile, fp32 weights then u16 row
-//        indices (6 B per entry); row r's tail is [rowptr[r] - RD*r, rowptr[r+1] - RD*(r+1)).  The fold runs the
+//        entries) staged once per workgroup in LDS behind the tile; row r's tail is
+//        [rowptr[r] - RD*r, rowptr[r+1] - RD*(r+1)) there.  RAG = 2: {weight, row} pairs of 8 B
+//        (one ds_read_b64 per entry, +4 % on c4-ba); RAG = 1: fp32 weights then u16 rows (6 B,
+//        for tails that do not fit LDS at 8 B).  The fold runs the
 //        register head, then the tail, in CSR order: still the reference's left fold.
 template <int C, int KV, bool SGD, bool DEV, bool MIX, bool HALO, bool FAST, int RD = 0,
-          bool LAG = false, bool RAG = false>
+          bool LAG = false, int RAG = 0>
 __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
+    constexpr bool PACK = RAG == 2;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float4 *tile = reinterpret_cast<float4 *>(smem);
     constexpr int NT = kTileThreads;
@@ -163,6 +166,7 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
     const int ntail = RAG ? nnz - RD * Nr : 0;
     float *ltw = reinterpret_cast<float *>(smem + a.csr_off);
     uint16_t *ltc = reinterpret_cast<uint16_t *>(smem + a.csr_off + 4u * (uint32_t)ntail);
+    uint2 *ltp = reinterpret_cast<uint2 *>(smem + a.csr_off);   // RAG == 2
     if (RD > 0) {
 #pragma unroll
         for (int i = 0; i < (NRC + 1) / 2; ++i) ri[i] = 0u;
@@ -200,8 +204,12 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
                 const int e = t + RD * (r + 1);
                 const float we = a.w[e];
                 const int ce = a.col[e];
-                ltw[t] = we;
-                ltc[t] = (uint16_t)(ce * C + c);
+                if (PACK) {
+                    ltp[t] = make_uint2(__float_as_uint(we), (uint32_t)(ce * C + c));
+                } else {
+                    ltw[t] = we;
+                    ltc[t] = (uint16_t)(ce * C + c);
+                }
             }
             __syncthreads();
         }
@@ -345,24 +353,61 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
             // entry exposed two dependent LDS latencies each (4.5 ms per round, LDS-bound)
             uint32_t t = d & 0xffffu;
             const uint32_t t1 = t + (d >> 16);
-            // (one at a five-entry head: beside its 30 head registers even two per step spill
-            // 84 VGPRs in the local-step + deviation instantiation)
+            // (eight per step spill; one at a five-entry head: beside its 30 head registers even
+            // two per step spill 84 VGPRs in the local-step + deviation instantiation)
             constexpr int TU = RD >= 5 ? 1 : 4;
+            auto tail_w = [&](uint32_t i) {
+                if (PACK) return __uint_as_float(ltp[i].x);
+                return ltw[i];
+            };
+            auto tail_c = [&](uint32_t i) -> uint32_t {
+                if (PACK) return ltp[i].y;
+                return ltc[i];
+            };
+            // The fold runs on (x, y) / (z, w) pairs (v_pk_mul_f32 / v_pk_add_f32 round every
+            // lane as the scalar ops do: same bits): a hub row's chain is one lane's, so its
+            // length is the VALU issue of a wave -- four packed ops per entry instead of eight
+            // (c4-ba 338 -> 363 rounds/s)
+            typedef float f32x2 __attribute__((ext_vector_type(2)));
+            f32x2 lo = {acc.x, acc.y}, hi = {acc.z, acc.w};
+            auto fold = [&](float w, const float4 &v) {
+                if (RD < 5) {   // (at a five-entry head the pairs spill)
+                    const f32x2 w2 = {w, w};
+                    lo = lo + w2 * f32x2{v.x, v.y};
+                    hi = hi + w2 * f32x2{v.z, v.w};
+                } else {
+                    lo.x = lo.x + w * v.x;
+                    lo.y = lo.y + w * v.y;
+                    hi.x = hi.x + w * v.z;
+                    hi.y = hi.y + w * v.w;
+                }
+            };
+            if constexpr (RD >= 5) {   // the pairs and the unroll spill beside a 5-entry head
+                for (; t < t1; ++t) axpy4(acc, tail_w(t), tile[tail_c(t)]);
+                return acc;
+            }
             if constexpr (TU > 1) for (; t + TU <= t1; t += TU) {
                 float w4[TU];
                 uint32_t c4[TU];
 #pragma unroll
                 for (int u = 0; u < TU; ++u) {
-                    w4[u] = ltw[t + u];
-                    c4[u] = ltc[t + u];
+                    if (PACK) {
+                        const uint2 pr = ltp[t + u];
+                        w4[u] = __uint_as_float(pr.x);
+                        c4[u] = pr.y;
+                    } else {
+                        w4[u] = ltw[t + u];
+                        c4[u] = ltc[t + u];
+                    }
                 }
                 float4 v4[TU];
 #pragma unroll
                 for (int u = 0; u < TU; ++u) v4[u] = tile[c4[u]];
 #pragma unroll
-                for (int u = 0; u < TU; ++u) axpy4(acc, w4[u], v4[u]);
+                for (int u = 0; u < TU; ++u) fold(w4[u], v4[u]);
             }
-            for (; t < t1; ++t) axpy4(acc, ltw[t], tile[ltc[t]]);
+            for (; t < t1; ++t) fold(tail_w(t), tile[tail_c(t)]);
+            acc = make_float4(lo.x, lo.y, hi.x, hi.y);
         }
         return acc;
     };
@@ -449,7 +494,8 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
             }
             // lands while we mix from LDS.  Issued after the staging barrier: issuing it before
             // (right after the staging writes) measured 10 % slower (scripts/grid_sweep.py,
-            // profiles/r05/grid_sweep_early_prefetch.log)
+            // profiles/r05/grid_sweep_early_prefetch.log; the register-head + LDS-tail kernel,
+            // one workgroup per CU, 10 % slower too: c4-ba 327 vs 361 rounds/s)
             if (nxt < a.n_tiles) prefetch(nxt);
             float *yt = const_cast<float *>(
                 reinterpret_cast<const float *>(tile_base(a.y, a.yts, tile_id)));
@@ -684,7 +730,7 @@ __global__ void __launch_bounds__(1024) stream_triad_tile_kernel(const float4 *_
 }
 
 template <int C, int KV, bool SGD, bool DEV, bool MIX, bool HALO, bool FAST, int RD = 0,
-          bool LAG = false, bool RAG = false>
+          bool LAG = false, int RAG = 0>
 hipError_t launch_one(const TileArgs &a, int grid, int lds, hipStream_t s) {
     auto k = mix_tile_kernel<C, KV, SGD, DEV, MIX, HALO, FAST, RD, LAG, RAG>;
     hipError_t e = allow_full_lds(reinterpret_cast<const void *>(k));
@@ -733,7 +779,7 @@ int tile_passes(int chunks, int n_src, bool fast) {
 // CSR that fits a 5-entry register head fits LDS too.)
 //   head == 0: regular graphs of 5 entries per row, the whole CSR in registers (path 4);
 //   head  > 0: rows of >= head entries, the first `head` in registers, the rest in LDS (path 5).
-template <int KV, int RD, bool RAG>
+template <int KV, int RD, int RAG>
 hipError_t launch_reg_kv(const TileArgs &a, bool sgd, bool dev, int grid, int lds, hipStream_t s) {
     if (sgd)
         return dev ? launch_one<1, KV, true, true, true, false, true, RD, false, RAG>(a, grid, lds, s)
@@ -742,7 +788,7 @@ hipError_t launch_reg_kv(const TileArgs &a, bool sgd, bool dev, int grid, int ld
                : launch_one<1, KV, false, false, true, false, true, RD, false, RAG>(a, grid, lds, s);
 }
 
-template <int RD, bool RAG>
+template <int RD, int RAG>
 hipError_t launch_reg(const TileArgs &a, bool sgd, bool dev, int grid, int lds, hipStream_t s) {
     return tile_passes(1, a.n_src, true) <= 2 ? launch_reg_kv<2, RD, RAG>(a, sgd, dev, grid, lds, s)
                                               : launch_reg_kv<4, RD, RAG>(a, sgd, dev, grid, lds, s);
@@ -760,20 +806,24 @@ bool reg_tail_supported(int chunks, int n_rows, int head, int n_halo) {
     return head > 0 && n_halo == 0 && chunks == 1 && tile_passes(chunks, n_rows, true) <= 4;
 }
 
-hipError_t launch_mix_tile_reg(const TileArgs &a, int chunks, int head, bool sgd, bool dev,
-                               int grid, int lds, hipStream_t s) {
+hipError_t launch_mix_tile_reg(const TileArgs &a, int chunks, int head, int tail_fmt, bool sgd,
+                               bool dev, int grid, int lds, hipStream_t s) {
     if (head == 0) {
         if (!reg_csr_supported(chunks, a.n_rows, a.regular, a.n_src - a.n_rows))
             return hipErrorInvalidValue;
-        return launch_reg<5, false>(a, sgd, dev, grid, lds, s);
+        return launch_reg<5, 0>(a, sgd, dev, grid, lds, s);
     }
     if (!reg_tail_supported(chunks, a.n_rows, head, a.n_src - a.n_rows) ||
-        a.nnz < head * a.n_rows)
+        a.nnz < head * a.n_rows || (tail_fmt != 1 && tail_fmt != 2) ||
+        (head >= 5 && tail_fmt != 1))
         return hipErrorInvalidValue;
+    const bool pk = tail_fmt == 2;
     switch (head) {
-        case 5: return launch_reg<5, true>(a, sgd, dev, grid, lds, s);
-        case 3: return launch_reg<3, true>(a, sgd, dev, grid, lds, s);
-        case 2: return launch_reg<2, true>(a, sgd, dev, grid, lds, s);
+        case 5: return launch_reg<5, 1>(a, sgd, dev, grid, lds, s);
+        case 3: return pk ? launch_reg<3, 2>(a, sgd, dev, grid, lds, s)
+                          : launch_reg<3, 1>(a, sgd, dev, grid, lds, s);
+        case 2: return pk ? launch_reg<2, 2>(a, sgd, dev, grid, lds, s)
+                          : launch_reg<2, 1>(a, sgd, dev, grid, lds, s);
         default: return hipErrorInvalidValue;
     }
 }

@@ -398,6 +398,33 @@ def lds_slot_order_native(csr, chunks, moves=4_000_000, seed=0):
     return order.astype(np.int64), int(conf[0]), int(conf[1])
 
 
+def random_irregular_metropolis(n, lo, hi, seed):
+    """Every agent on a ring (degree 2) plus random extra neighbours up to a degree drawn from
+    lo..hi (no hubs: rows of lo+1 .. ~hi+3 entries), Metropolis weights, self weight first,
+    neighbours in a scrambled (not sorted) order: an irregular graph without the Barabasi-Albert
+    hubs (bench --workload c4-ba --irregular deg)."""
+    rng = np.random.default_rng(seed)
+    adj = [set() for _ in range(n)]
+    for i in range(n):
+        adj[i].add((i + 1) % n)
+        adj[(i + 1) % n].add(i)
+    target = rng.integers(lo, hi + 1, n)
+    for i in range(n):
+        while len(adj[i]) < target[i]:
+            j = int(rng.integers(n))
+            if j != i:
+                adj[i].add(j)
+                adj[j].add(i)
+    rowptr, col, w = [0], [], []
+    for i in range(n):
+        nb = sorted(adj[i], key=lambda j: (j * 7919 + i) % n)
+        mw = [1.0 / (1.0 + max(len(adj[i]), len(adj[j]))) for j in nb]
+        col.extend([i] + nb)
+        w.extend([1.0 - sum(mw)] + mw)
+        rowptr.append(len(col))
+    return Csr(rowptr, col, w, keys=list(range(n)))
+
+
 def row_length_order(csr):
     """Agents by descending CSR row length (stable): order[slot] = agent.  The register-head +
     LDS-tail tile kernel (plan path 5) mixes rows s + k * 1024 in lane s of pass k, and a wave

@@ -83,7 +83,14 @@ CASES = {
     "deg5to9_4096": (lambda: dense_irregular(4096, 4, 8, 3), 5, False),
     "deg9to12_2048": (lambda: dense_irregular(2048, 8, 11, 4), 5, False),   # 2 rows per thread
     "ba2_3001": (lambda: ba(3001, 2, 5), 3, True),    # ragged last row pass (forced: fits LDS)
+    # a 3-entry head whose tail fits LDS at 6 B per entry but not at 8 B (the split format)
+    "deg2to7_4096": (lambda: rim(4096, 2, 7, 1), 3, False),
 }
+
+
+def rim(n, lo, hi, seed):
+    from distributed_learning_amd.graph import random_irregular_metropolis
+    return random_irregular_metropolis(n, lo, hi, seed)
 
 
 @pytest.mark.parametrize("layout", ["tiled", "rows"])
@@ -106,7 +113,11 @@ def test_register_head_lds_tail(cuda, monkeypatch, case, layout):
     eng = E.GossipEngine(csr, P, device=cuda, X=torch.from_numpy(X).to(cuda), layout=layout)
     plan = eng.plan()
     assert plan["path"] == 5 and plan["tile_cols"] == 4, plan
-    assert plan["lds_bytes"] >= n * 16 + 6 * (csr.nnz - head * n)
+    ntail = csr.nnz - head * n
+    assert plan["lds_bytes"] >= n * 16 + 6 * ntail
+    # 8-byte {weight, row} pairs whenever they fit LDS (heads < 5), else 6 B per entry
+    pairs = head < 5 and n * 16 + 256 + 8 * ntail <= 163840
+    assert (plan["lds_bytes"] >= n * 16 + 8 * ntail) == pairs, (plan, ntail)
     mean = torch.empty(P, device=cuda)
     eng.round(G=eng.layout_like(torch.from_numpy(G).to(cuda)), lr=0.02, deviation=True, mean=mean)
     torch.cuda.synchronize()

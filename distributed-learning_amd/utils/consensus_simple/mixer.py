@@ -89,23 +89,43 @@ class Mixer(object):
             stopping_criterion = self._update_stopping_criterion(X, times_done, times, eps)
             if not stopping_criterion and fused_dev:
                 X, times_done, stopping_criterion = self._mix_traced(W, X, times, eps)
+            P = X.shape[1]
+            # above _TRACE_TILED_ABOVE agents the remaining rounds run on a column-tiled copy of X
+            # (a row-major tile of all agents is a short segment of every row)
+            T = None
+            if not stopping_criterion and (fused_dev or eps is None):
+                T = self._loop_tile_cols(W, P)
+            tl = None
+            if T:
+                tl = (P, T)
+                X = _engine.to_tiled(X, T)
+                Y = torch.empty_like(X)
             if not stopping_criterion and eps is None:
                 # times rounds, no stop test in between: one pass over HBM (rows padded with
                 # zero columns to whole tiles; zeros mix to zeros)
-                P = X.shape[1]
-                Pp = -(-P // 64) * 64
-                Xp = torch.nn.functional.pad(X, (0, Pp - P)) if Pp != P else X
-                Yp = torch.empty_like(Xp)
-                if _engine.mix_rounds(W, Xp, Yp, math.ceil(times), workspace=self._wspace()):
-                    X, times_done = Yp[:, :P], math.ceil(times)
-                    stopping_criterion = True
+                if tl:
+                    Yt = torch.empty_like(X)
+                    if _engine.mix_rounds(W, X, Yt, math.ceil(times), workspace=self._wspace(),
+                                          tiled=tl):
+                        X, times_done = Yt, math.ceil(times)
+                        stopping_criterion = True
+                else:
+                    Pp = -(-P // 64) * 64
+                    Xp = torch.nn.functional.pad(X, (0, Pp - P)) if Pp != P else X
+                    Yp = torch.empty_like(Xp)
+                    if _engine.mix_rounds(W, Xp, Yp, math.ceil(times), workspace=self._wspace()):
+                        X, times_done = Yp[:, :P], math.ceil(times)
+                        stopping_criterion = True
             while not stopping_criterion:
                 _engine.mix_round(W, X, Y, dev_sq=dev_sq if fused_dev else None,
-                                  dev_max=dev_max if fused_dev else None, workspace=self._wspace())
+                                  dev_max=dev_max if fused_dev else None, workspace=self._wspace(),
+                                  tiled=tl)
                 X, Y = Y, X
                 times_done += 1
                 stopping_criterion = self._update_stopping_criterion(
                     X, times_done, times, eps, fused=(dev_max if fused_dev else None))
+            if tl:
+                X = _engine.from_tiled(X, P)
 
             self._write_back(X, agents)
 
@@ -164,6 +184,14 @@ class Mixer(object):
     # runs on a column-tiled copy of X: a row-major step reads a 16-byte segment of every row
     # (c4 torus, 4096 x 2^18: 486 rounds/s row-major against 2179 tiled, profiles/r10/trace4096)
     _TRACE_TILED_ABOVE = 1024
+
+    def _loop_tile_cols(self, W, P):
+        """Tile width of the column-tiled layout for the round loop above _TRACE_TILED_ABOVE
+        agents (the LDS tile kernels: paths 1, 4, 5), else None (row-major)."""
+        if W.n_rows <= self._TRACE_TILED_ABOVE or W.n_src != W.n_rows:
+            return None
+        plan = _engine.plan_shape(W, P, deviation=True, tile_cols=-1)
+        return plan["tile_cols"] if plan["path"] in (1, 4, 5) and plan["tile_cols"] > 0 else None
 
     def _mix_traced(self, W, X, times, eps):
         """mixer.py:27-32 with eps set, in passes of K rounds (dl_mix_rounds_trace): each pass

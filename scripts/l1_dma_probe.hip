@@ -33,6 +33,12 @@ constexpr int SLICE_F4 = (MB + NROWS) * 8; // float4 per slice image: 2048 = 32 
 #ifndef FRAG_FIRST
 #define FRAG_FIRST 1
 #endif
+#ifndef ORDER_ST
+#define ORDER_ST 0
+#endif
+#ifndef NODMA
+#define NODMA 0   // 1: no staging at all (the MFMA loop on whatever the ring holds)
+#endif
 #ifndef NOMMA
 #define NOMMA 0   // 1: stream the slices only (no fragment reads, no MFMAs)
 #endif
@@ -54,6 +60,7 @@ __global__ void __launch_bounds__(NT) l1_dma(const float *__restrict__ X, long l
     // DMA instruction i of a slice (32 per slice, 4 per wave): LDS float4 slots [64i, 64i + 64);
     // lane -> slot 64i + lane -> (row, position) -> the chunk that position holds
     auto issue = [&](int sl, int buf) {
+        if (NODMA) return;
         const int k0 = sl * BK;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -111,6 +118,14 @@ __global__ void __launch_bounds__(NT) l1_dma(const float *__restrict__ X, long l
 #if FRAG_FIRST
             __builtin_amdgcn_sched_barrier(0);
 #endif
+#if ORDER_ST   // k step outer, N-tile inner: five independent accumulators between dependent MFMAs
+#pragma unroll
+            for (int s = 0; s < 8; ++s)
+#pragma unroll
+                for (int t = 0; t < 5; ++t)
+                    acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(s < 4 ? a0[s] : a1[s - 4],
+                                                                  b[t][s >> 2][s & 3], acc[t], 0, 0, 0);
+#else
 #pragma unroll
             for (int t = 0; t < 5; ++t) {
 #pragma unroll
@@ -120,6 +135,7 @@ __global__ void __launch_bounds__(NT) l1_dma(const float *__restrict__ X, long l
                 for (int s = 0; s < 4; ++s)
                     acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[s], b[t][1][s], acc[t], 0, 0, 0);
             }
+#endif
         }
         __builtin_amdgcn_s_waitcnt(0);
         __syncthreads();

@@ -206,3 +206,33 @@ def test_plan_csr_reports_path5_and_refuses_bad_promise(cuda):
     with pytest.raises(Exception):
         Y = torch.empty(4096, 64, device=cuda)
         E.mix_round(W, torch.zeros(4096, 64, device=cuda), Y)
+
+
+@pytest.mark.parametrize("times,eps", [(1, 0.5), (2, None)])
+def test_mixer_4096_irregular_models(cuda, times, eps):
+    """The drop-in Mixer over 4096 models on the Barabasi-Albert graph (the reference's
+    dict-of-dicts topology, mixer.py:43-49): the round loop runs on a column-tiled copy of X
+    through plan path 5 -- the reference loop's round count and bits (mixer.py:18-41)."""
+    import logging
+    from oracle import mixer_ref as M
+    from distributed_learning_amd.utils.consensus_simple import Mixer
+    from distributed_learning_amd.utils.consensus_simple import mixer as mixer_mod
+    from distributed_learning_amd import engine as E
+    csr = ba(4096, 2, 3)
+    n = csr.n_rows
+    topo = {i: {int(csr.col[e]): float(csr.w[e]) for e in range(csr.rowptr[i], csr.rowptr[i + 1])}
+            for i in range(n)}
+    torch.manual_seed(5)
+    models = {i: torch.nn.Linear(24, 8).to(cuda) for i in range(n)}
+    X0 = np.stack([torch.cat([p.data.reshape(-1) for p in models[i].parameters()]).cpu().numpy()
+                   for i in range(n)])
+    rp, cl, w = M.topology_to_csr(topo)
+    want, want_n = M.mixer_mix(X0, rp, cl, w, times=times, eps=eps)
+    m = Mixer(models, topo, logging.getLogger("ba4096"))
+    W = m._device_csr()
+    assert m._loop_tile_cols(W, X0.shape[1]) == 4
+    assert E.plan_shape(W, X0.shape[1], tile_cols=4)["path"] == 5
+    assert m.mix(times=times, eps=eps) == want_n
+    got = np.stack([torch.cat([p.data.reshape(-1) for p in models[i].parameters()]).cpu().numpy()
+                    for i in range(n)])
+    assert np.array_equal(bits(got), bits(want))

@@ -1,5 +1,8 @@
-"""Mixer.mix(times, eps) wall time: the one-launch device loop (dl_mix_until) against the
-per-round host loop (dl_mix_round + 4-byte readback per round), same models, same result.
+"""Mixer.mix(times, eps) wall time: the one-launch device loop (dl_mix_until) against the path
+the Mixer takes when that loop is switched off (dl_mix_until_fits forced False): traced passes
+(dl_mix_rounds_trace + one readback per pass) with eps set, one dl_mix_rounds pass without --
+the per-round host loop (dl_mix_round + 4-byte readback per round) before round 2; same models,
+same result.
 Usage: python scripts/mixer_eps_probe.py  (GPU)."""
 import logging
 import os
@@ -54,7 +57,7 @@ def run(n, dims, times, eps, resident, reps=20):
 
 def main():
     print(f"{'agents':>6} {'params':>7} {'times':>5} {'eps':>7} {'rounds':>6} "
-          f"{'device ms':>9} {'host ms':>8} {'x':>6}", flush=True)
+          f"{'device ms':>9} {'passes ms':>9} {'x':>6}", flush=True)
     for n, dims in [(5, (30, 17, 5)), (8, (40, 20, 5)), (16, (20, 16, 4))]:
         for times, eps in [(1, 1e-3), (1, 1e-5), (10, None)]:
             td, kd, od = run(n, dims, times, eps, True)
@@ -62,7 +65,7 @@ def main():
             assert kd == kh and torch.equal(od, oh), (n, dims, times, eps, kd, kh)
             P = od.shape[1]
             print(f"{n:>6} {P:>7} {times:>5} {str(eps):>7} {kd:>6} {td * 1e3:>9.3f} "
-                  f"{th * 1e3:>8.3f} {th / td:>6.1f}", flush=True)
+                  f"{th * 1e3:>9.3f} {th / td:>6.1f}", flush=True)
 
 
 if __name__ == "__main__":

@@ -11,9 +11,9 @@ OBJ=distributed-learning_amd/_lib/obj
 OUT=scripts/_build/$NAME
 mkdir -p $OUT
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-result"
-VAR="capi mix_tile mix_trace mix_multi"
+VAR="capi mix_tile mix_trace mix_multi mlp_fused"
 for f in $VAR; do /opt/rocm/bin/hipcc $FLAGS "$@" -c $SRC/$f.hip -o $OUT/$f.o & done
 wait
-OTHERS=$(ls $OBJ/*.o | grep -v -E "/(capi|mix_tile|mix_trace|mix_multi)\.o$")
+OTHERS=$(ls $OBJ/*.o | grep -v -E "/(capi|mix_tile|mix_trace|mix_multi|mlp_fused)\.o$")
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT/libdlamd.so $OUT/*.o $OTHERS
 echo "built $OUT/libdlamd.so ($*)"

@@ -178,6 +178,15 @@ inline int32_t local_src(const dl_mix_args *a) {
     return a->n_local_src > 0 ? a->n_local_src : a->W.n_rows;
 }
 
+// An irregular graph of more than 2048 agents takes the register-head + LDS-tail kernel (path 5)
+// even when its whole CSR fits LDS beside the tile: above 2048 agents the tile is one 4-column
+// chunk either way, and path 1's per-lane CSR loop from LDS (row pointers, weights and rows read
+// per entry, a wave as long as its longest row) runs Barabasi-Albert m = 1 at 250 rounds/s
+// against 430 for path 5 (4096 x 2^18, `bench.py --workload c4-ba --irregular ba1`).
+bool prefer_reg_tail(const dl_csr &W, int32_t R, int c) {
+    return c == 1 && R > 2048 && W.uniform_row_nnz == 0 && dl::reg_head_rows(W.min_row_nnz) > 0;
+}
+
 // Register-CSR plan for c chunks -- path 4 (regular, 5 entries per row, all in registers) or
 // path 5 (rows of >= min_row_nnz entries: register head + LDS tail) -- or false when neither
 // applies.
@@ -242,8 +251,8 @@ int plan_mix(const dl_mix_args *a, Plan *pl) {
         const int64_t tile = (int64_t)R * c * 16;
         const int64_t scratch = want_dev ? (int64_t)(dl::kTileThreads / 64) * c * 16 : 0;
         const int64_t lds = tile + csr + scratch;
-        if ((csr == 0 || lds > dl::kLdsBytes || force_reg) && R <= 65535 &&
-            plan_reg(a, c, want_dev, pl))
+        if ((csr == 0 || lds > dl::kLdsBytes || force_reg || prefer_reg_tail(a->W, R, c)) &&
+            R <= 65535 && plan_reg(a, c, want_dev, pl))
             return DL_OK;
         if (csr == 0 || R > 65535 || (int64_t)R * c > (int64_t)dl::kRowsPerThread * dl::kTileThreads ||
             lds > dl::kLdsBytes)
@@ -270,7 +279,8 @@ int plan_mix(const dl_mix_args *a, Plan *pl) {
         pl->scratch_off = (uint32_t)(tile + csr);
         return DL_OK;
     }
-    if (force_reg && R <= 65535 && a->n_params % 4 == 0 && plan_reg(a, 1, want_dev, pl))
+    if ((force_reg || prefer_reg_tail(a->W, R, 1)) && R <= 65535 && a->n_params % 4 == 0 &&
+        plan_reg(a, 1, want_dev, pl))
         return DL_OK;
     if (csr > 0 && R <= 65535 && !force_gather) {
         for (int c = cmax; c >= 1; c >>= 1) {

@@ -77,12 +77,14 @@ def dense_irregular(n, lo, hi, seed, row_stochastic=False):
 CASES = {
     # name: (graph builder, register head the planner must pick, forced)
     "ba2_4096": (lambda: ba(4096, 2, 1), 3, False),   # the fixture-B construction at c4 scale
-    # a tree (leaves have 2 entries); its CSR (72 KiB) fits LDS beside the tile, so path 5 is
-    # forced (DLAMD_FORCE_REG=1) to cover the 2-entry head
-    "ba1_4096": (lambda: ba(4096, 1, 2), 2, True),
+    # a tree (leaves have 2 entries): its CSR (72 KiB) fits LDS beside the tile, and path 5
+    # still runs it (irregular, > 2048 agents: 430 vs 250 rounds/s for path 1's CSR loop)
+    "ba1_4096": (lambda: ba(4096, 1, 2), 2, False),
     "deg5to9_4096": (lambda: dense_irregular(4096, 4, 8, 3), 5, False),
     "deg9to12_2048": (lambda: dense_irregular(2048, 8, 11, 4), 5, False),   # 2 rows per thread
-    "ba2_3001": (lambda: ba(3001, 2, 5), 3, True),    # ragged last row pass (forced: fits LDS)
+    "ba2_3001": (lambda: ba(3001, 2, 5), 3, False),   # ragged last row pass (CSR fits LDS)
+    # 2048 agents, CSR fits LDS beside a 2-chunk tile: path 5 only when forced
+    "ba2_2048": (lambda: ba(2048, 2, 6), 3, True),
     # a 3-entry head whose tail fits LDS at 6 B per entry but not at 8 B (the split format)
     "deg2to7_4096": (lambda: rim(4096, 2, 7, 1), 3, False),
 }

@@ -419,8 +419,19 @@ def run_c3(args, dev, rank, world):
     gbs = mix_bytes / (mix_ms / 1e3) / 1e9
     if rank != 0:
         return
-    # HBM bytes per launch from the committed PMC passes of this workload (profiles/r09/c3)
-    c3_path = os.path.join(ROOT, "profiles", "r09", "c3", "summary.json")
+    # HBM bytes per launch from the committed PMC passes of this workload (profiles/r10/c3, r09
+    # before it), and the kernel's rocprofv3 average over the same command's timed graph steps
+    c3_path = os.path.join(ROOT, "profiles", "r10", "c3", "summary.json")
+    if not os.path.exists(c3_path):
+        c3_path = os.path.join(ROOT, "profiles", "r09", "c3", "summary.json")
+    prof_us = None
+    try:
+        with open(c3_path) as f:
+            for kname, e in json.load(f)["kernels"].items():
+                if "mlp_fused_kernel" in kname and ann.path == "fused":
+                    prof_us = e.get("avg_us")
+    except (OSError, ValueError, KeyError):
+        pass
     c3_grad_traffic, c3_src = (traffic_from_profile("mlp_fused_kernel", c3_path)
                                if ann.path == "fused" and args.c3_layout == "rows"
                                else (None, None))
@@ -435,6 +446,12 @@ def run_c3(args, dev, rank, world):
                      f"{grad_isolated_ms:.4f} ms)" if use_graph else
                      " (HIP events around 20 back-to-back launches)"),
                  "flops_per_launch": flops, "launch_ms": grad_ms,
+                 # the same kernel under rocprofv3 (committed profile of this command): its
+                 # average duration and the fraction it gives
+                 "rocprof_launch_ms": prof_us / 1e3 if prof_us else None,
+                 "rocprof_frac": (flops / (prof_us / 1e6) / 1e12 / FP32_MFMA_PEAK_TFLOPS
+                                  if prof_us else None),
+                 "rocprof_source": os.path.relpath(c3_path, ROOT) if prof_us else None,
                  "arithmetic": "fp32 GEMMs: layer 1, dW1 and the hidden forward / dZ GEMMs on the "
                                "bf16 matrix cores as exact 3-way bf16 splits (six products, "
                                "csrc/mlp_fused.hip), the hidden dW tiles and the head on the fp32 "

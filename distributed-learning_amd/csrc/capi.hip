@@ -279,8 +279,8 @@ int plan_mix(const dl_mix_args *a, Plan *pl) {
         pl->scratch_off = (uint32_t)(tile + csr);
         return DL_OK;
     }
-    if ((force_reg || prefer_reg_tail(a->W, R, 1)) && R <= 65535 && a->n_params % 4 == 0 &&
-        plan_reg(a, 1, want_dev, pl))
+    if ((force_reg || (prefer_reg_tail(a->W, R, 1) && !force_gather)) && R <= 65535 &&
+        a->n_params % 4 == 0 && plan_reg(a, 1, want_dev, pl))
         return DL_OK;
     if (csr > 0 && R <= 65535 && !force_gather) {
         for (int c = cmax; c >= 1; c >>= 1) {

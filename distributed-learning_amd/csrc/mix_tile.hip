@@ -386,20 +386,25 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
                 for (; t < t1; ++t) axpy4(acc, tail_w(t), tile[tail_c(t)]);
                 return acc;
             }
-            if constexpr (TU > 1) for (; t + TU <= t1; t += TU) {
-                float w4[TU];
-                uint32_t c4[TU];
+            auto pairs = [&](uint32_t t0, float (&w4)[TU], uint32_t (&c4)[TU]) {
 #pragma unroll
                 for (int u = 0; u < TU; ++u) {
                     if (PACK) {
-                        const uint2 pr = ltp[t + u];
+                        const uint2 pr = ltp[t0 + u];
                         w4[u] = __uint_as_float(pr.x);
                         c4[u] = pr.y;
                     } else {
-                        w4[u] = ltw[t + u];
-                        c4[u] = ltc[t + u];
+                        w4[u] = ltw[t0 + u];
+                        c4[u] = ltc[t0 + u];
                     }
                 }
+            };
+            // (software-pipelining the next step's pair reads over this step's tile reads and
+            // folds measured 3 % slower: c4-ba 367 vs 379 rounds/s)
+            if constexpr (TU > 1) for (; t + TU <= t1; t += TU) {
+                float w4[TU];
+                uint32_t c4[TU];
+                pairs(t, w4, c4);
                 float4 v4[TU];
 #pragma unroll
                 for (int u = 0; u < TU; ++u) v4[u] = tile[c4[u]];

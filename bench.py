@@ -84,6 +84,11 @@ def parse():
                    help="c2-gossip: traced passes (Mixer.mix(times, eps) stop test every round)")
     p.add_argument("--no-graph", action="store_true", help="c3/c5: eager launches, no hipGraph")
     p.add_argument("--streams", type=int, default=8, help="c5: HIP streams the agents share")
+    p.add_argument("--c3-emit", default="grad", choices=["step", "grad"],
+                   help="c3: what the fused gradient kernel writes -- step: the local step "
+                        "X - lr G, which the round then mixes (one matrix read); grad: G, and "
+                        "the round forms X - lr G (reads X and G; default: 3503 vs 3159 "
+                        "steps/s, profiles/r10/c3_step)")
     p.add_argument("--c3-layout", default="rows", choices=["rows", "tiled"],
                    help="c3: resident layout of X and G (tiled: the fused gradient kernel "
                         "addresses the round's column tiles; measured equal overall)")
@@ -346,8 +351,9 @@ def c3_cpu_baseline(ann, csr, lr, n_agents_sample=16):
 def run_c3(args, dev, rank, world):
     """Config c3: MLP consensus SGD.  One step = batched per-agent gradients of ANNModel on a
     synthetic MNIST-shaped batch (4 forward + xent + 7 backward fp32-MFMA batched GEMMs, weight
-    gradients written straight into G's rows) followed by the fused round X <- W (X - lr G) with
-    the disagreement, over a random 4-regular graph of 256 agents.  N>1: one independent
+    gradients written straight into G's rows, or with --c3-emit step the local step X - lr G) followed
+    by the round X <- W (X - lr G) with the disagreement, over a random 4-regular graph of 256
+    agents.  N>1: one independent
     256-agent system per GPU (replicas)."""
     from distributed_learning_amd import engine
     from distributed_learning_amd.networks.batched_ann import BatchedANN
@@ -368,8 +374,8 @@ def run_c3(args, dev, rank, world):
         X0 = torch.nn.functional.pad(X0, (0, P_pad - P))
         eng = engine.GossipEngine(csr, P_pad, device=dev, X=X0, layout="rows")
     del X0
-    sgd = MLPConsensusSGD(ann, eng, data, labels, lr, deviation=True)
-    G = sgd.G
+    sgd = MLPConsensusSGD(ann, eng, data, labels, lr, deviation=True,
+                          emit=args.c3_emit if ann.path == "fused" else "grad")
     stream = torch.cuda.current_stream(dev)
     # phase times: n_ev back-to-back launches of each phase between one pair of HIP events on
     # the launch stream, after warmup steps that load every kernel's code object.  The round's
@@ -384,13 +390,10 @@ def run_c3(args, dev, rank, world):
     torch.cuda.synchronize()
     e0.record(stream)
     for i in range(n_ev):
-        if eng.layout == "tiled":
-            ann.gradients(eng.X, data, labels, G)
-        else:
-            ann.gradients(eng.X[:, :P], data, labels, G[:, :P])
+        sgd.gradients()
     e1.record(stream)
     for i in range(n_ev):
-        eng.round(G=G, lr=lr, deviation=True)
+        sgd.round()
     e2.record(stream)
     torch.cuda.synchronize()
     grad_ms = e0.elapsed_time(e1) / n_ev
@@ -414,15 +417,18 @@ def run_c3(args, dev, rank, world):
     grad_ms = max_over_ranks(grad_ms, world, dev)
     mix_ms = max_over_ranks(mix_ms, world, dev)
     flops = ann.flops_per_step()
-    mix_bytes = 12 * n * P       # algorithmic: the real columns only (padding is overhead)
+    # algorithmic: the real columns only (padding is overhead); read T (step emission) or X and
+    # G, write X'
+    mix_bytes = (8 if sgd.emit == "step" else 12) * n * P
     tflops = flops / (grad_ms / 1e3) / 1e12
     gbs = mix_bytes / (mix_ms / 1e3) / 1e9
     if rank != 0:
         return
     # HBM bytes per launch from the committed PMC passes of this workload (profiles/r10/c3, r09
     # before it), and the kernel's rocprofv3 average over the same command's timed graph steps
-    c3_path = os.path.join(ROOT, "profiles", "r10", "c3", "summary.json")
-    if not os.path.exists(c3_path):
+    c3_path = os.path.join(ROOT, "profiles", "r10", "c3" if sgd.emit == "grad" else "c3_step",
+                           "summary.json")
+    if not os.path.exists(c3_path) and sgd.emit == "grad":
         c3_path = os.path.join(ROOT, "profiles", "r09", "c3", "summary.json")
     prof_us = None
     try:
@@ -440,7 +446,8 @@ def run_c3(args, dev, rank, world):
     grad_roof = {"bound": "mfma", "achieved": tflops, "peak": FP32_MFMA_PEAK_TFLOPS,
                  "unit": "TFLOP/s", "frac": tflops / FP32_MFMA_PEAK_TFLOPS,
                  "traffic": c3_grad_traffic, "traffic_source": c3_src if c3_grad_traffic else None,
-                 "kernel": ("mlp_fused_kernel" if ann.path == "fused" else
+                 "kernel": ("mlp_fused_kernel" + (" (writes X - lr G)" if sgd.emit == "step"
+                                                  else "") if ann.path == "fused" else
                             "dl_bgemm x11 + dl_xent_grad") + (
                      " (graph step time minus the round phase; back-to-back launches: "
                      f"{grad_isolated_ms:.4f} ms)" if use_graph else
@@ -460,7 +467,8 @@ def run_c3(args, dev, rank, world):
                 "frac": gbs / HBM_PEAK_GBS, "traffic": c3_mix_traffic,
                 "traffic_source": c3_src if c3_mix_traffic else None,
                 "kernel": "mix_tile_kernel (+dev_reduce), HIP events around 20 back-to-back "
-                          "rounds", "bytes_per_launch": mix_bytes,
+                          "rounds" + (" of T = X - lr G" if sgd.emit == "step" else
+                                      " fusing X - lr G"), "bytes_per_launch": mix_bytes,
                 "launch_ms": mix_ms}
     dominant = grad_roof if grad_ms >= mix_ms else mix_roof
     cpu = None
@@ -488,7 +496,7 @@ def run_c3(args, dev, rank, world):
         "config": {"workload": "c3: ANNModel consensus SGD (batched per-agent MFMA gradients + "
                                "fused round + deviation)",
                    "agents": n, "params": P, "params_padded": P_pad, "batch": B, "lr": lr,
-                   "layout": eng.layout, "gradient_path": ann.path,
+                   "layout": eng.layout, "gradient_path": ann.path, "emit": sgd.emit,
                    "graph": "random 4-regular",
                    "weights": f"best-constant {wconst:.6f}",
                    "launch": "hipGraph replay per step" if use_graph else "eager",

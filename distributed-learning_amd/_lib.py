@@ -96,7 +96,7 @@ class DlMlpArgs(ctypes.Structure):
     _fields_ = [("n_agents", _i32), ("batch", _i32), ("input_dim", _i32), ("hidden_dim", _i32),
                 ("output_dim", _i32), ("X", _vp), ("ldx", _i64), ("data", _vp), ("s_data", _i64),
                 ("labels", _vp), ("s_labels", _i64), ("G", _vp), ("ldg", _i64), ("loss", _vp),
-                ("tile_cols", _i32)]
+                ("tile_cols", _i32), ("out_mode", _i32), ("lr", ctypes.c_float)]
 
 
 EPI = {"none": 0, "bias": 1, "bias_relu": 2, "bias_tanh": 3, "bias_elu": 4, "drelu": 5,
@@ -144,7 +144,7 @@ SIGNATURES = {
     "dl_lds_slot_order": (_i32, [_i32, _i32, _vp, _i32, _i64, ctypes.c_uint64, _vp, _vp]),
 }
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 _lib = None
 
 

@@ -1267,10 +1267,14 @@ int dl_mlp_grad(const dl_mlp_args *a, dl_stream_t stream) {
     const size_t xb = T ? tb : ((size_t)a->n_agents - 1) * a->ldx * 4 + P * 4;
     const size_t gb = T ? tb : ((size_t)a->n_agents - 1) * a->ldg * 4 + P * 4;
     if (overlaps(a->X, xb, a->G, gb)) return fail(DL_ERR_INVALID, "dl_mlp_grad: G overlaps X");
+    if (a->out_mode != 0 && a->out_mode != 1)
+        return fail(DL_ERR_INVALID, "dl_mlp_grad: out_mode must be 0 (gradient) or 1 (step)");
+    if (a->out_mode == 1 && T == 0 && a->ldg != a->ldx)
+        return fail(DL_ERR_INVALID, "dl_mlp_grad: out_mode 1 needs ldg == ldx");
     hipError_t e = dl::launch_mlp_fused(a->X, a->ldx, a->data, a->s_data, a->labels, a->s_labels,
                                         a->G, a->ldg, a->loss, a->n_agents, a->input_dim,
-                                        a->hidden_dim, a->output_dim, T,
-                                        static_cast<hipStream_t>(stream));
+                                        a->hidden_dim, a->output_dim, T, a->out_mode == 1,
+                                        a->lr, static_cast<hipStream_t>(stream));
     return e == hipSuccess ? DL_OK : hip_fail(e, "mlp_fused launch");
 }
 

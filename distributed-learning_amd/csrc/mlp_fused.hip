@@ -197,19 +197,19 @@ __device__ __forceinline__ void gstore(float *p, float v) {
 #endif
 }
 
-// Store a finished 32 x 32 MFMA tile: register r holds row i0 + (r & 3) + 8 (r >> 2) of this
-// lane's column j (C/D map); every store instruction writes two 128-B runs.  (Issuing these
-// stores interleaved with the next tile's MFMA chain measured slower: dW1 53 -> 64 us.)
+// The G addresses of this lane's part of a finished 32 x 32 MFMA tile: register r holds row
+// i0 + (r & 3) + 8 (r >> 2) of column j (C/D map); every store instruction writes two 128-B runs.
 // Column j == cols is the ones column of the input image: its values are the bias gradient.
-template <typename M>
-__device__ __forceinline__ void store_tile(const f32x16 &v, int i0, int j, const M &m, int rows,
-                                           int cols, const M &bias) {
+// f(r, address) for every register that lands in the matrix.
+template <typename M, typename F>
+__device__ __forceinline__ void tile_addrs(int i0, int j, const M &m, int rows, int cols,
+                                           const M &bias, F f) {
     if (j > cols) return;
     if (j == cols) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int i = i0 + (r & 3) + 8 * (r >> 2);
-            if (i < rows) gstore(bias.at(0, i), v[r]);
+            if (i < rows) f(r, bias.at(0, i));
         }
         return;
     }
@@ -220,18 +220,55 @@ __device__ __forceinline__ void store_tile(const f32x16 &v, int i0, int j, const
             float *p = m.at(i0, j);
             const int ld = m.ld;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) gstore(p + ((r & 3) + 8 * (r >> 2)) * ld, v[r]);
+            for (int r = 0; r < 16; ++r) f(r, p + ((r & 3) + 8 * (r >> 2)) * ld);
         } else {
 #pragma unroll
-            for (int r = 0; r < 16; ++r) gstore(m.at(i0 + (r & 3) + 8 * (r >> 2), j), v[r]);
+            for (int r = 0; r < 16; ++r) f(r, m.at(i0 + (r & 3) + 8 * (r >> 2), j));
         }
         return;
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         const int i = i0 + (r & 3) + 8 * (r >> 2);
-        if (i < rows) gstore(m.at(i, j), v[r]);
+        if (i < rows) f(r, m.at(i, j));
     }
+}
+
+// What the kernel writes at a G address (dl_mlp_args.out_mode): the gradient g, or (STEP) the
+// local SGD step t = x - lr g of the same parameter, rounded fl(x - fl(lr g)) exactly as
+// dl_mix_round's fused step (mix_tile.hip sgd_step), so a plain round of T is bit-identical to
+// the fused round of X and G -- and reads one matrix instead of two.  x is read from X at the
+// element's own address shifted by dx = G - X (the two share the agent-row geometry), into
+// registers before the tile's MFMA chain (xo), so its latency hides behind the chain and every
+// store of the tile issues back to back.
+template <bool STEP>
+struct GOut {
+    float lr;
+    int64_t dx;   // G address - X address of the same element, in floats
+    template <typename M>
+    __device__ __forceinline__ void prefetch(f32x16 &xo, int i0, int j, const M &m, int rows,
+                                             int cols, const M &bias) const {
+        if constexpr (STEP)
+            tile_addrs(i0, j, m, rows, cols, bias,
+                       [&](int r, float *p) { xo[r] = *(const float *)(p - dx); });
+    }
+    __device__ __forceinline__ void put(float *p, float v, float x) const {
+        if constexpr (STEP) gstore(p, x - lr * v);
+        else gstore(p, v);
+    }
+    __device__ __forceinline__ void put(float *p, float v) const {   // x read here (small tiles)
+        if constexpr (STEP) gstore(p, *(const float *)(p - dx) - lr * v);
+        else gstore(p, v);
+    }
+};
+
+// Store a finished tile (xo: the prefetched x values of a STEP output).  (Issuing these stores
+// interleaved with the next tile's MFMA chain measured slower: dW1 53 -> 64 us.)
+template <bool STEP, typename M>
+__device__ __forceinline__ void store_tile(const f32x16 &v, const f32x16 &xo, int i0, int j,
+                                           const M &m, int rows, int cols, const M &bias,
+                                           const GOut<STEP> &o) {
+    tile_addrs(i0, j, m, rows, cols, bias, [&](int r, float *p) { o.put(p, v[r], xo[r]); });
 }
 
 // plain row-major matrix (the agent's input batch)
@@ -665,15 +702,17 @@ __device__ __forceinline__ void backward_dz_one(int dh, const float *dZ, int ldz
 // overlap the next tile's MFMAs (one accumulator: the 32x32x2 issue interval equals its
 // dependent latency).  C/D: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5): every
 // store instruction writes two 128-B runs.
-template <typename M>
+template <bool STEP, typename M>
 __device__ __forceinline__ void weight_grad_hidden(const float *dZ, const float *Hin, int dh,
-                                                   const M &gW, const M &gb) {
+                                                   const M &gW, const M &gb,
+                                                   const GOut<STEP> &o) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (int t = wave; t < 25; t += 8) {    // one tile at a time (one accumulator)
-        f32x16 acc;
+        f32x16 acc, xo;
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[r] = 0.f;
         const int ia = (t / 5) * 32 + (lane & 31), jb = (t % 5) * 32 + (lane & 31);
+        o.prefetch(xo, (t / 5) * 32 + 4 * (lane >> 5), jb, gW, dh, dh, gb);
 #if MLP_PROBE_MODE != 7   // measurement only: 7 = no hidden-layer dW MFMAs
 #pragma unroll 8
         for (int ks = 0; ks < MB / 2; ++ks) {
@@ -682,7 +721,7 @@ __device__ __forceinline__ void weight_grad_hidden(const float *dZ, const float 
         }
 #endif
 #if MLP_PROBE_MODE != 6   // measurement only: 6 = no hidden-layer dW stores
-        store_tile(acc, (t / 5) * 32 + 4 * (lane >> 5), jb, gW, dh, dh, gb);
+        store_tile(acc, xo, (t / 5) * 32 + 4 * (lane >> 5), jb, gW, dh, dh, gb, o);
 #endif
     }
 }
@@ -701,6 +740,7 @@ struct MlpArgs {
     int32_t tsh;        // column-tiled X and G: log2 of the tile width (0 = row-major)
     int64_t tstride;    // column-tiled: n_agents * T floats per tile
     uint64_t *stamps;   // nullable: per-phase wall clocks of every workgroup (scripts/mlp_probe)
+    float lr;           // STEP: G receives x - lr g
 };
 
 #define STAMP(i) \
@@ -710,7 +750,8 @@ struct MlpArgs {
 // 3-way split (bf16x6, above; the hidden dW tiles stay on the fp32 MFMA: a per-fragment split of
 // both batch-strided operands measured no faster); false = everything on the fp32 MFMA
 // (DLAMD_MLP_L1=fp32, a measurement knob)
-template <bool TILED, bool L1X6>
+// STEP: G receives the local step T = X - lr G instead of the gradient (GOut)
+template <bool TILED, bool L1X6, bool STEP>
 __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     float *H1 = lds, *H2 = lds + H_FLOATS, *H3 = lds + 2 * H_FLOATS;
@@ -729,6 +770,7 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
         Gr = {p.G + (int64_t)a * p.ldg, 0, 0};
     }
     const float *x = p.data + (int64_t)a * p.s_data;
+    const GOut<STEP> go{p.lr, (int64_t)(Gr.base - Xr.base)};
     // parameter offsets in the Mixer flatten order (fc1.w, fc1.b, fc2.w, fc2.b, ...)
     STAMP(0);
     if (p.stamps && threadIdx.x == 0) p.stamps[(int64_t)blockIdx.x * 16 + 14] = __builtin_amdgcn_s_memtime();
@@ -1009,8 +1051,8 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int i = 4 * (lane >> 4) + r;
-                if (i < dout && j < dh) gstore(Gr.at(o_w4 + i * dh + j), acc[r]);
-                if (i < dout && j == dh) gstore(Gr.at(o_b4 + i), acc[r]);   // H3's ones column
+                if (i < dout && j < dh) go.put(Gr.at(o_w4 + i * dh + j), acc[r]);
+                if (i < dout && j == dh) go.put(Gr.at(o_b4 + i), acc[r]);   // H3's ones column
             }
         }
     }
@@ -1020,14 +1062,14 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
                     [&] { load_all_wt(t5, mat(Xr, o_w3, dh), dh, dh); });
     __syncthreads();
     STAMP(5);
-    weight_grad_hidden(H3, H2, dh, mat(Gr, o_w3, dh), mat(Gr, o_b3, 0));
+    weight_grad_hidden(H3, H2, dh, mat(Gr, o_w3, dh), mat(Gr, o_b3, 0), go);
     __syncthreads();
     STAMP(6);
     backward_dz_all<L1X6>(dh, H3, LDH, H2, stage, 1, t5,    // dZ2 into H2; dZ1's W2^T rolls in
                     [&](int sl) { t5[sl].load(mat(Xr, o_w2, dh), dh, dh, sl * BK); });
     __syncthreads();
     STAMP(7);
-    weight_grad_hidden(H2, H1, dh, mat(Gr, o_w2, dh), mat(Gr, o_b2, 0));
+    weight_grad_hidden(H2, H1, dh, mat(Gr, o_w2, dh), mat(Gr, o_b2, 0), go);
     __syncthreads();
     STAMP(8);
     backward_dz_all<L1X6>(dh, H2, LDH, H1, stage, 0, t5, [](int) {});   // dZ1 into H1
@@ -1107,9 +1149,10 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
             const int ntc = min(CW / 32, (din + 1 - c0 + 31) / 32);
             for (int it = wave; it < 5 * ntc; it += 8) {
                 const int nt = it % ntc, t = it / ntc;
-                f32x16 big, sml;
+                f32x16 big, sml, xo;
 #pragma unroll
                 for (int q = 0; q < 16; ++q) big[q] = sml[q] = 0.f;
+                go.prefetch(xo, 32 * t + 4 * hh, c0 + 32 * nt + r, gw1, dh, din, gb1);
 #pragma unroll
                 for (int ks = 0; ks < MB / 16; ++ks) {
                     const int b = 16 * ks + 8 * hh;
@@ -1123,7 +1166,7 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
                     mfma32_x6(ah, am, al, bh, bm, bl, big, sml);
                 }
                 big += sml;
-                store_tile(big, 32 * t + 4 * hh, c0 + 32 * nt + r, gw1, dh, din, gb1);
+                store_tile(big, xo, 32 * t + 4 * hh, c0 + 32 * nt + r, gw1, dh, din, gb1, go);
             }
             __syncthreads();
         };
@@ -1169,9 +1212,10 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
             for (int it = wave; it < 5 * ntc; it += 8) {
                 const int nt = it % ntc, t = it / ntc;
                 const int nl = 32 * nt + (lane & 31);
-                f32x16 acc;
+                f32x16 acc, xo;
 #pragma unroll
                 for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+                go.prefetch(xo, 32 * t + 4 * (lane >> 5), c0 + nl, gw1, dh, din, gb1);
 #if MLP_PROBE_MODE != 5   // measurement only: 5 = no dW1 MFMAs
 #pragma unroll 8
                 for (int ks = 0; ks < MB / 2; ++ks) {
@@ -1180,7 +1224,7 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
                 }
 #endif
 #if MLP_PROBE_MODE != 4   // measurement only: 4 = no dW1 stores
-                store_tile(acc, 32 * t + 4 * (lane >> 5), c0 + nl, gw1, dh, din, gb1);
+                store_tile(acc, xo, 32 * t + 4 * (lane >> 5), c0 + nl, gw1, dh, din, gb1, go);
 #endif
             }
             __syncthreads();
@@ -1200,11 +1244,11 @@ int mlp_fused_supported(int batch, int din, int dh, int dout) {
 hipError_t launch_mlp_fused(const float *X, int64_t ldx, const float *data, int64_t s_data,
                             const int32_t *labels, int64_t s_lab, float *G, int64_t ldg,
                             float *loss, int n_agents, int din, int dh, int dout, int tile_cols,
-                            hipStream_t s) {
+                            bool step, float lr, hipStream_t s) {
     int tsh = 0;
     while (tile_cols > 0 && (1 << tsh) < tile_cols) ++tsh;
     MlpArgs p{X, ldx, data, s_data, labels, s_lab, G, ldg, loss, din, dh, dout, tsh,
-              (int64_t)n_agents * tile_cols, nullptr};
+              (int64_t)n_agents * tile_cols, nullptr, lr};
     static const bool l1_fp32 = [] {
         const char *v = getenv("DLAMD_MLP_L1");
         return v && v[0] == 'f';
@@ -1216,9 +1260,13 @@ hipError_t launch_mlp_fused(const float *X, int64_t ldx, const float *data, int6
                            LDS_FLOATS * sizeof(float), s, p);
         return hipGetLastError();
     };
-    if (tile_cols > 0)
-        return l1_fp32 ? go(mlp_fused_kernel<true, false>) : go(mlp_fused_kernel<true, true>);
-    return l1_fp32 ? go(mlp_fused_kernel<false, false>) : go(mlp_fused_kernel<false, true>);
+    auto pick = [&](auto tiled) {
+        constexpr bool T = decltype(tiled)::value;
+        if (step)
+            return l1_fp32 ? go(mlp_fused_kernel<T, false, true>) : go(mlp_fused_kernel<T, true, true>);
+        return l1_fp32 ? go(mlp_fused_kernel<T, false, false>) : go(mlp_fused_kernel<T, true, false>);
+    };
+    return tile_cols > 0 ? pick(std::true_type{}) : pick(std::false_type{});
 }
 
 }  // namespace dl

@@ -515,9 +515,11 @@ class GossipEngine:
             lib = _lib.load()
             self.ws.get(lib.dl_mix_workspace_bytes(self.n, self.W.n_src - self.n, self.P))
 
-    def round(self, G=None, lr=0.0, deviation=False, mean=None, halo=None):
-        """G must already be in the resident layout (``layout_like``)."""
-        mix_round(self.W, self.X, self.Y, G=G, lr=lr, halo=halo,
+    def round(self, G=None, lr=0.0, deviation=False, mean=None, halo=None, src=None):
+        """G must already be in the resident layout (``layout_like``).  src (optional, resident
+        layout): mix it instead of X -- e.g. the local step X - lr G a gradient kernel already
+        formed -- into the new X; X itself is then only the buffer the next round writes."""
+        mix_round(self.W, self.X if src is None else src, self.Y, G=G, lr=lr, halo=halo,
                   dev_sq=self.dev_sq if deviation else None,
                   dev_max=self.dev_max if deviation else None, mean=mean, workspace=self.ws,
                   tiled=(self.P, self.T) if self.layout == "tiled" else None)

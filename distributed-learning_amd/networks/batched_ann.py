@@ -72,12 +72,21 @@ class BatchedANN:
             p(labels), labels.stride(0) if labels is not None else 0, p(loss))
         _lib.check(lib.dl_bgemm(ctypes.byref(args), _lib.stream_handle(self.device)), "dl_bgemm")
 
-    def gradients(self, X, data, labels, G):
+    def gradients(self, X, data, labels, G, lr=None):
         """G[a] = d loss_a / d params_a for every agent.  X, G: [N, P] row-major fp32 (row stride
         may exceed P), or -- fused path only -- the engine's column-tiled [tiles, N, T] tensors
         (tiles * T >= P); data: [N, B, input_dim] fp32; labels: [N, B] int32.  Returns the
-        per-agent mean cross-entropy (device tensor [N])."""
+        per-agent mean cross-entropy (device tensor [N]).
+
+        lr (fused path only): G instead receives the local SGD step X - lr * grad, rounded as
+        the fused round's step rounds it (dl_mlp_args.out_mode 1), so a plain round of G equals
+        the fused round of X and the gradient bit for bit (row-major: G's row stride must equal
+        X's)."""
         lib = _lib.load()
+        step = lr is not None
+        if step and self.path != "fused":
+            raise ValueError("the local-step output (lr=...) needs the fused kernel")
+        mode = (1, float(lr)) if step else (0, 0.0)
         N, B, din, dh, dout, P = self.N, self.B, self.din, self.dh, self.dout, self.P
         if tuple(data.shape) != (N, B, din) or not data.is_contiguous():
             raise ValueError(f"data must be contiguous [{N}, {B}, {din}] fp32")
@@ -94,7 +103,7 @@ class BatchedANN:
                                  "columns")
             args = _lib.DlMlpArgs(N, B, din, dh, dout, _lib.ptr(X), 0, _lib.ptr(data), B * din,
                                   _lib.ptr(labels), labels.stride(0), _lib.ptr(G), 0,
-                                  _lib.ptr(self.loss), T)
+                                  _lib.ptr(self.loss), T, *mode)
             _lib.check(lib.dl_mlp_grad(ctypes.byref(args), _lib.stream_handle(self.device)),
                        "dl_mlp_grad")
             return self.loss
@@ -109,7 +118,7 @@ class BatchedANN:
         if self.path == "fused":
             args = _lib.DlMlpArgs(N, B, din, dh, dout, _lib.ptr(X), X.stride(0), _lib.ptr(data),
                                   B * din, _lib.ptr(labels), labels.stride(0), _lib.ptr(G),
-                                  G.stride(0), _lib.ptr(self.loss), 0)
+                                  G.stride(0), _lib.ptr(self.loss), 0, *mode)
             _lib.check(lib.dl_mlp_grad(ctypes.byref(args), _lib.stream_handle(self.device)),
                        "dl_mlp_grad")
             return self.loss

@@ -140,13 +140,20 @@ class MLPConsensusSGD:
     reference's consensus notebooks (Man_Colab.ipynb cells 12-23: local SGD step, then
     ``Mixer.mix``), with all agents resident in HBM.
 
-    One ``step()`` = batched per-agent gradients (``BatchedANN.gradients`` -> G rows) followed by
-    the fused round X <- W (X - lr G) and the disagreement (``GossipEngine.round``).  Every call
+    One ``step()`` = batched per-agent gradients followed by the round X <- W (X - lr G) and the
+    disagreement (``GossipEngine.round``).  emit="grad" (default): the kernel writes G and the
+    fused round forms X - lr G on the fly (reads X and G).  emit="step" (fused kernel only): the
+    gradient kernel writes the local step T = X - lr G itself and the round mixes T -- one matrix
+    read instead of two, bit-identical X' -- but the kernel must then read every parameter again
+    where its gradient is stored, and fc1.weight (72 % of them) is long out of the caches by
+    then: at c3 the round saves 22 us and the gradient kernel loses 58 (3159 vs 3503 steps/s,
+    PMC bytes per step 975 vs 985 MB; profiles/r10/c3_step).  ``G`` holds whichever was
+    written.  Every call
     is stream-ordered with no host synchronisation, so ``capture()`` can record a step as a
     hipGraph (two graphs: the engine ping-pongs X/Y) and ``replay()`` then runs steps with one
     graph launch each instead of ~15 kernel launches from Python."""
 
-    def __init__(self, ann, eng, data, labels, lr, deviation=True):
+    def __init__(self, ann, eng, data, labels, lr, deviation=True, emit="auto"):
         if eng.layout == "tiled" and ann.path != "fused":
             raise ValueError("the layered gradients read X row-major: use GossipEngine("
                              "layout='rows') or the fused kernel")
@@ -156,6 +163,11 @@ class MLPConsensusSGD:
         self.ann, self.eng = ann, eng
         self.data, self.labels = data, labels
         self.lr, self.deviation = float(lr), bool(deviation)
+        if emit == "auto":
+            emit = "grad"
+        if emit not in ("step", "grad") or (emit == "step" and ann.path != "fused"):
+            raise ValueError("emit must be 'grad', or 'step' with the fused gradient kernel")
+        self.emit = emit
         # Row-major engines may carry zero padding columns [ann.P, eng.P) (a whole number of mix
         # tiles: no ragged tail launch); the tiled layout zero-pads its last tile itself.  Padding
         # stays exactly zero -- G is zero there and W 0 = 0 -- and adds exact zeros to the
@@ -176,13 +188,25 @@ class MLPConsensusSGD:
         T = plan_shape(DeviceCsr(csr, device), n_params, deviation=True)["tile_cols"]
         return -(-n_params // T) * T if T else n_params
 
-    def step(self):
+    def gradients(self):
+        """The gradient phase alone: G (emit="grad") or T = X - lr G (emit="step")."""
         P = self.ann.P
+        lr = self.lr if self.emit == "step" else None
         if self.eng.layout == "tiled":     # the fused kernel addresses the tiles directly
-            self.ann.gradients(self.eng.X, self.data, self.labels, self.G)
+            self.ann.gradients(self.eng.X, self.data, self.labels, self.G, lr=lr)
         else:
-            self.ann.gradients(self.eng.X[:, :P], self.data, self.labels, self.G[:, :P])
-        self.eng.round(G=self.G, lr=self.lr, deviation=self.deviation)
+            self.ann.gradients(self.eng.X[:, :P], self.data, self.labels, self.G[:, :P], lr=lr)
+
+    def round(self):
+        """The round phase alone (after ``gradients``)."""
+        if self.emit == "step":
+            self.eng.round(src=self.G, deviation=self.deviation)
+        else:
+            self.eng.round(G=self.G, lr=self.lr, deviation=self.deviation)
+
+    def step(self):
+        self.gradients()
+        self.round()
 
     def capture(self):
         """Record one step per ping-pong parity.  Runs nothing: the engine state afterwards is

@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define DLAMD_ABI_VERSION 6
+#define DLAMD_ABI_VERSION 7
 
 typedef void *dl_stream_t; /* hipStream_t; NULL = the legacy default stream */
 
@@ -504,6 +504,10 @@ int dl_xent_grad(const float *Z, int64_t sZ, const int32_t *y, int64_t sY, float
  *   tile_cols T > 0: X and G are instead in the column-tiled layout of dl_mix_args
  *     ([ceil(P/T)][n_agents][T], T a power of two >= 4; ldx, ldg ignored), the resident layout
  *     the fused round streams fastest.
+ *   out_mode 1 (ABI 7): G receives the local SGD step T = X - lr G instead of the gradient, each
+ *     element rounded fl(x - fl(lr g)) as dl_mix_round's fused step computes it, so a round of T
+ *     (dl_mix_round with G = NULL) gives bit-for-bit the X' of the fused round of X and G while
+ *     streaming one matrix instead of two; row-major needs ldg == ldx.  0: the gradient.
  * X, data and G 16-byte aligned, ldx, ldg and s_data multiples of 4, G disjoint from X. */
 typedef struct dl_mlp_args {
     int32_t n_agents, batch, input_dim, hidden_dim, output_dim;
@@ -513,6 +517,8 @@ typedef struct dl_mlp_args {
     float *G; int64_t ldg;
     float *loss;
     int32_t tile_cols;   /* 0 = row-major X, G;  T > 0 = column-tiled (see above) */
+    int32_t out_mode;    /* 0 = gradient, 1 = local step X - lr G (ABI 7) */
+    float lr;            /* out_mode 1: the step size */
 } dl_mlp_args;
 int dl_mlp_grad(const dl_mlp_args *args, dl_stream_t stream);
 

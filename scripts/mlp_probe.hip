@@ -28,8 +28,16 @@ int main(int argc, char **argv) {
     const bool x6 = !(argc > 1 && argv[1][0] == 'f');
     // argv[2] == "tiled": X and G in the engine's column-tiled layout (T = 64 for 256 agents)
     const bool tiled = argc > 2 && argv[2][0] == 't';
-    auto kern = tiled ? (x6 ? dl::mlp_fused_kernel<true, true> : dl::mlp_fused_kernel<true, false>)
-                      : (x6 ? dl::mlp_fused_kernel<false, true> : dl::mlp_fused_kernel<false, false>);
+    // argv[3] == "step": G receives the local step x - lr g (dl_mlp_args.out_mode 1)
+    const bool step = argc > 3 && argv[3][0] == 's';
+    auto kern = step ? (tiled ? (x6 ? dl::mlp_fused_kernel<true, true, true>
+                                    : dl::mlp_fused_kernel<true, false, true>)
+                              : (x6 ? dl::mlp_fused_kernel<false, true, true>
+                                    : dl::mlp_fused_kernel<false, false, true>))
+                     : (tiled ? (x6 ? dl::mlp_fused_kernel<true, true, false>
+                                    : dl::mlp_fused_kernel<true, false, false>)
+                              : (x6 ? dl::mlp_fused_kernel<false, true, false>
+                                    : dl::mlp_fused_kernel<false, false, false>));
     const int N = 256, B = 64, din = 784, dh = 150, dout = 10;
     const long P = (long)dh * din + dh + 2 * (dh * dh + dh) + dout * dh + dout;
     const long ld = (P + 63) / 64 * 64;
@@ -55,7 +63,7 @@ int main(int argc, char **argv) {
     CHECK(dl::allow_full_lds(reinterpret_cast<const void *>(kern)));
     // tiled: T = 64 -> tsh 6, tile stride N * 64 floats (ld is a multiple of 64: whole tiles)
     dl::MlpArgs p{X, ld, D, (long)B * din, Y, B, G, ld, L, din, dh, dout, tiled ? 6 : 0,
-                  tiled ? (long)N * 64 : 0, st};
+                  tiled ? (long)N * 64 : 0, st, 0.05f};
     int rate_khz = 0;
     CHECK(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, 0));
     const char *names[] = {"layer1 fwd", "fwd2", "fwd3", "logits+xent", "dW4+db4+dZ3", "dW3",

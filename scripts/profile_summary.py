@@ -10,6 +10,7 @@ import csv
 import glob
 import json
 import os
+import re
 import shutil
 import sys
 
@@ -51,7 +52,23 @@ def main(src, dst, note):
             e["hbm_write_bytes"] = write[r["Name"]] * 1024
             e["hbm_bytes_per_launch"] = e["hbm_read_bytes_corrected"] + e["hbm_write_bytes"]
         kernels[r["Name"]] = e
-    json.dump({"note": note, "kernels": kernels}, open(f"{dst}/summary.json", "w"), indent=1)
+    out = {"note": note, "kernels": kernels}
+    last = int(os.environ.get("LAST", "0"))
+    if last:   # the timed steps: the last LAST launches of every kernel launched that often
+        per = collections.defaultdict(list)
+        for t in csv.DictReader(open(trace)):
+            per[t["Kernel_Name"]].append((int(t["Start_Timestamp"]),
+                                          (int(t["End_Timestamp"]) - int(t["Start_Timestamp"])) / 1e3))
+        g = {"note": f"the last {last} launches of each kernel in kernel_trace.csv (the timed steps)"}
+        for name, v in per.items():
+            if len(v) >= last:
+                d = [x[1] for x in sorted(v)[-last:]]
+                m = re.search(r"(\w+)\s*[<(]", name.replace("(anonymous namespace)", ""))
+                short = m.group(1) if m else name
+                g.setdefault(f"{short}_avg_us", sum(d) / last)
+                g.setdefault(f"{short}_kernels", []).append(name)
+        out["graph_step_launches"] = g
+    json.dump(out, open(f"{dst}/summary.json", "w"), indent=1)
     print(f"wrote {dst}/summary.json ({len(kernels)} kernels)")
 
 

@@ -40,7 +40,7 @@ def test_struct_layout_matches_c(tmp_path):
                     'offsetof(dl_mix_args, lr), offsetof(dl_mix_args, mean),'
                     'sizeof(dl_mix_plan), sizeof(dl_perron_args));'
                     'printf("%zu %zu %zu %zu %zu\\n", sizeof(dl_sgd_args), offsetof(dl_sgd_args, lr),'
-                    'sizeof(dl_mlp_args), offsetof(dl_mlp_args, tile_cols), sizeof(dl_bgemm_args));'
+                    'sizeof(dl_mlp_args), offsetof(dl_mlp_args, lr), sizeof(dl_bgemm_args));'
                     'return 0;}\n')
     exe = tmp_path / "layout"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(prog), "-o", str(exe)],
@@ -50,7 +50,7 @@ def test_struct_layout_matches_c(tmp_path):
     py = [ctypes.sizeof(_lib.DlCsr), ctypes.sizeof(_lib.DlMixArgs), _lib.DlMixArgs.W.offset,
           _lib.DlMixArgs.lr.offset, _lib.DlMixArgs.mean.offset, ctypes.sizeof(_lib.DlMixPlan),
           ctypes.sizeof(_lib.DlPerronArgs), ctypes.sizeof(_lib.DlSgdArgs),
-          _lib.DlSgdArgs.lr.offset, ctypes.sizeof(_lib.DlMlpArgs), _lib.DlMlpArgs.tile_cols.offset,
+          _lib.DlSgdArgs.lr.offset, ctypes.sizeof(_lib.DlMlpArgs), _lib.DlMlpArgs.lr.offset,
           ctypes.sizeof(_lib.DlBgemmArgs)]
     assert c == py
 
@@ -150,6 +150,14 @@ def test_new_entry_points_validate_before_any_device_call():
     m = _lib.DlMlpArgs(4, 64, 784, 150, 10)
     m.tile_cols = 6                                                         # not a power of 2
     assert lib.dl_mlp_grad(ctypes.byref(m), None) == _lib.DL_ERR_INVALID
+    P = 150 * 784 + 150 + 2 * (150 * 150 + 150) + 10 * 150 + 10
+    m = _lib.DlMlpArgs(4, 64, 784, 150, 10, 16, P + 48, 1 << 36, 64 * 784, 1 << 38, 64,
+                       1 << 40, P + 48, None, 0, 2, 0.1)                  # out_mode 2
+    assert lib.dl_mlp_grad(ctypes.byref(m), None) == _lib.DL_ERR_INVALID
+    assert b"out_mode" in lib.dl_last_error()
+    m.out_mode, m.ldg = 1, P + 112                                          # step, ldg != ldx
+    assert lib.dl_mlp_grad(ctypes.byref(m), None) == _lib.DL_ERR_INVALID
+    assert b"ldg == ldx" in lib.dl_last_error()
     x = _lib.DlMixArgs()
     x.x, x.y, x.n_params, x.ldx, x.ldy = 256, 1 << 20, 64, 64, 64
     x.W = _lib.DlCsr(16, 16, 16, 4, 12, 3, 1, 1)

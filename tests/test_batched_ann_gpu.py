@@ -50,6 +50,47 @@ def test_gradients_match_autograd(cuda, n, b, dims, path):
     assert torch.isnan(Gbuf[:, P:]).all()       # nothing written past the parameter columns
 
 
+@pytest.mark.parametrize("layout", ["rows", "tiled"])
+@pytest.mark.parametrize("n,dims", [(4, (784, 150, 10)), (5, (52, 40, 7)), (3, (16, 152, 16))])
+def test_step_output_is_the_local_sgd_step(cuda, n, dims, layout):
+    """dl_mlp_args.out_mode 1: the kernel writes T = X - lr G instead of G -- bit for bit
+    fl(x - fl(lr g)) of the same kernel's gradient launch (what dl_mix_round's fused step
+    computes), in both resident layouts, and nothing outside the parameter columns."""
+    from distributed_learning_amd import engine
+    from distributed_learning_amd.networks.batched_ann import BatchedANN
+    din, dh, dout = dims
+    gen = torch.Generator(device=cuda).manual_seed(21)
+    bann = BatchedANN(n, 64, din, dh, dout, device=cuda, path="fused")
+    P, lr = bann.P, 0.07
+    X0 = 0.1 * torch.randn(n, P, device=cuda, generator=gen)
+    data = torch.randn(n, 64, din, device=cuda, generator=gen)
+    labels = torch.randint(0, dout, (n, 64), device=cuda, generator=gen, dtype=torch.int32)
+    if layout == "rows":
+        ld = -(-P // 64) * 64
+        X = torch.zeros(n, ld, device=cuda)
+        X[:, :P] = X0
+        G, T = (torch.full((n, ld), float("nan"), device=cuda) for _ in range(2))
+        bann.gradients(X[:, :P], data, labels, G[:, :P])
+        bann.gradients(X[:, :P], data, labels, T[:, :P], lr=lr)
+        torch.cuda.synchronize()
+        g, t = G[:, :P], T[:, :P]
+        assert torch.isnan(T[:, P:]).all()
+    else:
+        X = engine.to_tiled(X0, 8)
+        G, T = (torch.full_like(X, float("nan")) for _ in range(2))
+        bann.gradients(X, data, labels, G)
+        bann.gradients(X, data, labels, T, lr=lr)
+        torch.cuda.synchronize()
+        g, t = engine.from_tiled(G, P), engine.from_tiled(T, P)
+        assert torch.isnan(T.reshape(-1, n, 8).permute(1, 0, 2).reshape(n, -1)[:, P:]).all()
+    assert torch.isfinite(g).all()
+    want = X0 - g * lr               # two fp32 roundings: fl(x - fl(lr g))
+    assert torch.equal(t, want)
+    with pytest.raises(ValueError):
+        BatchedANN(n, 64, din, dh, dout, device=cuda, path="layers").gradients(
+            X0, data, labels, torch.empty_like(X0), lr=lr)
+
+
 def test_consensus_sgd_round_with_batched_grads(cuda):
     """One c3 round: G from the batched kernels, then the fused local step + mix; equals the
     per-agent autograd step followed by the oracle mix (to fp32 GEMM rounding)."""
@@ -184,3 +225,43 @@ def test_mlp_consensus_tiled_layout_matches_rows(cuda):
     assert torch.equal(res["rows"][0], res["tiled"][0])
     assert torch.equal(res["rows"][2], res["tiled"][2])
     torch.testing.assert_close(res["rows"][1], res["tiled"][1], rtol=1e-5, atol=0)
+
+
+@pytest.mark.parametrize("layout", ["rows", "tiled"])
+def test_mlp_consensus_step_emission_matches_gradient_emission(cuda, layout):
+    """MLPConsensusSGD(emit="step") -- the kernel writes X - lr G, the round mixes it -- gives the
+    parameters, losses and deviation of emit="grad" (the kernel writes G, the fused round forms
+    X - lr G) bit for bit, eager and under hipGraph replay."""
+    from distributed_learning_amd import engine
+    from distributed_learning_amd.graph import from_edge_weights, random_regular_edges
+    from distributed_learning_amd.networks.batched_ann import BatchedANN
+    from distributed_learning_amd.workloads import MLPConsensusSGD
+    n, b = 40, 64
+    gen = torch.Generator(device=cuda).manual_seed(13)
+    bann = BatchedANN(n, b, 96, 50, 10, device=cuda)
+    P = bann.P
+    X0 = 0.1 * torch.randn(n, P, device=cuda, generator=gen)
+    data = torch.randn(n, b, 96, device=cuda, generator=gen)
+    labels = torch.randint(0, 10, (n, b), device=cuda, generator=gen, dtype=torch.int32)
+    edges = random_regular_edges(4, n, seed=6)
+    csr = from_edge_weights(edges, [0.2] * len(edges), list(range(n)))
+    cols = P if layout == "tiled" else MLPConsensusSGD.padded_params(csr, P, cuda)
+    res = {}
+    for emit in ("grad", "step", "step-graph"):
+        eng = engine.GossipEngine(csr, cols, device=cuda,
+                                  X=torch.nn.functional.pad(X0, (0, cols - P)), layout=layout)
+        sgd = MLPConsensusSGD(bann, eng, data, labels, lr=0.1, emit=emit.split("-")[0])
+        assert sgd.emit == emit.split("-")[0]
+        if emit == "step-graph":
+            sgd.capture()
+            sgd.replay(3)
+        else:
+            for _ in range(3):
+                sgd.step()
+        torch.cuda.synchronize()
+        res[emit] = (eng.rows().clone(), eng.dev_sq.clone(), sgd.loss.clone())
+    for emit in ("step", "step-graph"):
+        for a, b_ in zip(res["grad"], res[emit]):
+            assert torch.equal(a, b_), emit
+    assert MLPConsensusSGD(bann, engine.GossipEngine(csr, cols, device=cuda, layout=layout),
+                           data, labels, lr=0.1).emit == "grad"

@@ -8,6 +8,8 @@ c3: 256 agents x ANNModel(784, 150, 10), B = 64, random 4-regular graph -- three
         fp32's own (no entry beyond 8x), and its norm-wise relative error is below 1e-5;
       * round: X' == W (X - lr G) computed by the C oracle (oracle/cref.mix_round) from the same
         X and the kernel's own G -- bit for bit (the mix is exact, tests/test_mix_gpu.py).
+    A second system steps alongside with emit="step" (the kernel writes X - lr G, the round
+    mixes that) and must hold the same bits after every step.
 c5: Wide-ResNet-16-4.  3 agents of the full model against the reference-style CPU loop
     (oracle/consensus_sgd_ref: per-agent torch modules + optim.SGD + the numpy Mixer round), and
     the full 64-agent, B = 64 step with property checks: two agents' local SGD steps against
@@ -59,14 +61,20 @@ def test_c3_full_shape_three_steps(cuda):
     cols = MLPConsensusSGD.padded_params(csr, P, cuda)
     eng = engine.GossipEngine(csr, cols, device=cuda,
                               X=torch.nn.functional.pad(X0, (0, cols - P)), layout="rows")
-    sgd = MLPConsensusSGD(bann, eng, data, labels, lr=lr)
+    sgd = MLPConsensusSGD(bann, eng, data, labels, lr=lr, emit="grad")
+    eng2 = engine.GossipEngine(csr, cols, device=cuda,
+                               X=torch.nn.functional.pad(X0, (0, cols - P)), layout="rows")
+    sgd2 = MLPConsensusSGD(bann, eng2, data, labels, lr=lr, emit="step")
     m32, m64 = ANNModel(*dims).to(cuda), ANNModel(*dims).to(cuda).double()
     ratios_max, ratios_norm, rels, rels_torch = [], [], [], []
     for step in range(3):
         X = eng.X[:, :P].clone()
         sgd.step()
+        sgd2.step()
         torch.cuda.synchronize()
         G = sgd.G[:, :P]
+        assert torch.equal(sgd2.G[:, :P], X - G * lr), step     # T = fl(x - fl(lr g))
+        assert torch.equal(eng2.X, eng.X), step
         for a in range(n):
             g = []
             for m, dt in ((m32, torch.float32), (m64, torch.float64)):

@@ -352,7 +352,11 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
             // entries on the c4-ba graph) is one lane's serial chain, and read-then-fold per
             // entry exposed two dependent LDS latencies each (4.5 ms per round, LDS-bound)
             uint32_t t = d & 0xffffu;
+#ifdef MIX_TAIL_CAP   // measurement only (wrong results): at most MIX_TAIL_CAP tail entries a row
+            const uint32_t t1 = t + min(d >> 16, (uint32_t)MIX_TAIL_CAP);
+#else
             const uint32_t t1 = t + (d >> 16);
+#endif
             // (eight per step spill; one at a five-entry head: beside its 30 head registers even
             // two per step spill 84 VGPRs in the local-step + deviation instantiation)
             constexpr int TU = RD >= 5 ? 1 : 4;

@@ -382,6 +382,9 @@ struct ColSlice {   // loads unconditional, zeroing in store() (see RowSlice)
 
 __device__ __forceinline__ float act_fwd(int layer, float z) {
     if (layer == 0) return z > 0.f ? z : 0.f;   // ReLU
+#if MLP_ACT_PROBE   // measurement only (wrong results): the transcendental activations' cost
+    return z;
+#endif
     if (layer == 1) return tanhf(z);            // Tanh
     return z > 0.f ? z : expm1f(z);             // ELU(alpha = 1)
 }

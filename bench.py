@@ -57,8 +57,10 @@ def parse():
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--workload", default="c2",
-                   choices=["c1", "c2", "c2-mix", "c2-gossip", "c2-halo", "c3", "c4", "c4-gather", "c4-ba",
-                            "c5"])
+                   choices=["c1", "c2", "c2-mix", "c2-gossip", "c2-halo", "c3", "c4", "c4-rank",
+                            "c4-gather", "c4-ba", "c5"])
+    p.add_argument("--rank-of", type=int, default=8,
+                   help="c4-rank: the GPU count of the partition whose rank 0 is measured alone")
     p.add_argument("--irregular", default="ba2", choices=["ba2", "ba1", "deg"],
                    help="c4-ba: Barabasi-Albert m=2 (the headline), m=1, or a hub-free random "
                         "graph of degree 2..6 (graph.random_irregular_metropolis)")
@@ -215,17 +217,26 @@ def copy_ceiling(dev, nbytes=4 << 30, reps=10):
     return (max(best[v] for v in (0, 1, 2, 3)), max(best[v] for v in (4, 5, 6)), best)
 
 
-def kernel_name(plan, sgd, dev, n_src):
-    """The mix_tile_kernel instantiation dl_mix_round launches for this plan (FAST path)."""
+def kernel_name(plan, sgd, dev, n_src, halo=0, lag=False):
+    """The full mix_tile_kernel instantiation dl_mix_round launches for this plan (FAST path):
+    mix_tile_kernel<C, KV, SGD, DEV, MIX, HALO, FAST, RD, LAG, RAG>(dl::TileArgs), as rocprofv3
+    prints it.  Paths 4 / 5 keep RD = plan head entries in registers, path 5 its LDS tail in
+    format RAG = plan tail_fmt; halo: 0 none, 1 row-major halo rows, 2 column-tiled halo blocks
+    (the lagged-deviation instantiation of a partition round has DEV false, LAG true)."""
     c = plan["tile_cols"] // 4
     need = -(-n_src // (1024 // c))
     kv = 2 if need <= 2 else 4 if need <= 4 else 8
     b = lambda v: "true" if v else "false"  # noqa: E731
-    # prefix of the instantiation (the trailing RD / LAG parameters are the defaults)
-    return f"mix_tile_kernel<{c}, {kv}, {b(sgd)}, {b(dev)}, true, false, true, 0, false>"
+    rd = plan.get("head", 0) if plan["path"] in (4, 5) else 0
+    rag = plan.get("tail_fmt", 0) if plan["path"] == 5 else 0
+    return (f"mix_tile_kernel<{c}, {kv}, {b(sgd)}, {b(dev)}, true, {halo}, true, {rd}, {b(lag)}, "
+            f"{rag}>(dl::TileArgs)")
 
 
-def traffic_from_profile(kname, path=os.path.join(ROOT, "profiles", "r09", "summary.json")):
+PROFILE_C2 = os.path.join(ROOT, "profiles", "r11", "c2", "summary.json")
+
+
+def traffic_from_profile(kname, path=PROFILE_C2):
     """HBM bytes per launch of this kernel from the committed rocprofv3 PMC summary
     (FETCH_SIZE x 2 + WRITE_SIZE, gfx950 correction), or None if it was not profiled."""
     try:
@@ -547,17 +558,16 @@ def run_gather(args, dev, rank, world):
         else:
             csr = graph.barabasi_albert_metropolis(4096, 2 if args.irregular == "ba2" else 1, 1)
         n = csr.n_rows
-        kname = "mix_tile_kernel<1, 4, true, true, true, false, true, 3, false, 2>"
         gname = ({"ba2": "c4-ba: Barabasi-Albert m=2 (seed 1)", "ba1": "c4-ba: Barabasi-Albert "
                   "m=1 (seed 1)", "deg": "c4-ba --irregular deg: ring + random degree 2..6"}
                  [args.irregular] + ", Metropolis weights, 4096 agents, fused local step + mix "
                  "+ deviation")
         kdesc = "mix_tile_kernel register head + LDS tail (+dev_reduce), HIP-event time"
         metric = "consensus rounds/sec, 4096 agents x 2^18 fp32 params, irregular graph"
-        prof_dir = os.path.join(ROOT, "profiles", "r10", "ba")
+        # the committed profile is of the Barabasi-Albert m = 2 graph only
+        prof_dir = os.path.join(ROOT, "profiles", "r11", "c4ba") if args.irregular == "ba2" else None
     else:
         csr, n = per_edge_torus(64, 64)
-        kname = "mix_tile_kernel<1, 4, true, true, true, false, true, 5>"
         gname = ("c4-gather: 64x64 torus, per-edge weights (best constant x U[0.9, 1.1]), fused "
                  "local step + mix + deviation")
         kdesc = "mix_tile_kernel register-CSR (+dev_reduce), HIP-event time"
@@ -584,6 +594,7 @@ def run_gather(args, dev, rank, world):
                               order="auto" if args.order == "auto" else None)
     G = eng.layout_like(torch.randn(n, P, device=dev, generator=gen))
     plan = eng.plan(deviation=True)
+    kname = kernel_name(plan, True, True, n)     # the instance this plan launches
     elapsed, launch_ms = timed(lambda: eng.round(G=G, lr=lr, deviation=True))
     del eng, G
     torch.cuda.empty_cache()
@@ -601,9 +612,9 @@ def run_gather(args, dev, rank, world):
     g_mix = timed(lambda: engine.mix_round(W, X, Y, G=Gr, lr=lr, workspace=ws))
     del os.environ["DLAMD_FORCE_GATHER"]
     bytes_per_round = 12 * n * P
-    prof = os.path.join(prof_dir, "summary.json")
-    traffic, src = traffic_from_profile(kname, prof)
-    g_traffic, g_src = traffic_from_profile("mix_gather_kernel", prof)
+    prof = os.path.join(prof_dir, "summary.json") if prof_dir else None
+    traffic, src = traffic_from_profile(kname, prof) if prof else (None, None)
+    g_traffic, g_src = traffic_from_profile("mix_gather_kernel", prof) if prof else (None, None)
     achieved = bytes_per_round / (launch_ms / 1e3) / 1e9
     g_achieved = bytes_per_round / (g_mix[1] / 1e3) / 1e9
     if rank == 0:
@@ -653,8 +664,8 @@ def _halo_schemes(args, dev, rank, world, csr, parts, P, lr, gen):
                                    chunk_cols=P // 8 if name == "chunks" else None,
                                    n_agents_total=n, overlap=name)
         shard.X.normal_(generator=gen)
-        if G is None:   # synthetic gradient rows, shared by both schemes (same row count)
-            G = engine.staggered_zeros((rp.n_local, P), 2, dev).normal_(generator=gen)
+        if G is None:   # synthetic gradient rows, shared by both schemes (same shape and layout)
+            G = engine.staggered_zeros(shard._shape(rp.n_local), 2, dev).normal_(generator=gen)
         evs = event_pairs(args.steps, 2)
 
         def step(i, shard=shard, evs=evs):
@@ -667,6 +678,7 @@ def _halo_schemes(args, dev, rank, world, csr, parts, P, lr, gen):
         lm = max_over_ranks(float(np.mean([a.elapsed_time(b) for a, b in evs])), world, dev)
         extra = 8 * (rp.n_local - rp.n_deep) * P if name == "split" else 0
         schemes[name] = {"rounds_per_s": args.steps / el, "elapsed_s": el, "launch_ms": lm,
+                         "layout": shard.layout, "tile_cols": shard.T,
                          "n_local": rp.n_local, "n_halo": rp.n_halo,
                          "n_interior": rp.n_interior if name == "split" else None,
                          "n_deep": rp.n_deep if name == "split" else None,
@@ -676,7 +688,8 @@ def _halo_schemes(args, dev, rank, world, csr, parts, P, lr, gen):
         del shard
         torch.cuda.empty_cache()
     best = max(schemes, key=lambda k: schemes[k]["rounds_per_s"])
-    plan = {"path": "halo", "overlap": best, "n_local": schemes[best]["n_local"],
+    plan = {"path": "halo", "overlap": best, "layout": schemes[best]["layout"],
+            "tile_cols": schemes[best]["tile_cols"], "n_local": schemes[best]["n_local"],
             "n_halo": schemes[best]["n_halo"],
             "peers": sorted(schemes[best]["halo_rows_per_peer"])}
     return schemes[best]["elapsed_s"], schemes[best]["launch_ms"], plan, schemes
@@ -785,6 +798,134 @@ def run_c4(args, dev, rank, world):
         "xgmi": xgmi,
         "dist": getattr(args, "dist_info", None),
         "overlap_schemes": schemes or None,
+        "cpu_baseline": None,
+    }
+    print(json.dumps(rec), flush=True)
+
+
+def c4_torus():
+    import math
+    from distributed_learning_amd import graph
+    rows = cols = 64
+    n = rows * cols
+    wconst = 2.0 / (2.0 - 2.0 * math.cos(2 * math.pi / cols) + 8.0)
+    csr = graph.from_edge_weights(graph.torus_edges(rows, cols), [wconst] * (2 * n),
+                                  list(range(n)))
+    return csr, rows, cols, wconst
+
+
+def run_c4rank(args, dev, rank, world):
+    """One rank of config c4's N-GPU agent partition, alone on one GPU (``--rank-of N``, default
+    8): rank 0's 2-D torus block of the 64 x 64 torus x 2^18 params (N = 8: 32 x 16 = 512 local
+    rows + 96 halo rows from 3 peers), column-tiled X / Y / G and per-peer tiled halo blocks
+    resident in HBM, the halo buffers filled once and no interconnect in the timed region
+    (``sharding.ResidentHaloTransport``).  This is the per-rank HBM work the 8-GPU round runs;
+    xGMI is then the only thing the real run adds.  Each overlap scheme's whole round (pack the
+    boundary rows for every peer + the mix launch(es) + the lagged deviation's bookkeeping) is
+    timed, and the dominant kernel -- the halo-round mix_tile_kernel of the whole-round scheme
+    (HALO = 2, LAG) -- on its own with HIP events: its algorithmic bytes per launch are
+    4 B x P x (2 n_local read x and g + n_halo halo rows read + n_local written) + 8 P
+    (mean_prev read, this rank's column sums written).  N>1 GPUs: independent replicas."""
+    from distributed_learning_amd import engine, sharding
+    csr, rows, cols, wconst = c4_torus()
+    n, P, lr = csr.n_rows, 1 << 18, 1e-3
+    parts = sharding.torus_block_partition(rows, cols, args.rank_of)
+    gen = torch.Generator(device=dev).manual_seed(1000 + rank)
+    stream = torch.cuda.current_stream(dev)
+    schemes = {}
+    names = {"whole": ("chunks", None), "chunks": ("chunks", P // 8), "split": ("split", None)}
+    G = kern = None
+    for name, (overlap, chunk) in names.items():
+        rp = (sharding.split_halo_plans if overlap == "split" else sharding.halo_plans)(
+            csr, parts)[0]
+        shard = sharding.HaloShard(rp, P, dev, sharding.ResidentHaloTransport(),
+                                   chunk_cols=chunk, n_agents_total=n, overlap=overlap)
+        shard.X.normal_(generator=gen)
+        if G is None:   # synthetic gradient rows, shared by every scheme (same shape and layout)
+            G = engine.staggered_zeros(shard._shape(rp.n_local), 2, dev).normal_(generator=gen)
+        for c0, c1 in (shard.chunks() if overlap == "chunks" else [(0, P)]):
+            for slot in (0, 1):
+                _, halo, _ = shard._buffers(slot, c1 - c0)
+                halo.normal_(generator=gen)     # the resident halo (an exchange's payload)
+        evs = event_pairs(args.steps, 2)
+
+        def step(i, shard=shard, evs=evs):
+            if i is not None:
+                evs[i][0].record(stream)
+            shard.round(G=G, lr=lr, deviation=True)
+            if i is not None:
+                evs[i][1].record(stream)
+        el = timed_loop(step, args, 1, dev)
+        lm = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+        schemes[name] = {"overlap": overlap, "chunk_cols": shard.chunk, "rounds_per_s":
+                         args.steps / el, "elapsed_s": el, "round_ms": lm,
+                         "layout": shard.layout, "tile_cols": shard.T,
+                         "n_local": rp.n_local, "n_halo": rp.n_halo,
+                         "halo_blocks": shard.halo_blocks,
+                         "n_interior": rp.n_interior if overlap == "split" else None,
+                         "n_deep": rp.n_deep if overlap == "split" else None}
+        if name == "whole":   # the dominant kernel alone: the halo-round mix launch + its pack
+            _, halo, _ = shard._buffers(0, P)
+            colsum = torch.empty(P, device=dev)
+            dsq = torch.empty(rp.n_local, device=dev)
+            mean_prev = torch.zeros(P, device=dev)
+            kev, pev = event_pairs(args.steps, 2), event_pairs(args.steps, 2)
+            for i in range(-args.warmup, args.steps):
+                if i >= 0:
+                    pev[i][0].record(stream)
+                shard.pack(0, 0, P, G, lr)
+                if i >= 0:
+                    pev[i][1].record(stream)
+                    kev[i][0].record(stream)
+                shard.mix_chunk(0, P, halo, G, lr, (mean_prev, colsum, dsq))
+                if i >= 0:
+                    kev[i][1].record(stream)
+            torch.cuda.synchronize()
+            plan = engine.plan_shape(shard.W, P, deviation=True, tile_cols=shard.T)
+            kb = 4 * P * (3 * rp.n_local + rp.n_halo) + 8 * P
+            pb = 12 * P * sum(len(r) for r in rp.send_to.values())
+            kern = {"mix_ms": float(np.mean([a.elapsed_time(b) for a, b in kev])),
+                    "pack_ms": float(np.mean([a.elapsed_time(b) for a, b in pev])),
+                    "mix_bytes": kb, "pack_bytes": pb, "plan": plan,
+                    "kernel_instance": kernel_name(plan, True, False, rp.n_local + rp.n_halo,
+                                                   halo=2, lag=True)}
+        del shard
+        torch.cuda.empty_cache()
+    if rank != 0:
+        return
+    best = max(schemes, key=lambda k: schemes[k]["rounds_per_s"])
+    for v in schemes.values():
+        v["round_hbm_bytes"] = kern["mix_bytes"] + kern["pack_bytes"]
+        v["round_hbm_frac"] = v["round_hbm_bytes"] / (v["round_ms"] / 1e3) / 1e9 / HBM_PEAK_GBS
+    achieved = kern["mix_bytes"] / (kern["mix_ms"] / 1e3) / 1e9
+    traffic, src = traffic_from_profile(kern["kernel_instance"], os.path.join(
+        ROOT, "profiles", "r11", "c4rank", "summary.json"))
+    rec = {
+        "metric": f"c4 per-rank halo round, one rank of {args.rank_of} alone (64x64 torus, "
+                  f"4096 agents x 2^18 fp32 params)",
+        "value": schemes[best]["rounds_per_s"], "unit": "rounds/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": schemes[best]["elapsed_s"] / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (X, G, halo ~ N(0,1) resident in HBM)",
+        "config": {"workload": f"c4-rank: rank 0 of a {args.rank_of}-way 2-D torus block "
+                               "partition, halo resident (no transport), fused local step + mix "
+                               "+ lagged deviation", "agents_total": n, "params": P,
+                   "weights": f"best-constant {wconst:.6f}", "rank_of": args.rank_of,
+                   "parallelism": f"{world} independent replicas" if world > 1 else "single GPU",
+                   "best_scheme": best},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_source": src,
+                     "kernel": "halo-round mix_tile_kernel (column-tiled halo blocks, lagged "
+                               "deviation), HIP events per launch",
+                     "kernel_instance": kern["kernel_instance"],
+                     "bytes_per_launch": kern["mix_bytes"], "launch_ms": kern["mix_ms"]},
+        "pack": {"kernel": "step_rows_tiled_kernel x peers", "bytes": kern["pack_bytes"],
+                 "ms": kern["pack_ms"],
+                 "frac": kern["pack_bytes"] / (kern["pack_ms"] / 1e3) / 1e9 / HBM_PEAK_GBS},
+        "plan": kern["plan"],
+        "schemes": schemes,
         "cpu_baseline": None,
     }
     print(json.dumps(rec), flush=True)
@@ -1320,6 +1461,35 @@ def halo_probe(world, backend, steps=20, warmup=3, timeout_s=240, workload="c4",
             "wall_s": time.perf_counter() - t0}
 
 
+def label_decompositions(rec, world, h):
+    """At N > 1 the c2 line carries two decompositions; say which is which.
+    ``value`` is the column-stripe (P-split) rate: every rank mixes 2^20 columns of all 1024
+    agents with no data exchange (one N-float all-reduce per round), SURVEY 8e's "upper bound"
+    decomposition.  The agent partition of north_star (c) -- config c4's torus blocks with the
+    RCCL halo exchange over xGMI, strong scaling -- is the child probe ``h``; its per-N figures
+    are first-class fields: rounds/s, HBM and xGMI fractions, the winning overlap scheme."""
+    rec["decomposition"] = "P-split upper bound"
+    rec["config"]["parallelism"] = (f"column stripes x{world} (P-split upper bound, SURVEY 8e: no "
+                                    f"data exchange, deviation all-reduce only)")
+    ok = h.get("status") == "ok"
+    rec["agent_partition"] = {
+        "decomposition": "agent partition (north_star (c)): c4 64x64 torus 2-D blocks, RCCL "
+                         "send/recv halo over xGMI, strong scaling",
+        "status": h.get("status"),
+        "rounds_per_s": h["value"] if ok else None,
+        "hbm_frac": h["hbm"]["frac"] if ok else None,
+        "xgmi_frac": h["xgmi"]["frac"] if ok and h.get("xgmi") else None,
+        "overlap": h["plan"].get("overlap") if ok else None,
+        "layout": (h["plan"].get("layout") if ok else None),
+    }
+    # (the flat keys of earlier rounds, kept for the driver's records)
+    rec["c4_halo_rounds_per_s"] = rec["agent_partition"]["rounds_per_s"]
+    rec["c4_halo_hbm_frac"] = rec["agent_partition"]["hbm_frac"]
+    rec["c4_halo_xgmi_frac"] = rec["agent_partition"]["xgmi_frac"]
+    rec["c4_halo_overlap"] = rec["agent_partition"]["overlap"]
+    return rec
+
+
 def dist_info(args, world):
     """What the process group saw (for the driver's one multi-GPU record): backend, world size,
     RCCL version, visible devices."""
@@ -1355,10 +1525,11 @@ def main():
             dist.init_process_group(args.dist_backend)
     args.dist_info = dist_info(args, world)
 
-    if args.workload in ("c1", "c2-gossip", "c2-halo", "c3", "c4", "c4-gather", "c4-ba", "c5"):
-        {"c1": run_c1, "c2-gossip": run_gossip, "c2-halo": run_c2halo, "c3": run_c3,
-         "c4": run_c4, "c4-gather": run_gather, "c4-ba": run_gather, "c5": run_c5}[args.workload](args, dev, rank,
-                                                                              world)
+    runners = {"c1": run_c1, "c2-gossip": run_gossip, "c2-halo": run_c2halo, "c3": run_c3,
+               "c4": run_c4, "c4-rank": run_c4rank, "c4-gather": run_gather,
+               "c4-ba": run_gather, "c5": run_c5}
+    if args.workload in runners:
+        runners[args.workload](args, dev, rank, world)
         if world > 1:
             dist.destroy_process_group()
         return
@@ -1491,12 +1662,7 @@ def main():
             rec["c2_halo"] = halo_probe(world, args.dist_backend, timeout_s=180,
                                         workload="c2-halo")
             rec["c4_halo"] = h = halo_probe(world, args.dist_backend)
-            # the agent-partitioned path's figures as first-class fields of the line
-            ok = h.get("status") == "ok"
-            rec["c4_halo_rounds_per_s"] = h["value"] if ok else None
-            rec["c4_halo_hbm_frac"] = h["hbm"]["frac"] if ok else None
-            rec["c4_halo_xgmi_frac"] = h["xgmi"]["frac"] if ok and h.get("xgmi") else None
-            rec["c4_halo_overlap"] = h["plan"].get("overlap") if ok else None
+            label_decompositions(rec, world, h)
         print(json.dumps(rec), flush=True)
 
 

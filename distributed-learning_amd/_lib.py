@@ -32,7 +32,8 @@ class DlMixArgs(ctypes.Structure):
                 ("W", DlCsr), ("g", _vp), ("ldg", _i64), ("lr", _f32), ("halo", _vp),
                 ("ldh", _i64), ("n_halo", _i32), ("dev_sq", _vp), ("dev_max", _vp),
                 ("mean", _vp), ("tile_cols", _i32), ("mean_prev", _vp), ("colsum_out", _vp),
-                ("n_local_src", _i32)]
+                ("n_local_src", _i32), ("n_halo_blocks", _i32), ("halo_block_rows", _vp),
+                ("n_hub_rows", _i32)]
 
 
 class DlMixUntilArgs(ctypes.Structure):
@@ -50,7 +51,7 @@ class DlConsensusGdArgs(ctypes.Structure):
 
 class DlMixPlan(ctypes.Structure):
     _fields_ = [("path", _i32), ("tile_cols", _i32), ("grid", _i32), ("lds_bytes", _i32),
-                ("n_tiles", _i32), ("regular", _i32)]
+                ("n_tiles", _i32), ("regular", _i32), ("head", _i32), ("tail_fmt", _i32)]
 
 
 class DlPerronArgs(ctypes.Structure):
@@ -131,6 +132,7 @@ SIGNATURES = {
     "dl_column_sum": (_i32, [_vp, _i64, _i32, _i64, _vp, _vp]),
     "dl_max_column_std": (_i32, [_vp, _i64, _i32, _i64, _vp, _vp]),
     "dl_step_rows": (_i32, [_vp, _i64, _vp, _i64, _f32, _vp, _i32, _i64, _vp, _i64, _vp]),
+    "dl_step_rows_tiled": (_i32, [_vp, _i32, _vp, _i32, _f32, _vp, _i32, _i64, _i32, _vp, _vp]),
     "dl_stream_copy": (_i32, [_vp, _vp, _i64, _i32, _vp]),
     "dl_sgd_step": (_i32, [ctypes.POINTER(DlSgdArgs), _vp]),
     "dl_mlp_grad": (_i32, [ctypes.POINTER(DlMlpArgs), _vp]),
@@ -144,7 +146,7 @@ SIGNATURES = {
     "dl_lds_slot_order": (_i32, [_i32, _i32, _vp, _i32, _i64, ctypes.c_uint64, _vp, _vp]),
 }
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 _lib = None
 
 

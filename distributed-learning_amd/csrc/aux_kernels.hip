@@ -88,6 +88,58 @@ __global__ void __launch_bounds__(256) step_rows_kernel(const float *__restrict_
     }
 }
 
+// Column-tiled form: thread (i, cc) of the x dimension owns float4 chunk cc of selected row i in
+// every tile t = blockIdx.y, blockIdx.y + gridDim.y, ... (row index and offsets computed once; no
+// division in the loop), four tiles' loads in flight before their stores.  x / g tiles are
+// [x_rows][T] / [g_rows][T] blocks, out tiles [n_sel][T]: each output tile is one contiguous
+// block, the reads are T*4-byte row segments.
+__global__ void __launch_bounds__(256) step_rows_tiled_kernel(
+    const float4 *__restrict__ x, int x_rows, const float4 *__restrict__ g, int g_rows, float lr,
+    const int32_t *__restrict__ rows, int n_sel, int64_t n_tiles, int tcq,
+    float4 *__restrict__ out) {
+    const int q = blockIdx.x * 256 + threadIdx.x;
+    if (q >= n_sel * tcq) return;
+    const int i = q / tcq, cc = q - (q / tcq) * tcq;
+    const int64_t r = rows[i];
+    const int64_t xs = (int64_t)x_rows * tcq, gs = (int64_t)g_rows * tcq,
+                  os = (int64_t)n_sel * tcq;
+    const float4 *xp = x + r * tcq + cc;
+    const float4 *gp = g ? g + r * tcq + cc : nullptr;
+    float4 *op = out + q;
+    constexpr int U = 4;
+    int64_t t = blockIdx.y;
+    const int64_t gy = gridDim.y;
+    for (; t + (U - 1) * gy < n_tiles; t += U * gy) {
+        float4 v[U], w[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            v[u] = xp[(t + u * gy) * xs];
+            if (gp) w[u] = gp[(t + u * gy) * gs];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (gp) {
+                v[u].x = v[u].x - lr * w[u].x;
+                v[u].y = v[u].y - lr * w[u].y;
+                v[u].z = v[u].z - lr * w[u].z;
+                v[u].w = v[u].w - lr * w[u].w;
+            }
+            op[(t + u * gy) * os] = v[u];
+        }
+    }
+    for (; t < n_tiles; t += gy) {
+        float4 v = xp[t * xs];
+        if (gp) {
+            const float4 w = gp[t * gs];
+            v.x = v.x - lr * w.x;
+            v.y = v.y - lr * w.y;
+            v.z = v.z - lr * w.z;
+            v.w = v.w - lr * w.w;
+        }
+        op[t * os] = v;
+    }
+}
+
 // ---------------------------------------------------------------- local optimizer step
 // torch.optim.SGD.step (single-tensor form, torch/optim/sgd.py) over a block of agent rows, in
 // the rounding of torch's fused add-with-alpha (one fma per `add(.., alpha=..)`):
@@ -332,6 +384,26 @@ hipError_t launch_step_rows(const float *x, int64_t ldx, const float *g, int64_t
     if (bx > 1024) bx = 1024;
     hipLaunchKernelGGL(step_rows_kernel, dim3((unsigned)bx, n_sel), dim3(256), 0, s, x, ldx, g,
                        ldg, lr, rows, n_sel, n_params, out, ldo);
+    return hipGetLastError();
+}
+
+hipError_t launch_step_rows_tiled(const float *x, int x_rows, const float *g, int g_rows,
+                                  float lr, const int32_t *rows, int n_sel, int64_t n_tiles,
+                                  int tile_cols, float *out, hipStream_t s) {
+    const int tcq = tile_cols / 4;
+    const int64_t lanes = (int64_t)n_sel * tcq;
+    const int64_t bx = (lanes + 255) / 256;
+    if (bx > 65535) return hipErrorInvalidValue;
+    // about 2048 resident threads per CU over 256 CUs; each thread walks >= 4 tiles
+    int64_t gy = (256 * 2048) / (bx * 256);
+    const int64_t gmax = (n_tiles + 3) / 4;
+    if (gy > gmax) gy = gmax;
+    if (gy > 65535) gy = 65535;
+    if (gy < 1) gy = 1;
+    hipLaunchKernelGGL(step_rows_tiled_kernel, dim3((unsigned)bx, (unsigned)gy), dim3(256), 0, s,
+                       reinterpret_cast<const float4 *>(x), x_rows,
+                       reinterpret_cast<const float4 *>(g), g_rows, lr, rows, n_sel, n_tiles, tcq,
+                       reinterpret_cast<float4 *>(out));
     return hipGetLastError();
 }
 

@@ -148,20 +148,24 @@ bool force_reg_env() {
     return f && f[0] == '1' && !(g && g[0] == '1');
 }
 
-int choose_tiled_chunks(const dl_csr &W, int32_t R, uint32_t csr, bool want_dev) {
+// R = every source row (local + halo); halo rounds have no register-CSR kernels
+int choose_tiled_chunks(const dl_csr &W, int32_t R, uint32_t csr, bool want_dev, bool halo) {
     if (R > 65535) return 0;
-    const bool reg_any = dl::reg_csr_supported(1, R, W.uniform_row_nnz, 0) ||
-                         reg_tail_lds(W, R, 1, want_dev, nullptr) > 0;
+    const bool reg_any = !halo && (dl::reg_csr_supported(1, R, W.uniform_row_nnz, 0) ||
+                                   reg_tail_lds(W, R, 1, want_dev, nullptr) > 0);
     if (force_reg_env() && reg_any) return 1;
     if (csr > 0) {
         for (int c = dl::kMaxChunks; c >= 1; c >>= 1) {
-            if ((int64_t)R * c > (int64_t)dl::kRowsPerThread * dl::kTileThreads) continue;
+            // (the column-tiled halo kernel runs at most 4 row passes per thread)
+            if ((int64_t)R * c > (int64_t)(halo ? 4 : dl::kRowsPerThread) * dl::kTileThreads)
+                continue;
             const int64_t tile = (int64_t)R * c * 16;
             if (tile > 65536 && c > 1) continue;
             const int64_t scratch = want_dev ? (int64_t)(dl::kTileThreads / 64) * c * 16 : 0;
             if (tile + csr + scratch <= dl::kLdsBytes) return c;
         }
     }
+    if (halo) return 0;
     // the CSR does not fit beside any tile: the register-CSR kernels need LDS for the tile (and
     // path 5 for the CSR entries past each row's register head)
     const int64_t tile = (int64_t)R * 16;
@@ -216,6 +220,8 @@ bool plan_reg(const dl_mix_args *a, int c, bool want_dev, Plan *pl) {
     pl->pub.lds_bytes = (int32_t)lds;
     pl->pub.n_tiles = (int32_t)n_tiles;
     pl->pub.regular = head > 0 ? 0 : 1;
+    pl->pub.head = head > 0 ? head : 5;
+    pl->pub.tail_fmt = head > 0 ? pl->tail_fmt : 0;
     pl->chunks = c;
     pl->head = head;
     pl->csr_off = (uint32_t)(tile + scratch);   // path 5: the LDS tail
@@ -255,6 +261,7 @@ int plan_mix(const dl_mix_args *a, Plan *pl) {
             R <= 65535 && plan_reg(a, c, want_dev, pl))
             return DL_OK;
         if (csr == 0 || R > 65535 || (int64_t)R * c > (int64_t)dl::kRowsPerThread * dl::kTileThreads ||
+            (a->n_halo > 0 && (int64_t)R * c > 4 * (int64_t)dl::kTileThreads) ||
             lds > dl::kLdsBytes)
             return fail(DL_ERR_INVALID, "dl_mix_round: tile_cols %d does not fit this graph "
                                         "(%d rows); query dl_mix_plan_query on row-major args",
@@ -339,24 +346,54 @@ int check_mix_args(const dl_mix_args *a) {
     if ((int64_t)W.n_rows > (int64_t)NL + a->n_halo)
         return fail(DL_ERR_INVALID, "dl_mix_round: n_rows %d > n_local_src + n_halo %lld",
                     W.n_rows, (long long)NL + a->n_halo);
-    if (part && a->tile_cols != 0)
-        return fail(DL_ERR_INVALID, "dl_mix_round: n_local_src != n_rows needs row-major operands");
     if (W.nnz < 0) return fail(DL_ERR_INVALID, "dl_mix_round: nnz < 0");
+    if (a->n_hub_rows < 0) return fail(DL_ERR_INVALID, "dl_mix_round: n_hub_rows < 0");
     if (!a->x || !a->y || !W.row_ptr || (W.nnz > 0 && (!W.col || !W.w)))
         return fail(DL_ERR_INVALID, "dl_mix_round: null x/y/row_ptr/col/w");
-    if (a->tile_cols == 0 && (a->ldx < a->n_params || a->ldy < a->n_params))
-        return fail(DL_ERR_INVALID, "dl_mix_round: ldx/ldy smaller than n_params");
-    if (a->tile_cols == 0 && a->g && a->ldg < a->n_params)
-        return fail(DL_ERR_INVALID, "dl_mix_round: ldg < n_params");
-    if (a->n_halo > 0 && (!a->halo || a->ldh < a->n_params))
-        return fail(DL_ERR_INVALID, "dl_mix_round: n_halo > 0 needs halo with ldh >= n_params");
     if (a->tile_cols < 0 || (a->tile_cols > 0 && (a->tile_cols % 4 || a->tile_cols < 4 ||
                                                    a->tile_cols > 4 * dl::kMaxChunks ||
                                                    (a->tile_cols & (a->tile_cols - 1)))))
         return fail(DL_ERR_INVALID, "dl_mix_round: tile_cols must be 0 or a power of two in [4, %d]",
                     4 * dl::kMaxChunks);
-    if (a->tile_cols > 0 && a->n_halo > 0)
-        return fail(DL_ERR_INVALID, "dl_mix_round: the column-tiled layout takes no halo rows");
+    const bool tiled = a->tile_cols > 0;
+    if (!tiled && (a->ldx < a->n_params || a->ldy < a->n_params))
+        return fail(DL_ERR_INVALID, "dl_mix_round: ldx/ldy smaller than n_params");
+    if (!tiled && a->g && a->ldg < a->n_params)
+        return fail(DL_ERR_INVALID, "dl_mix_round: ldg < n_params");
+    // column-tiled: ld* = rows of each operand's tiled blocks (0 = the operand's own rows)
+    if (tiled && (a->ldx < 0 || a->ldy < 0 || a->ldg < 0 || (a->ldx > 0 && a->ldx < NL) ||
+                  (a->ldy > 0 && a->ldy < W.n_rows) || (a->g && a->ldg > 0 && a->ldg < NL) ||
+                  a->ldx > 65535 * 4 || a->ldy > 65535 * 4 || a->ldg > 65535 * 4))
+        return fail(DL_ERR_INVALID, "dl_mix_round: tiled ldx/ldg (>= n_local_src) or ldy (>= "
+                                    "n_rows) out of range");
+    if (a->n_halo > 0 && !a->halo)
+        return fail(DL_ERR_INVALID, "dl_mix_round: n_halo > 0 needs a halo buffer");
+    if (!tiled && a->n_halo > 0 && a->ldh < a->n_params)
+        return fail(DL_ERR_INVALID, "dl_mix_round: n_halo > 0 needs halo with ldh >= n_params");
+    if (!tiled && a->n_halo_blocks != 0)
+        return fail(DL_ERR_INVALID, "dl_mix_round: n_halo_blocks is for the column-tiled layout");
+    if (tiled && a->n_halo > 0) {
+        if (a->n_halo_blocks < 0 || a->n_halo_blocks > dl::kMaxHaloBlocks ||
+            (a->n_halo_blocks > 0 && !a->halo_block_rows))
+            return fail(DL_ERR_INVALID, "dl_mix_round: n_halo_blocks must be 0..%d with "
+                                        "halo_block_rows", dl::kMaxHaloBlocks);
+        int64_t sum = 0;
+        for (int b = 0; b < a->n_halo_blocks; ++b) {
+            if (a->halo_block_rows[b] <= 0)
+                return fail(DL_ERR_INVALID, "dl_mix_round: halo_block_rows[%d] <= 0", b);
+            sum += a->halo_block_rows[b];
+        }
+        if (a->n_halo_blocks > 0 && sum != a->n_halo)
+            return fail(DL_ERR_INVALID, "dl_mix_round: halo_block_rows sum to %lld, n_halo %d",
+                        (long long)sum, a->n_halo);
+        const int64_t ntl = (a->n_params + a->tile_cols - 1) / a->tile_cols;
+        if (ntl * a->n_halo * a->tile_cols * 4 >= ((int64_t)1 << 32))
+            return fail(DL_ERR_INVALID, "dl_mix_round: the tiled halo must span < 4 GiB");
+    }
+    // a column-tiled partition round reads mean_prev / colsum_out a float4 per chunk, tiles whole
+    if (tiled && (a->n_halo > 0 || part) && a->n_params % a->tile_cols)
+        return fail(DL_ERR_INVALID, "dl_mix_round: a column-tiled partition round needs "
+                                    "n_params %% tile_cols == 0");
     if (W.uniform_row_nnz < 0 ||
         (W.uniform_row_nnz > 0 && (int64_t)W.uniform_row_nnz * W.n_rows != W.nnz))
         return fail(DL_ERR_INVALID, "dl_mix_round: uniform_row_nnz * n_rows != nnz");
@@ -377,15 +414,28 @@ int check_mix_args(const dl_mix_args *a) {
         return fail(DL_ERR_INVALID,
                     "dl_mix_round: a halo round's deviation is the lagged one: mean_prev, "
                     "colsum_out and dev_sq together (or dl_column_sum + dl_deviation after it)");
-    const size_t tiled_b = a->tile_cols > 0 ? (size_t)((a->n_params + a->tile_cols - 1) /
-                                                       a->tile_cols) * a->tile_cols * W.n_rows * 4
-                                            : 0;
-    const size_t xb = a->tile_cols ? tiled_b : ((size_t)(NL - 1) * a->ldx + a->n_params) * 4;
-    const size_t yb = a->tile_cols ? tiled_b : ((size_t)(W.n_rows - 1) * a->ldy + a->n_params) * 4;
+    // extents: a tiled operand of `rows` used rows inside blocks of `ld` rows spans (tiles - 1)
+    // block strides plus its used rows of the last tile
+    const int64_t Tc = a->tile_cols;
+    const int64_t ntl = tiled ? (a->n_params + Tc - 1) / Tc : 0;
+    auto tiled_b = [&](int64_t ld, int64_t rows) {
+        return (size_t)(((ntl - 1) * ld + rows) * Tc * 4);
+    };
+    const size_t xb = tiled ? tiled_b(a->ldx ? a->ldx : NL, NL)
+                            : ((size_t)(NL - 1) * a->ldx + a->n_params) * 4;
+    const size_t yb = tiled ? tiled_b(a->ldy ? a->ldy : W.n_rows, W.n_rows)
+                            : ((size_t)(W.n_rows - 1) * a->ldy + a->n_params) * 4;
     if (overlaps(a->x, xb, a->y, yb)) return fail(DL_ERR_INVALID, "dl_mix_round: y overlaps x");
     if (a->g) {
-        const size_t gb = a->tile_cols ? tiled_b : ((size_t)(NL - 1) * a->ldg + a->n_params) * 4;
+        const size_t gb = tiled ? tiled_b(a->ldg ? a->ldg : NL, NL)
+                                : ((size_t)(NL - 1) * a->ldg + a->n_params) * 4;
         if (overlaps(a->g, gb, a->y, yb)) return fail(DL_ERR_INVALID, "dl_mix_round: y overlaps g");
+    }
+    if (a->n_halo > 0) {
+        const size_t hb = tiled ? (size_t)(ntl * a->n_halo * Tc * 4)
+                                : ((size_t)(a->n_halo - 1) * a->ldh + a->n_params) * 4;
+        if (overlaps(a->halo, hb, a->y, yb))
+            return fail(DL_ERR_INVALID, "dl_mix_round: y overlaps halo");
     }
     return DL_OK;
 }
@@ -438,11 +488,27 @@ dl::TileArgs tile_args(const dl_mix_args *a) {
     const int64_t R = t.n_loc > t.n_rows ? t.n_loc : t.n_rows;
     if (a->tile_cols > 0) {
         vec = aligned16(a->x) && aligned16(a->y) && (!a->g || aligned16(a->g)) &&
-              (!a->mean || aligned16(a->mean));
+              (!a->mean || aligned16(a->mean)) && (!a->halo || aligned16(a->halo)) &&
+              (!a->mean_prev || aligned16(a->mean_prev)) &&
+              (!a->colsum_out || aligned16(a->colsum_out));
         t.tiled = 1;
+        // per-peer halo blocks (check_mix_args: <= kMaxHaloBlocks, rows summing to n_halo,
+        // the whole halo < 4 GiB)
+        const int64_t Tc = a->tile_cols;
+        const int64_t ntl = (a->n_params + Tc - 1) / Tc;
+        const int nb = a->n_halo > 0 ? (a->n_halo_blocks > 0 ? a->n_halo_blocks : 1) : 0;
+        t.n_hblk = nb;
+        int32_t r0 = 0;
+        for (int b = 0; b < nb; ++b) {
+            t.hblk_row0[b] = r0;
+            t.hblk_off[b] = (uint32_t)(ntl * r0 * Tc * 4);
+            r0 += a->n_halo_blocks > 0 ? a->halo_block_rows[b] : a->n_halo;
+        }
+        t.hblk_row0[nb] = r0;
     } else if (((R - 1) * a->ldx + 128) * 4 >= lim || ((R - 1) * a->ldy + 128) * 4 >= lim ||
                (a->g && ((R - 1) * a->ldg + 128) * 4 >= lim) ||
-        (a->n_halo > 0 && ((int64_t)(a->n_halo - 1) * a->ldh + 128) * 4 >= lim)) {
+               // a halo row's offset (row and column) is one 32-bit value
+               (a->n_halo > 0 && (int64_t)a->n_halo * a->ldh * 4 >= lim)) {
         vec = false;
     }
     t.vec = vec ? 1 : 0;
@@ -659,7 +725,8 @@ int dl_mix_rounds_trace(const dl_mix_args *args, int32_t rounds, float *trace, v
     if (t.tiled) {
         const int64_t T = args->tile_cols;
         t.lchunks = (int32_t)(T / 4);
-        t.xts = t.yts = (int64_t)N * T * 4;
+        t.xts = (args->ldx ? args->ldx : (int64_t)N) * T * 4;
+        t.yts = (args->ldy ? args->ldy : (int64_t)N) * T * 4;
         t.xrs = t.yrs = (uint32_t)(T * 4);
     } else {
         t.lchunks = 1;
@@ -710,7 +777,9 @@ int dl_mix_rounds(const dl_mix_args *args, int32_t rounds, void *workspace, size
                                         "rows");
     const int64_t T = pl.pub.tile_cols;
     if (t.tiled) {
-        t.xts = t.gts = t.yts = (int64_t)Nr * T * 4;
+        t.xts = (args->ldx ? args->ldx : (int64_t)Nr) * T * 4;
+        t.gts = (args->ldg ? args->ldg : (int64_t)Nr) * T * 4;
+        t.yts = (args->ldy ? args->ldy : (int64_t)Nr) * T * 4;
         t.xrs = t.grs = t.yrs = (uint32_t)(T * 4);
     } else {
         t.xts = t.gts = t.yts = T * 4;
@@ -894,14 +963,19 @@ int plan_from_csr(const dl_csr &W, int32_t n_halo, int64_t n_params, int32_t dev
     a.n_params = n_params;
     float dummy;
     if (deviation) a.dev_max = &dummy;
-    if (tile_cols == -1) {  // pick the column-tiled width (no halo rows in that layout)
+    if (tile_cols == -1) {  // pick the column-tiled width (a tile of every source row in LDS)
         const int reg = W.uniform_row_nnz > 0 ? 1 : 0;
         const int32_t n_w = (reg && a.W.shared_row_weights) ? W.uniform_row_nnz : W.nnz;
-        const int c = n_halo == 0 ? choose_tiled_chunks(a.W, W.n_rows,
-                                                        dl::csr_lds_bytes(W.n_rows, W.nnz, reg, n_w),
-                                                        deviation != 0)
-                                  : 0;
+        const int64_t R = (int64_t)W.n_rows + n_halo;
+        const int c = R > 65535 ? 0
+                                : choose_tiled_chunks(a.W, (int32_t)R,
+                                                      dl::csr_lds_bytes(W.n_rows, W.nnz, reg, n_w),
+                                                      deviation != 0, n_halo > 0);
         tile_cols = 4 * c;   // 0: not tileable, report the row-major plan
+        // a tiled halo round needs whole tiles (check_mix_args)
+        if (n_halo > 0 && tile_cols > 0)
+            while (tile_cols > 4 && n_params % tile_cols) tile_cols >>= 1;
+        if (n_halo > 0 && tile_cols > 0 && n_params % tile_cols) tile_cols = 0;
     }
     a.tile_cols = tile_cols;
     Plan pl;
@@ -966,7 +1040,10 @@ int dl_mix_round(const dl_mix_args *args, void *workspace, size_t ws_bytes, dl_s
         if (t.tiled) {
             if (!t.vec)
                 return fail(DL_ERR_INVALID, "dl_mix_round: tiled operands must be 16-byte aligned");
-            t.xts = t.gts = t.yts = (int64_t)Nr * T * 4;
+            // tile stride = the operand's block rows (ld*, 0 = its own rows) x T floats
+            t.xts = (args->ldx ? args->ldx : t.n_loc) * T * 4;
+            t.gts = (args->ldg ? args->ldg : t.n_loc) * T * 4;
+            t.yts = (args->ldy ? args->ldy : (int64_t)Nr) * T * 4;
             t.xrs = t.grs = t.yrs = (uint32_t)(T * 4);
         } else {
             t.xts = t.gts = t.yts = T * 4;
@@ -990,6 +1067,23 @@ int dl_mix_round(const dl_mix_args *args, void *workspace, size_t ws_bytes, dl_s
         if (const char *v = getenv("DLAMD_LDS_MIN")) {  // measurement knob: LDS per workgroup
             const int m = atoi(v);                        // bounds workgroups per CU
             if (m > lds) lds = m < (int)dl::kLdsBytes ? m : (int)dl::kLdsBytes;
+        }
+        if (pl.pub.path == 5 && pl.head < 5 && args->n_hub_rows > 0) {
+            // hub rows' register heads behind the LDS tail: as many as fit, <= 256
+            const int hb = pl.head * 8;
+            const int room = ((int)dl::kLdsBytes - lds) / hb;
+            int nh = args->n_hub_rows < 256 ? args->n_hub_rows : 256;
+            if (nh > Nr) nh = Nr;
+            if (nh > room) nh = room;
+            if (nh > 0) {
+                t.n_hub = nh;
+                t.hub_off = (uint32_t)((lds + 15) & ~15);
+                lds = (int)t.hub_off + nh * hb;
+                if (lds > (int)dl::kLdsBytes) {   // (alignment) fall back to no hub lanes
+                    t.n_hub = 0;
+                    lds = pl.pub.lds_bytes;
+                }
+            }
         }
         if (grid_full > 0) {
             t.n_tiles = (int32_t)n_full;
@@ -1207,6 +1301,27 @@ int dl_step_rows(const float *x, int64_t ldx, const float *g, int64_t ldg, float
     hipError_t e = dl::launch_step_rows(x, ldx, g, ldg, lr, rows, n_sel, n_params, out, ldo,
                                         static_cast<hipStream_t>(stream));
     return e == hipSuccess ? DL_OK : hip_fail(e, "step_rows launch");
+}
+
+int dl_step_rows_tiled(const float *x, int32_t x_rows, const float *g, int32_t g_rows, float lr,
+                       const int32_t *rows, int32_t n_sel, int64_t n_params, int32_t tile_cols,
+                       float *out, dl_stream_t stream) {
+    g_err.clear();
+    if (n_sel == 0) return DL_OK;
+    if (!x || !rows || !out || n_sel < 0 || n_sel > 65535 || n_params <= 0 || x_rows <= 0 ||
+        (g && g_rows <= 0) || tile_cols < 4 || tile_cols > 4 * dl::kMaxChunks ||
+        (tile_cols & (tile_cols - 1)))
+        return fail(DL_ERR_INVALID, "dl_step_rows_tiled: bad arguments");
+    if (!aligned16(x) || !aligned16(out) || (g && !aligned16(g)))
+        return fail(DL_ERR_INVALID, "dl_step_rows_tiled: operands must be 16-byte aligned");
+    const int64_t n_tiles = (n_params + tile_cols - 1) / tile_cols;
+    const size_t ob = (size_t)n_tiles * n_sel * tile_cols * 4;
+    if (overlaps(out, ob, x, (size_t)n_tiles * x_rows * tile_cols * 4) ||
+        (g && overlaps(out, ob, g, (size_t)n_tiles * g_rows * tile_cols * 4)))
+        return fail(DL_ERR_INVALID, "dl_step_rows_tiled: out overlaps x or g");
+    hipError_t e = dl::launch_step_rows_tiled(x, x_rows, g, g_rows, lr, rows, n_sel, n_tiles,
+                                              tile_cols, out, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? DL_OK : hip_fail(e, "step_rows_tiled launch");
 }
 
 int dl_sgd_step(const dl_sgd_args *a, dl_stream_t stream) {

@@ -56,7 +56,18 @@ struct TileArgs {
                                  // so that launch needs no memset of its own)
     const float *mean_prev;      // halo rounds: global column mean of x (lagged deviation)
     float *colsum_out;           // halo rounds: this rank's column sums of y
+    // column-tiled halo (tiled != 0, n_src > n_loc): n_hblk per-peer blocks back to back; block
+    // b holds halo rows [hblk_row0[b], hblk_row0[b + 1]) as [n_tiles][rows_b][T], starting
+    // hblk_off[b] bytes into `halo`
+    int32_t n_hblk;
+    int32_t hblk_row0[17];
+    uint32_t hblk_off[16];
+    // path 5: rows [0, n_hub) folded by four column lanes each; their register heads as
+    // {weight, row} pairs at LDS byte offset hub_off
+    int32_t n_hub;
+    uint32_t hub_off;
 };
+constexpr int kMaxHaloBlocks = 16;
 
 // LDS bytes the staged CSR needs (0 if it cannot be staged: > 65535 rows/entries).
 // Raise kernel k's dynamic-LDS limit to the whole CU (kLdsBytes), once per (kernel, device):
@@ -138,6 +149,9 @@ hipError_t launch_max_column_std(const float *x, int64_t ldx, int n_rows, int64_
 hipError_t launch_step_rows(const float *x, int64_t ldx, const float *g, int64_t ldg, float lr,
                             const int32_t *rows, int n_sel, int64_t n_params, float *out,
                             int64_t ldo, hipStream_t s);
+hipError_t launch_step_rows_tiled(const float *x, int x_rows, const float *g, int g_rows,
+                                  float lr, const int32_t *rows, int n_sel, int64_t n_tiles,
+                                  int tile_cols, float *out, hipStream_t s);
 hipError_t launch_sgd_step(const float *x, int64_t ldx, const float *g, int64_t ldg, float *buf,
                            int64_t ldb, float *out, int64_t ldo, int n_rows, int64_t n_params,
                            float lr, float mu, float damp, float wd, int first, int nesterov,

@@ -110,7 +110,8 @@ __device__ __forceinline__ float4 *at(float *base, uint32_t off) {
 // SGD  : fused local step x - lr*g on local rows before mixing
 // DEV  : fused column mean + per-agent ||y_a - mean||^2 (needs all agents in the tile)
 // MIX  : false = deviation of x only (no LDS staging, no output rows)
-// HALO : source rows [n_loc, n_src) come from the halo buffer; output rows [0, n_rows) follow the
+// HALO : 1, 2: source rows [n_loc, n_src) come from the halo buffer (1: row-major rows of ldh; 2:
+//        column-tiled per-peer blocks, dl_mix_args.n_halo_blocks); output rows [0, n_rows) follow the
 //        CSR and need not be source rows (n_loc != n_rows: an interior or boundary row set of
 //        an agent partition, sharding.py)
 // FAST : every tile is full and every operand 16-byte aligned (float4 path with 32-bit
@@ -133,7 +134,7 @@ __device__ __forceinline__ float4 *at(float *base, uint32_t off) {
 //        (one ds_read_b64 per entry, +4 % on c4-ba); RAG = 1: fp32 weights then u16 rows (6 B,
 //        for tails that do not fit LDS at 8 B).  The fold runs the
 //        register head, then the tail, in CSR order: still the reference's left fold.
-template <int C, int KV, bool SGD, bool DEV, bool MIX, bool HALO, bool FAST, int RD = 0,
+template <int C, int KV, bool SGD, bool DEV, bool MIX, int HALO, bool FAST, int RD = 0,
           bool LAG = false, int RAG = 0>
 __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
     constexpr bool PACK = RAG == 2;
@@ -167,6 +168,25 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
     float *ltw = reinterpret_cast<float *>(smem + a.csr_off);
     uint16_t *ltc = reinterpret_cast<uint16_t *>(smem + a.csr_off + 4u * (uint32_t)ntail);
     uint2 *ltp = reinterpret_cast<uint2 *>(smem + a.csr_off);   // RAG == 2
+    // RAG, hub rows: rows [0, NH) (the longest ones, in a row-length order) are each folded by
+    // four lanes, one column each, instead of by their owner alone: a Barabasi-Albert hub's tail
+    // (169 entries at c4-ba) is one lane's serial chain, and column lanes fold it with scalar
+    // ops, twice the entries per LDS round trip.  Each column keeps its CSR-order left fold, so
+    // the bits are the owner's.  The lanes are the LAST 4 NH threads (their own rows are the
+    // shortest); the owners skip those rows.  NH is wave-uniform (host: <= 256).
+    // (not at a five-entry head: beside its 30 head registers the hub loop spills)
+    const int NH = (RAG && RD < 5) ? a.n_hub : 0;
+    const int hl = tid - (NT - 4 * NH);           // >= 0: hub lane
+    const bool hub_lane = RAG && RD < 5 && hl >= 0;
+    const int hr = hub_lane ? hl >> 2 : 0, hc = hl & 3;
+    uint2 *hubp = reinterpret_cast<uint2 *>(smem + a.hub_off);
+    uint32_t hdesc = 0u;   // hub lane: its row's tail [start, start + len) in the LDS tail
+    if (hub_lane) {
+        const int e0 = a.rowptr[hr], e1 = a.rowptr[hr + 1];
+        const int st = min(max(e0 - RD * hr, 0), ntail);
+        hdesc = (uint32_t)st | ((uint32_t)min(max(e1 - e0 - RD, 0), ntail - st) << 16);
+    }
+    float hacc = 0.f;      // hub lane: its column's squared deviations over the tiles
     if (RD > 0) {
 #pragma unroll
         for (int i = 0; i < (NRC + 1) / 2; ++i) ri[i] = 0u;
@@ -178,14 +198,19 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
 #pragma unroll
             for (int e = 0; e < RD; ++e) {
                 const int j = k * RD + e;
-                const int idx = e0 + e;
+                // (RAG: a wrong min_row_nnz promise -- a row shorter than the head -- gives
+                // wrong results but never reads past the CSR: indices are clamped into it)
+                const int idx = RAG ? min(max(e0 + e, 0), nnz - 1) : e0 + e;
                 rw[j] = a.w[idx];
                 ri[j >> 1] |= ((uint32_t)a.col[idx] * C + c) << (16 * (j & 1));
             }
             if (RAG) {
+                // this row's tail [st, st + ln) in the LDS tail, clamped into [0, ntail) for the
+                // same reason
                 const int e1 = a.rowptr[rr + 1];
-                rdesc[k] = r < Nr ? (uint32_t)(e0 - RD * rr) | ((uint32_t)(e1 - e0 - RD) << 16)
-                                  : 0u;
+                const int st = min(max(e0 - RD * rr, 0), ntail);
+                const int ln = min(max(e1 - e0 - RD, 0), ntail - st);
+                rdesc[k] = r < Nr ? (uint32_t)st | ((uint32_t)ln << 16) : 0u;
             }
         }
         if (RAG) {
@@ -201,7 +226,8 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
             __syncthreads();
             for (int t = tid; t < ntail; t += NT) {
                 const int r = trow[t];
-                const int e = t + RD * (r + 1);
+                // (clamped: with a wrong min_row_nnz promise a slot may hold no row of its own)
+                const int e = min(t + RD * (r + 1), nnz - 1);
                 const float we = a.w[e];
                 const int ce = a.col[e];
                 if (PACK) {
@@ -210,6 +236,13 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
                     ltw[t] = we;
                     ltc[t] = (uint16_t)(ce * C + c);
                 }
+            }
+            // hub rows: their register heads as {weight, row} pairs behind the tail, for the
+            // four column lanes that fold each one (below)
+            for (int i = tid; i < NH * RD; i += NT) {
+                const int h = i / RD, e = i - (i / RD) * RD;
+                const int idx = min(max(a.rowptr[h] + e, 0), nnz - 1);
+                hubp[i] = make_uint2(__float_as_uint(a.w[idx]), (uint32_t)a.col[idx]);
             }
             __syncthreads();
         }
@@ -236,6 +269,42 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
     };
     float4 *scratch = reinterpret_cast<float4 *>(smem + a.scratch_off);
 
+    // HALO == 2 (column-tiled halo, FAST): per pass, the byte offset of this lane's halo row in
+    // tile 0 and its per-tile stride -- one [n_tiles][rows_b][T] block per peer, so a row's tile
+    // stride is its block's rows_b*T*4, picked by an unrolled select over the block table (no
+    // dynamic indexing of the kernel arguments).  Local passes keep 16c / 0 (not read).  Two
+    // registers per pass: the host keeps this instantiation at KV <= 4 (no spills).
+    constexpr bool HT = HALO == 2;
+    uint32_t hoff[HT ? KV : 1], hstr[HT ? KV : 1];
+    if (HT) {
+#pragma unroll
+        for (int k = 0; k < KV; ++k) {
+            const int h = s + k * SLOTS - NL;
+            uint32_t o = 16u * c, st = 0u;
+            if (h >= 0 && h < R - NL) {
+                {
+                    int r0 = 0, r1 = R - NL;
+                    uint32_t bo = 0u;
+#pragma unroll
+                    for (int b = 1; b < kMaxHaloBlocks; ++b) {
+                        if (b < a.n_hblk && h >= a.hblk_row0[b]) {
+                            r0 = a.hblk_row0[b];
+                            bo = a.hblk_off[b];
+                        }
+                    }
+#pragma unroll
+                    for (int b = 1; b <= kMaxHaloBlocks; ++b)
+                        if (b <= a.n_hblk && a.hblk_row0[b] > h && a.hblk_row0[b - 1] <= h)
+                            r1 = a.hblk_row0[b];
+                    o += bo + (uint32_t)(h - r0) * (uint32_t)(T * 4);
+                    st = (uint32_t)(r1 - r0) * (uint32_t)(T * 4);
+                }
+            }
+            hoff[k] = o;
+            hstr[k] = st;
+        }
+    }
+
     float4 px[KV], pg[KV];
     float4 pm = zero4();             // LAG: this lane's chunk of mean_prev, prefetched with px
     float lacc[LAG ? KV : 1];        // LAG: per-pass partial ||x - mean_prev||^2 of the chunk
@@ -250,21 +319,25 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
 
     auto prefetch = [&](int tile_id) {
         const int64_t col0 = a.col_base + (int64_t)tile_id * T;
+        // (FAST tiles are whole: row-major tails take the guarded launch, and a column-tiled
+        // partition round needs n_params % T == 0, checked by the host)
         if (LAG)
             pm = FAST ? *reinterpret_cast<const float4 *>(a.mean_prev + col0 + 4 * c)
                       : ld4(a.mean_prev, col0 + 4 * c, P, false);
         if (FAST && HALO) {
             // local rows from x/g (32-bit offsets), halo rows from the halo buffer (row-major,
-            // ldh); the per-lane base select keeps every pass straight-line code
+            // ldh; or per-peer tiled blocks, hoff/hstr); the per-lane base select keeps every
+            // pass straight-line code
             const char *xt = tile_base(a.x, a.xts, tile_id);
             const char *gt = SGD ? tile_base(a.g, a.gts, tile_id) : nullptr;
-            const char *ht = reinterpret_cast<const char *>(a.halo) + col0 * 4;
+            const char *ht = reinterpret_cast<const char *>(a.halo) + (HT ? 0 : col0 * 4);
 #pragma unroll
             for (int k = 0; k < KV; ++k) {
                 const int r = s + k * SLOTS;
                 const bool loc = r < NL;
                 const bool ok = r < R;
-                const uint32_t oh = (uint32_t)(r - NL) * a.hrs + 16u * c;
+                const uint32_t oh = HT ? hoff[k] + (uint32_t)tile_id * hstr[k]
+                                       : (uint32_t)(r - NL) * a.hrs + 16u * c;
                 const char *bx = loc || !ok ? xt : ht;
                 const uint32_t o1 = loc ? ox + k * sx : ok ? oh : 16u * c;
                 const float4 *p1 = reinterpret_cast<const float4 *>(bx + o1);
@@ -352,11 +425,7 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
             // entries on the c4-ba graph) is one lane's serial chain, and read-then-fold per
             // entry exposed two dependent LDS latencies each (4.5 ms per round, LDS-bound)
             uint32_t t = d & 0xffffu;
-#ifdef MIX_TAIL_CAP   // measurement only (wrong results): at most MIX_TAIL_CAP tail entries a row
-            const uint32_t t1 = t + min(d >> 16, (uint32_t)MIX_TAIL_CAP);
-#else
             const uint32_t t1 = t + (d >> 16);
-#endif
             // (eight per step spill; one at a five-entry head: beside its 30 head registers even
             // two per step spill 84 VGPRs in the local-step + deviation instantiation)
             constexpr int TU = RD >= 5 ? 1 : 4;
@@ -419,6 +488,52 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
             acc = make_float4(lo.x, lo.y, hi.x, hi.y);
         }
         return acc;
+    };
+
+    // hub lane: column hc of row hr, the row's left fold in CSR order (register head's entries
+    // from the hub area, then the tail) on scalars -- the same IEEE operations per column as
+    // mix_row_reg's float4 / pair fold, so the same bits; eight entries' reads issued per step
+    auto hub_fold = [&]() {
+        const float *tf = reinterpret_cast<const float *>(tile);
+        float acc = 0.f;
+#pragma unroll
+        for (int e = 0; e < (RD > 0 ? RD : 1); ++e) {
+            const uint2 pr = hubp[hr * RD + e];
+            acc = acc + __uint_as_float(pr.x) * tf[pr.y * 4u + hc];
+        }
+        uint32_t t = hdesc & 0xffffu;
+        const uint32_t t1 = t + (hdesc >> 16);
+        auto entry = [&](uint32_t i, float &w, uint32_t &ci) {
+            if (PACK) {
+                const uint2 pr = ltp[i];
+                w = __uint_as_float(pr.x);
+                ci = pr.y;
+            } else {
+                w = ltw[i];
+                ci = ltc[i];
+            }
+        };
+        constexpr int HU = 8;
+        for (; t + HU <= t1; t += HU) {
+            float w8[HU], v8[HU];
+            uint32_t c8[HU];
+#pragma unroll
+            for (int u = 0; u < HU; ++u) entry(t + u, w8[u], c8[u]);
+#pragma unroll
+            for (int u = 0; u < HU; ++u) v8[u] = tf[c8[u] * 4u + hc];
+#pragma unroll
+            for (int u = 0; u < HU; ++u) acc = acc + w8[u] * v8[u];
+        }
+        for (; t < t1; ++t) {
+            float w;
+            uint32_t ci;
+            entry(t, w, ci);
+            acc = acc + w * tf[ci * 4u + hc];
+        }
+        return acc;
+    };
+    auto pick = [](const float4 &v, int i) {
+        return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w;
     };
 
     // column mean of the tile over all agents from per-thread partial sums: thread -> wave
@@ -509,12 +624,29 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
             float *yt = const_cast<float *>(
                 reinterpret_cast<const float *>(tile_base(a.y, a.yts, tile_id)));
             float4 cs = zero4();
+            float hy = 0.f;   // hub lane: column hc of row hr (plain store: few rows)
+            if (RAG && hub_lane) {
+                hy = hub_fold();
+                *reinterpret_cast<float *>(reinterpret_cast<char *>(yt) + (uint32_t)hr * a.yrs +
+                                           4u * (uint32_t)hc) = hy;
+                if (DEV) {
+                    if (mfi) {
+                        const float d = hy - pick(mean_t, hc);
+                        hacc += d * d;
+                    } else {
+                        cs.x += hc == 0 ? hy : 0.f;
+                        cs.y += hc == 1 ? hy : 0.f;
+                        cs.z += hc == 2 ? hy : 0.f;
+                        cs.w += hc == 3 ? hy : 0.f;
+                    }
+                }
+            }
             // passes stay rolled: interleaving them would hold KV accumulators at once on top
             // of the 2*KV prefetch registers
 #pragma unroll 1
             for (int k = 0; k < KV; ++k) {
                 const int ag = s + k * SLOTS;
-                if (ag < Nr) {
+                if (ag < Nr && !(RAG && ag < NH)) {   // (hub rows: folded by their lanes above)
                     const float4 acc = RD > 0 ? mix_row_reg(k) : mix_row(ag);
                     if (FAST) {
                         if (a.nt_store)
@@ -540,7 +672,12 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
 #pragma unroll 1
                 for (int k = 0; k < KV; ++k) {
                     const int ag = s + k * SLOTS;
-                    if (ag < Nr) dev_add(k, RD > 0 ? mix_row_reg(k) : mix_row(ag), mean);
+                    if (ag < Nr && !(RAG && ag < NH))
+                        dev_add(k, RD > 0 ? mix_row_reg(k) : mix_row(ag), mean);
+                }
+                if (RAG && hub_lane) {
+                    const float d = hy - pick(mean, hc);
+                    hacc += d * d;
                 }
             }
         } else {
@@ -576,7 +713,14 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
         for (int j = 0; j < ND; ++j) {
             const int k = j * C + c;  // the pass this lane's slot j holds
             const int ag = s + k * SLOTS;
-            if (k < KV && ag < Nr) a.dev_partial[(int64_t)blockIdx.x * Nr + ag] = dacc[j];
+            if (k < KV && ag < Nr && !(RAG && ag < NH))
+                a.dev_partial[(int64_t)blockIdx.x * Nr + ag] = dacc[j];
+        }
+        if (RAG && NH > 0) {   // hub rows: the four column lanes' sums (lanes 4h..4h+3, one wave)
+            float v = hacc;
+            v += __shfl_xor(v, 1);
+            v += __shfl_xor(v, 2);
+            if (hub_lane && hc == 0) a.dev_partial[(int64_t)blockIdx.x * Nr + hr] = v;
         }
         if (a.dev_max_zero != nullptr && blockIdx.x == 0 && tid == 0) *a.dev_max_zero = 0u;
     }
@@ -738,7 +882,7 @@ __global__ void __launch_bounds__(1024) stream_triad_tile_kernel(const float4 *_
     }
 }
 
-template <int C, int KV, bool SGD, bool DEV, bool MIX, bool HALO, bool FAST, int RD = 0,
+template <int C, int KV, bool SGD, bool DEV, bool MIX, int HALO, bool FAST, int RD = 0,
           bool LAG = false, int RAG = 0>
 hipError_t launch_one(const TileArgs &a, int grid, int lds, hipStream_t s) {
     auto k = mix_tile_kernel<C, KV, SGD, DEV, MIX, HALO, FAST, RD, LAG, RAG>;
@@ -748,21 +892,30 @@ hipError_t launch_one(const TileArgs &a, int grid, int lds, hipStream_t s) {
     return hipGetLastError();
 }
 
+template <int C, int KV, bool FAST, int H>
+hipError_t launch_part(const TileArgs &a, bool sgd, int grid, int lds, hipStream_t s) {
+    if (tile_lag(a))   // lagged: previous iterate vs mean_prev, colsum_out for the next
+        return sgd ? launch_one<C, KV, true, false, true, H, FAST, 0, true>(a, grid, lds, s)
+                   : launch_one<C, KV, false, false, true, H, FAST, 0, true>(a, grid, lds, s);
+    return sgd ? launch_one<C, KV, true, false, true, H, FAST>(a, grid, lds, s)
+               : launch_one<C, KV, false, false, true, H, FAST>(a, grid, lds, s);
+}
+
 template <int C, int KV, bool FAST>
 hipError_t launch_mode(const TileArgs &a, bool sgd, bool dev, bool mix, int grid, int lds,
                        hipStream_t s) {
-    if (!mix) return launch_one<C, KV, false, true, false, false, FAST>(a, grid, lds, s);
+    if (!mix) return launch_one<C, KV, false, true, false, 0, FAST>(a, grid, lds, s);
     if (tile_partitioned(a)) {  // halo rows / a row set: the exact deviation needs the global mean
-        if (tile_lag(a))        // lagged: previous iterate vs mean_prev, colsum_out for the next
-            return sgd ? launch_one<C, KV, true, false, true, true, FAST, 0, true>(a, grid, lds, s)
-                       : launch_one<C, KV, false, false, true, true, FAST, 0, true>(a, grid, lds, s);
-        return sgd ? launch_one<C, KV, true, false, true, true, FAST>(a, grid, lds, s)
-                   : launch_one<C, KV, false, false, true, true, FAST>(a, grid, lds, s);
+        if (a.tiled && a.n_src > a.n_loc) {   // column-tiled halo blocks: FAST, KV <= 4 only
+            if constexpr (FAST && KV <= 4) return launch_part<C, KV, FAST, 2>(a, sgd, grid, lds, s);
+            return hipErrorInvalidValue;
+        }
+        return launch_part<C, KV, FAST, 1>(a, sgd, grid, lds, s);
     }
-    if (sgd) return dev ? launch_one<C, KV, true, true, true, false, FAST>(a, grid, lds, s)
-                        : launch_one<C, KV, true, false, true, false, FAST>(a, grid, lds, s);
-    return dev ? launch_one<C, KV, false, true, true, false, FAST>(a, grid, lds, s)
-               : launch_one<C, KV, false, false, true, false, FAST>(a, grid, lds, s);
+    if (sgd) return dev ? launch_one<C, KV, true, true, true, 0, FAST>(a, grid, lds, s)
+                        : launch_one<C, KV, true, false, true, 0, FAST>(a, grid, lds, s);
+    return dev ? launch_one<C, KV, false, true, true, 0, FAST>(a, grid, lds, s)
+               : launch_one<C, KV, false, false, true, 0, FAST>(a, grid, lds, s);
 }
 
 // FAST kernels: every C x KV in {2,4,8}; guarded kernels: every C, KV = 8.
@@ -791,10 +944,10 @@ int tile_passes(int chunks, int n_src, bool fast) {
 template <int KV, int RD, int RAG>
 hipError_t launch_reg_kv(const TileArgs &a, bool sgd, bool dev, int grid, int lds, hipStream_t s) {
     if (sgd)
-        return dev ? launch_one<1, KV, true, true, true, false, true, RD, false, RAG>(a, grid, lds, s)
-                   : launch_one<1, KV, true, false, true, false, true, RD, false, RAG>(a, grid, lds, s);
-    return dev ? launch_one<1, KV, false, true, true, false, true, RD, false, RAG>(a, grid, lds, s)
-               : launch_one<1, KV, false, false, true, false, true, RD, false, RAG>(a, grid, lds, s);
+        return dev ? launch_one<1, KV, true, true, true, 0, true, RD, false, RAG>(a, grid, lds, s)
+                   : launch_one<1, KV, true, false, true, 0, true, RD, false, RAG>(a, grid, lds, s);
+    return dev ? launch_one<1, KV, false, true, true, 0, true, RD, false, RAG>(a, grid, lds, s)
+               : launch_one<1, KV, false, false, true, 0, true, RD, false, RAG>(a, grid, lds, s);
 }
 
 template <int RD, int RAG>

@@ -34,9 +34,6 @@ namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-#ifndef MLP_PROBE_MODE
-#define MLP_PROBE_MODE 0   // scripts/mlp_probe builds measurement variants (modes below)
-#endif
 
 constexpr int NTHR = 512;     // 8 waves, 2 per SIMD
 constexpr int MB = 64;        // batch rows per agent
@@ -91,12 +88,6 @@ __device__ __forceinline__ void split2(float x0, float x1, bf16x2 &h, bf16x2 &m,
 }
 
 __device__ __forceinline__ void split4(const f32x4 &x, bf16x4 &h, bf16x4 &m, bf16x4 &l) {
-#if MLP_PROBE_MODE == 10   // measurement only: no split arithmetic (raw bits as the planes)
-    h = __builtin_bit_cast(bf16x4, __builtin_shufflevector(x, x, 0, 1));
-    m = __builtin_bit_cast(bf16x4, __builtin_shufflevector(x, x, 2, 3));
-    l = h;
-    return;
-#endif
     bf16x2 h0, m0, l0, h1, m1, l1;
     split2(x.x, x.y, h0, m0, l0);
     split2(x.z, x.w, h1, m1, l1);
@@ -184,17 +175,10 @@ struct ParMat {
     __device__ __forceinline__ float *at(int r, int c) const { return row.at(off + r * ld + c); }
 };
 
-#ifndef G_NT
-#define G_NT 0
-#endif
-// one gradient value into G (G_NT: non-temporal, so G does not displace X' and the batch in the
-// MALL; measurement knob)
+// one gradient value into G (plain store: non-temporal G stores, so that X' and the batch could
+// stay in the MALL, measured 3722 vs 3722 steps/s)
 __device__ __forceinline__ void gstore(float *p, float v) {
-#if G_NT
-    __builtin_nontemporal_store(v, p);
-#else
     *p = v;
-#endif
 }
 
 // The G addresses of this lane's part of a finished 32 x 32 MFMA tile: register r holds row
@@ -344,9 +328,7 @@ struct RowSlice4 {
 // split once when the producer waves stage them.  A lane's fragment is 8 consecutive k of one
 // row = one ds_read_b128 per plane; the 16-byte chunk c of row n sits at chunk c ^ ((n >> 2) & 3),
 // so the 16 rows a read spans cover all 64 banks.
-#ifndef L1_RING
-#define L1_RING 4                                 // layer-1 slices in flight (producer register sets)
-#endif
+constexpr int L1_RING = 4;                        // layer-1 slices in flight (producer register sets)
 constexpr int L1P_BYTES = 160 * BK * 2;           // 10240 per plane
 __device__ __forceinline__ uint32_t l1_wofs(int n, int k) {   // byte offset in a plane
     return (uint32_t)(n * 64 + ((((k >> 3) ^ (n >> 2)) & 3) << 4) + (k & 7) * 2);
@@ -382,9 +364,6 @@ struct ColSlice {   // loads unconditional, zeroing in store() (see RowSlice)
 
 __device__ __forceinline__ float act_fwd(int layer, float z) {
     if (layer == 0) return z > 0.f ? z : 0.f;   // ReLU
-#if MLP_ACT_PROBE   // measurement only (wrong results): the transcendental activations' cost
-    return z;
-#endif
     if (layer == 1) return tanhf(z);            // Tanh
     return z > 0.f ? z : expm1f(z);             // ELU(alpha = 1)
 }
@@ -412,31 +391,19 @@ __device__ __forceinline__ void mma_rows64(f32x4 (&acc)[5], const float *A, int 
     float a[2], b[2][5];
     auto read = [&](int s, int buf) {
         const int k = 4 * s + (lane >> 4);
-#if MLP_PROBE_MODE == 8   // measurement only: fragments from registers, not LDS
-        a[buf] = (float)(k + m);
-#pragma unroll
-        for (int t = 0; t < 5; ++t) b[buf][t] = (float)(n0 + 16 * t + k);
-        (void)A; (void)lda; (void)Bs;
-#else
         a[buf] = A[m * lda + k];
 #pragma unroll
         for (int t = 0; t < 5; ++t) {
             const int n = n0 + 16 * t;
             b[buf][t] = B_KMAJOR ? Bs[k * LDT + n] : Bs[n * LDS1 + k];
         }
-#endif
     };
     read(0, 0);
 #pragma unroll
     for (int s = 0; s < BK / 4; ++s) {
         if (s + 1 < BK / 4) read(s + 1, (s + 1) & 1);
-#if MLP_PROBE_MODE == 11   // measurement only: hidden fwd / dZ fragments read, no MFMAs
-#pragma unroll
-        for (int t = 0; t < 5; ++t) acc[t][0] += a[s & 1] * b[s & 1][t];
-#else
 #pragma unroll
         for (int t = 0; t < 5; ++t) acc[t] = mfma4(a[s & 1], b[s & 1][t], acc[t]);
-#endif
     }
 }
 
@@ -716,16 +683,12 @@ __device__ __forceinline__ void weight_grad_hidden(const float *dZ, const float 
         for (int r = 0; r < 16; ++r) acc[r] = 0.f;
         const int ia = (t / 5) * 32 + (lane & 31), jb = (t % 5) * 32 + (lane & 31);
         o.prefetch(xo, (t / 5) * 32 + 4 * (lane >> 5), jb, gW, dh, dh, gb);
-#if MLP_PROBE_MODE != 7   // measurement only: 7 = no hidden-layer dW MFMAs
 #pragma unroll 8
         for (int ks = 0; ks < MB / 2; ++ks) {
             const int b = 2 * ks + (lane >> 5);
             acc = mfma32(dZ[b * LDH + ia], Hin[b * LDH + jb], acc);
         }
-#endif
-#if MLP_PROBE_MODE != 6   // measurement only: 6 = no hidden-layer dW stores
         store_tile(acc, xo, (t / 5) * 32 + 4 * (lane >> 5), jb, gW, dh, dh, gb, o);
-#endif
     }
 }
 
@@ -822,9 +785,6 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
             // loads unknown, and the wait before a set's LDS store degrades to vmcnt(0), which
             // drains every slice in flight (measured on this kernel: all 61 waits were vmcnt(0)).
             auto load = [&](int set, int sl) {
-#if MLP_PROBE_MODE == 2   // measurement only: every slice re-reads slice 0 (L2-resident)
-                sl = 0;
-#endif
                 const int k0 = sl * BK;
 #pragma unroll
                 for (int i = 0; i < XQ; ++i) {
@@ -891,7 +851,6 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
             }
             const int m = wave * 16 + (lane & 15), hq = lane >> 4;
             auto compute = [&](const char *img) {
-#if MLP_PROBE_MODE != 1   // measurement only: 1 = no MFMAs
                 const uint32_t oa = l1_wofs(m, 8 * hq);
                 const bf16x8 ah = *reinterpret_cast<const bf16x8 *>(img + oa);
                 const bf16x8 am = *reinterpret_cast<const bf16x8 *>(img + XPL + oa);
@@ -905,9 +864,6 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
                     const bf16x8 bl = *reinterpret_cast<const bf16x8 *>(wpl + 2 * L1P_BYTES + ob);
                     mfma_x6(ah, am, al, bh, bm, bl, acc[t], sml[t]);
                 }
-#else
-                (void)img;
-#endif
             };
             for (int sl = 0; sl < ns; ++sl) {
                 if (sl > 0) compute(img0 + ((sl - 1) & 1) * IMGB);
@@ -940,24 +896,15 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
         pipeline_db<L1>(
             (din + BK - 1) / BK,
             [&](L1 &v, int s) {
-#if MLP_PROBE_MODE == 2   // measurement only: every slice re-reads slice 0 (L2-resident)
-                s = 0;
-#endif
-#if MLP_PROBE_MODE != 3   // measurement only: 3 = no staging at all
                 v.x.load(PlainMat{x, din}, MB, din, s * BK);
                 v.w.load(mat(Xr, o_w1, din), dh, din, s * BK);
-#endif
             },
             [&](const L1 &v, int buf) {
-#if MLP_PROBE_MODE != 3
                 v.x.store(H2 + buf * IMG);
                 v.w.store(H2 + buf * IMG + MB * LDS1);
-#endif
             },
             [&](int s, int buf) {
-#if MLP_PROBE_MODE != 1   // measurement only: 1 = no MFMAs
                 mma_rows64<false>(acc, H2 + buf * IMG, LDS1, H2 + buf * IMG + MB * LDS1);
-#endif
             });
         load_all_w(w5, mat(Xr, o_w2, dh), dh);   // layer 2's weights
         epi_rows64_t(acc, [&](int m, int n, int t, float v) {
@@ -970,9 +917,6 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
     }
     __syncthreads();
     STAMP(1);
-#if MLP_PROBE_MODE == 12   // measurement only: layer 1 alone (PMC of its traffic)
-    return;
-#endif
     forward_hidden_all<L1X6>(mat(Xr, o_b2, 0), dh, H1, H2, stage, 1, w5,
                        [&](int sl) { w5[sl].load(mat(Xr, o_w3, dh), dh, dh, sl * BK); });
     __syncthreads();
@@ -1219,16 +1163,12 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
 #pragma unroll
                 for (int r = 0; r < 16; ++r) acc[r] = 0.f;
                 go.prefetch(xo, 32 * t + 4 * (lane >> 5), c0 + nl, gw1, dh, din, gb1);
-#if MLP_PROBE_MODE != 5   // measurement only: 5 = no dW1 MFMAs
 #pragma unroll 8
                 for (int ks = 0; ks < MB / 2; ++ks) {
                     const int b = 2 * ks + (lane >> 5);
                     acc = mfma32(H1[b * LDH + 32 * t + (lane & 31)], xs[b * LDC + nl], acc);
                 }
-#endif
-#if MLP_PROBE_MODE != 4   // measurement only: 4 = no dW1 stores
                 store_tile(acc, xo, 32 * t + 4 * (lane >> 5), c0 + nl, gw1, dh, din, gb1, go);
-#endif
             }
             __syncthreads();
         }

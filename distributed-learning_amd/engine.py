@@ -35,6 +35,7 @@ class DeviceCsr:
         self.doubly_stochastic = int(csr.doubly_stochastic)
         self.shared_row_weights = int(csr.shared_row_weights)
         self.min_row_nnz = csr.min_row_nnz
+        self.hub_rows = 0       # dl_mix_args.n_hub_rows (plan path 5 hint; GossipEngine sets it)
 
     def c_struct(self):
         return _lib.DlCsr(_lib.ptr(self.rowptr), _lib.ptr(self.col), _lib.ptr(self.w),
@@ -102,18 +103,54 @@ def _check_tiled(t, name, shape, device):
                          f"on {device} (got {tuple(t.shape)}, {t.dtype}, {t.device})")
 
 
+def _tiled_ld(t, name, rows, n_params, tile_cols, device):
+    """Block rows (dl_mix_args ld* in the column-tiled layout) of a [tiles, rows, T] operand: a
+    contiguous tiled matrix, or a view of whole rows / whole tiles of a wider one (a partition
+    row set X[:, a:b], a column chunk X[t0:t1]); its tile stride is ld*T floats."""
+    tiles = (n_params + tile_cols - 1) // tile_cols
+    if t.dtype != torch.float32 or t.device != device or t.dim() != 3 or \
+            tuple(t.shape) != (tiles, rows, tile_cols) or t.stride(2) != 1 or \
+            t.stride(1) != tile_cols or (tiles > 1 and t.stride(0) % tile_cols) or \
+            (tiles > 1 and t.stride(0) < rows * tile_cols):
+        raise ValueError(f"{name} must be a float32 [tiles={tiles}, rows={rows}, T={tile_cols}] "
+                         f"column-tiled tensor (or a row / tile view of one) on {device} "
+                         f"(got {tuple(t.shape)}, strides {t.stride()}, {t.dtype}, {t.device})")
+    return t.stride(0) // tile_cols if tiles > 1 else rows
+
+
 def mix_args_tiled(W: DeviceCsr, n_params, tile_cols, X, Y, G=None, lr=0.0, dev_sq=None,
-                   dev_max=None, mean=None):
-    shape = tiled_shape(W.n_rows, n_params, tile_cols)
-    _check_tiled(X, "X", shape, W.device)
-    _check_tiled(Y, "Y", shape, W.device)
-    if G is not None:
-        _check_tiled(G, "G", shape, W.device)
-    if W.n_src != W.n_rows:
-        raise ValueError("the column-tiled layout takes no halo rows")
-    return _lib.DlMixArgs(
-        _lib.ptr(X), 0, _lib.ptr(Y), 0, int(n_params), W.c_struct(), _lib.ptr(G), 0, float(lr),
-        None, 0, 0, _lib.ptr(dev_sq), _lib.ptr(dev_max), _lib.ptr(mean), int(tile_cols))
+                   dev_max=None, mean=None, halo=None, halo_blocks=None):
+    """dl_mix_args for column-tiled operands (3-D [tiles, rows, T] tensors or row / tile views of
+    them).  X (and G) hold the W.n_local local source rows, Y the W.n_rows output rows; halo rows
+    (W.n_src > W.n_local) come from ``halo``, a contiguous buffer of per-peer tiled blocks of
+    ``halo_blocks`` rows each (dlamd.h n_halo_blocks; None = one block)."""
+    dev = W.device
+    ldx = _tiled_ld(X, "X", W.n_local, n_params, tile_cols, dev)
+    ldy = _tiled_ld(Y, "Y", W.n_rows, n_params, tile_cols, dev)
+    ldg = _tiled_ld(G, "G", W.n_local, n_params, tile_cols, dev) if G is not None else 0
+    n_halo = W.n_src - W.n_local
+    blocks = None
+    if n_halo > 0:
+        tiles = (n_params + tile_cols - 1) // tile_cols
+        if halo is None:
+            raise ValueError(f"graph has {n_halo} halo rows but no halo buffer was given")
+        if halo.dtype != torch.float32 or halo.device != dev or not halo.is_contiguous() or \
+                halo.numel() < tiles * n_halo * tile_cols:
+            raise ValueError(f"halo must be a contiguous float32 buffer of >= {tiles} x {n_halo} "
+                             f"x {tile_cols} floats on {dev}")
+        hb = [int(b) for b in halo_blocks] if halo_blocks is not None else []
+        if hb and sum(hb) != n_halo:
+            raise ValueError(f"halo_blocks {hb} do not sum to the {n_halo} halo rows")
+        blocks = (ctypes.c_int32 * max(len(hb), 1))(*hb) if hb else None
+    args = _lib.DlMixArgs(
+        _lib.ptr(X), ldx, _lib.ptr(Y), ldy, int(n_params), W.c_struct(), _lib.ptr(G), ldg,
+        float(lr), _lib.ptr(halo) if n_halo > 0 else None, 0, n_halo, _lib.ptr(dev_sq),
+        _lib.ptr(dev_max), _lib.ptr(mean), int(tile_cols), None, None,
+        W.n_local if W.n_local != W.n_rows else 0, len(blocks) if blocks is not None else 0,
+        ctypes.cast(blocks, ctypes.c_void_p) if blocks is not None else None)
+    args._keep = blocks   # the host block table must outlive the call
+    args.n_hub_rows = int(getattr(W, "hub_rows", 0))
+    return args
 
 
 def mix_args(W: DeviceCsr, X, Y, G=None, lr=0.0, halo=None, dev_sq=None, dev_max=None,
@@ -130,12 +167,14 @@ def mix_args(W: DeviceCsr, X, Y, G=None, lr=0.0, halo=None, dev_sq=None, dev_max
         if halo is None:
             raise ValueError(f"graph has {n_halo} halo rows but no halo buffer was given")
         _check(halo, "halo", n_halo, P, W.device)
-    return _lib.DlMixArgs(
+    args = _lib.DlMixArgs(
         _lib.ptr(X), _ld(X), _lib.ptr(Y), _ld(Y), P, W.c_struct(),
         _lib.ptr(G), _ld(G) if G is not None else 0, float(lr),
         _lib.ptr(halo) if n_halo > 0 else None, _ld(halo) if n_halo > 0 else 0, n_halo,
         _lib.ptr(dev_sq), _lib.ptr(dev_max), _lib.ptr(mean), 0, None, None,
         W.n_local if W.n_local != n else 0)
+    args.n_hub_rows = int(getattr(W, "hub_rows", 0))
+    return args
 
 
 class Workspace:
@@ -157,16 +196,18 @@ class Workspace:
 
 def mix_round(W: DeviceCsr, X, Y, G=None, lr=0.0, halo=None, dev_sq=None, dev_max=None,
               mean=None, workspace: Workspace = None, tiled=None, mean_prev=None,
-              colsum_out=None):
+              colsum_out=None, halo_blocks=None):
     """One consensus round on the current stream: Y = W (X - lr G) [+ deviation of Y].
-    ``tiled=(n_params, tile_cols)``: X, G, Y are in the column-tiled layout.
+    ``tiled=(n_params, tile_cols)``: X, G, Y are in the column-tiled layout (``halo`` then a
+    buffer of per-peer tiled blocks of ``halo_blocks`` rows, see ``mix_args_tiled``).
     Halo rounds (``halo`` rows): ``mean_prev`` (the global column mean of X), ``colsum_out`` and
     ``dev_sq`` together give the lagged deviation -- dev_sq = ||x_a - mean_prev||^2 of the
     INPUT rows, colsum_out = this rank's column sums of X - lr G (include/dlamd.h)."""
     lib = _lib.load()
     if tiled is not None:
         P = tiled[0]
-        args = mix_args_tiled(W, tiled[0], tiled[1], X, Y, G, lr, dev_sq, dev_max, mean)
+        args = mix_args_tiled(W, tiled[0], tiled[1], X, Y, G, lr, dev_sq, dev_max, mean, halo,
+                              halo_blocks)
     else:
         P = X.shape[1]
         args = mix_args(W, X, Y, G, lr, halo, dev_sq, dev_max, mean)
@@ -367,6 +408,26 @@ def step_rows(X, rows, out, G=None, lr=0.0):
     return out
 
 
+def step_rows_tiled(X, rows, out, G=None, lr=0.0):
+    """Column-tiled dl_step_rows_tiled: out[t, i] = X[t, rows[i]] - lr * G[t, rows[i]] for every
+    tile t -- one peer's halo block [tiles, n_sel, T] (X, G: [tiles, rows, T] or tile views)."""
+    lib = _lib.load()
+    tiles, _, T = X.shape
+    n_sel = rows.numel()
+    if rows.dtype != torch.int32 or rows.device != X.device:
+        raise ValueError("rows must be a device int32 tensor (every entry < X.shape[1]: checked "
+                         "once by the caller, a bad row faults the GPU)")
+    xl = _tiled_ld(X, "X", X.shape[1], tiles * T, T, X.device)
+    gl = _tiled_ld(G, "G", G.shape[1], tiles * T, T, X.device) if G is not None else 0
+    if G is not None and G.shape[1] < X.shape[1]:
+        raise ValueError("G has fewer rows than X")
+    _check_tiled(out, "out", (tiles, n_sel, T), X.device)
+    _lib.check(lib.dl_step_rows_tiled(_lib.ptr(X), xl, _lib.ptr(G), gl, float(lr),
+                                      _lib.ptr(rows), n_sel, tiles * T, T, _lib.ptr(out),
+                                      _lib.stream_handle(X.device)), "dl_step_rows_tiled")
+    return out
+
+
 def perron_round(Y, rowptr, col, eps, conv_eps, weight=None, mean_weight=1.0, max_iter=1 << 30,
                  workspace: Workspace = None, conv_eps_rows=None):
     """In-place asyncio-style consensus round on Y (fp32 or fp64).  Returns the iteration count."""
@@ -385,6 +446,24 @@ def perron_round(Y, rowptr, col, eps, conv_eps, weight=None, mean_weight=1.0, ma
     _lib.check(lib.dl_perron_round(ctypes.byref(args), wp, wn, _lib.stream_handle(Y.device)),
                "dl_perron_round")
     return int(iters.item())
+
+
+HUB_TAIL = 32   # plan path 5: rows with more tail entries than this are folded by column lanes
+
+
+def hub_rows(csr, head, tail=HUB_TAIL, cap=256):
+    """dl_mix_args.n_hub_rows for plan path 5: the leading rows (a descending row-length order
+    puts the longest first) whose LDS tails exceed ``tail`` entries, at most ``cap``.  Measured:
+    a Barabasi-Albert hub's serial fold bounds the tile (irregular graphs).
+    DLAMD_HUB_ROWS=k overrides it (0 = off; measurements)."""
+    env = os.environ.get("DLAMD_HUB_ROWS")
+    if env is not None:
+        return max(0, min(int(env), cap, csr.n_rows))
+    lens = np.diff(np.asarray(csr.rowptr)) - int(head)
+    k = 0
+    while k < min(cap, len(lens)) and lens[k] > tail:
+        k += 1
+    return k
 
 
 # Resident operands of the one-round kernel are streamed together, tile t of X, G and Y at the
@@ -454,6 +533,8 @@ class GossipEngine:
         self.n, self.P = csr.n_rows, int(n_params)
         plan = plan_shape(self.W, self.P, deviation=True,
                           tile_cols=int(tile_cols) if tile_cols else -1)
+        if plan["path"] == 5:
+            self.W.hub_rows = hub_rows(csr, plan["head"])
         tiled_ok = plan["path"] in (1, 4, 5) and plan["tile_cols"] >= 4 and self.W.n_src == self.n
         if layout == "auto":
             layout = "tiled" if tiled_ok else "rows"

@@ -408,6 +408,22 @@ class _LocalEndpoint:
         return t
 
 
+class ResidentHaloTransport:
+    """One rank of an N-rank partition measured alone (``bench.py --workload c4-rank``): the
+    received halo stays resident in its buffers from whatever filled them, sends go nowhere and
+    the all-reduces see one rank.  Every kernel of the rank's round runs at its real shape
+    (pack, interior / boundary or chunked mixes, the lagged deviation) with no interconnect in
+    the timed region."""
+
+    rank = 0
+
+    def exchange(self, sends, recvs):
+        return []
+
+    def all_reduce_(self, t, op="sum"):
+        return t
+
+
 class HipOps:
     """Device compute of a shard: libdlamd kernels (the product path)."""
 
@@ -421,16 +437,19 @@ class HipOps:
         return self.E.DeviceCsr(csr, self.device)
 
     def step_rows(self, X, rows, out, G=None, lr=0.0):
+        if X.dim() == 3:   # column-tiled [tiles, rows, T]
+            return self.E.step_rows_tiled(X, rows, out, G=G, lr=lr)
         return self.E.step_rows(X, rows, out, G=G, lr=lr)
 
-    def mix(self, W, X, Y, G=None, lr=0.0, halo=None, lag=None):
-        """lag = (mean_prev, colsum_out, dev_sq): the lagged deviation of a halo round."""
-        if lag is None:
-            self.E.mix_round(W, X, Y, G=G, lr=lr, halo=halo, workspace=self.ws)
-        else:
-            mean_prev, colsum, dsq = lag
-            self.E.mix_round(W, X, Y, G=G, lr=lr, halo=halo, dev_sq=dsq, mean_prev=mean_prev,
-                             colsum_out=colsum, workspace=self.ws)
+    def mix(self, W, X, Y, G=None, lr=0.0, halo=None, lag=None, halo_blocks=None):
+        """lag = (mean_prev, colsum_out, dev_sq): the lagged deviation of a halo round.
+        Column-tiled operands are 3-D [tiles, rows, T] (views), the halo then a flat buffer of
+        per-peer tiled blocks of ``halo_blocks`` rows."""
+        tiled = (X.shape[0] * X.shape[2], X.shape[2]) if X.dim() == 3 else None
+        mean_prev, colsum, dsq = lag if lag is not None else (None, None, None)
+        self.E.mix_round(W, X, Y, G=G, lr=lr, halo=halo, dev_sq=dsq, mean_prev=mean_prev,
+                         colsum_out=colsum, workspace=self.ws, tiled=tiled,
+                         halo_blocks=halo_blocks)
 
     def column_sum(self, X):
         return self.E.column_sum(X)
@@ -458,37 +477,66 @@ class StripeShard:
 
 
 class HaloShard:
-    """One rank's agent block with halo exchange (row-major X[n_local, P])."""
+    """One rank's agent block with halo exchange.  X, Y (and the caller's G) are resident in the
+    column-tiled layout [P/T][n_local][T] (``layout="tiled"``, the default when the plan allows
+    it: every tile the kernel stages is one contiguous HBM block, 5.7-5.9 TB/s against 3.1-3.8
+    for row-major tiles) or row-major [n_local, P] (``layout="rows"``).
+    Row-major data goes in and out through ``load_rows`` / ``rows`` / ``layout_like``."""
 
     def __init__(self, plan: RankPlan, n_params, device, transport, chunk_cols=None,
-                 n_agents_total=None, ops=None, doubly_stochastic=None, overlap="chunks"):
+                 n_agents_total=None, ops=None, doubly_stochastic=None, overlap="chunks",
+                 layout="auto", tile_cols=None):
         """overlap="chunks": the columns are processed in chunks, the exchange of chunk j+1 in
         flight while chunk j is mixed.  overlap="split" (a boundary-last plan from
         split_halo_plans): ONE exchange of every column per round, in flight while the interior
-        rows mix; the boundary rows mix after it lands (RankPlan.row_sets)."""
+        rows mix; the boundary rows mix after it lands (RankPlan.row_sets).
+        layout: "auto" (tiled when the LDS tile kernel takes every local + halo row at a tile
+        width dividing n_params), "tiled" or "rows"; tile_cols overrides the planner's width."""
         if overlap not in ("chunks", "split"):
             raise ValueError(f"overlap must be 'chunks' or 'split' (got {overlap!r})")
         if overlap == "split" and plan.n_interior < 0:
             raise ValueError("overlap='split' needs a boundary-last plan (split_halo_plans)")
+        if layout not in ("auto", "tiled", "rows"):
+            raise ValueError(f"layout must be 'auto', 'tiled' or 'rows' (got {layout!r})")
         self.overlap = overlap
         self.plan = plan
         self.P = int(n_params)
         self.device = torch.device(device)
         self.transport = transport
         self.ops = ops if ops is not None else HipOps(self.device)
+        self.T = 0
+        if layout != "rows":
+            from .engine import plan_shape
+            T = int(tile_cols) if tile_cols else \
+                plan_shape(plan.csr, self.P, deviation=True, tile_cols=-1)["tile_cols"]
+            if T >= 4 and self.P % T == 0:
+                self.T = T
+            elif layout == "tiled":
+                raise ValueError(f"no column-tiled plan for {plan.n_local} + {plan.n_halo} rows "
+                                 f"x {self.P} params (tile width {T})")
+        self.layout = "tiled" if self.T else "rows"
         self.W = self.ops.csr(plan.csr)
         if overlap == "split":
             ci, cb = plan.row_sets()
             self.W_int = self.ops.csr(ci) if plan.n_interior > 0 else None
             self.W_bnd = self.ops.csr(cb) if plan.n_interior < plan.n_local else None
         self.n_total = n_agents_total
-        self.chunk = int(chunk_cols or self.P)
+        chunk = int(chunk_cols or self.P)
+        if self.T:      # chunks of whole tiles
+            chunk = max(self.T, chunk - chunk % self.T)
+        self.chunk = chunk
+        for q, rows in plan.send_to.items():   # (a row past X would fault the pack kernel)
+            if len(rows) and (int(np.max(rows)) >= plan.n_local or int(np.min(rows)) < 0):
+                raise ValueError(f"send rows for peer {q} index past the {plan.n_local} local rows")
         self.send_rows = {q: torch.as_tensor(rows.astype(np.int32), device=self.device)
                           for q, rows in plan.send_to.items()}
+        # per-peer halo blocks in halo_offset order (dl_mix_args.n_halo_blocks)
+        self.halo_blocks = [len(plan.halo_from[q]) for q in
+                            sorted(plan.halo_from, key=lambda q: plan.halo_offset[q])]
         # X, Y (and the caller's G) stream together: staggered so they do not alias in HBM
         from .engine import staggered_zeros
-        self.X = staggered_zeros((plan.n_local, self.P), 0, self.device)
-        self.Y = staggered_zeros((plan.n_local, self.P), 1, self.device)
+        self.X = staggered_zeros(self._shape(plan.n_local), 0, self.device)
+        self.Y = staggered_zeros(self._shape(plan.n_local), 1, self.device)
         self._bufs = {}
         self.mean_prev = None      # global column mean of X (lagged deviation), once known
         # the lagged deviation needs sum(W t) = sum(t): W doubly stochastic over ALL agents.
@@ -497,31 +545,82 @@ class HaloShard:
         ds = bool(plan.doubly_stochastic)
         self.doubly_stochastic = ds if doubly_stochastic is None else (ds and bool(doubly_stochastic))
 
+    # ---------------------------------------------------------------- layout
+    def _shape(self, rows, width=None):
+        width = self.P if width is None else width
+        return (width // self.T, rows, self.T) if self.T else (rows, width)
+
+    def _cols(self, A, c0, c1):
+        """Columns [c0, c1) of a resident matrix: whole tiles (a contiguous view) when tiled."""
+        return A[c0 // self.T:c1 // self.T] if self.T else A[:, c0:c1]
+
+    def _rows(self, A, r0, r1=None):
+        """Rows [r0, r1) of a resident matrix (a view)."""
+        return A[:, r0:r1] if self.T else A[r0:r1]
+
+    def layout_like(self, A):
+        """A row-major [n_local, P] tensor in the resident layout (a copy; G, X, ...)."""
+        n = self.plan.n_local
+        if tuple(A.shape) != (n, self.P):
+            raise ValueError(f"expected shape ({n}, {self.P}), got {tuple(A.shape)}")
+        A = A.to(self.device, torch.float32)
+        if not self.T:
+            return A.contiguous()
+        return A.reshape(n, self.P // self.T, self.T).permute(1, 0, 2).contiguous()
+
+    def load_rows(self, X):
+        """Set this rank's iterate from row-major [n_local, P] rows (forgets the lagged mean)."""
+        self.X.copy_(self.layout_like(X))
+        self.mean_prev = None
+
+    def rows(self, A=None):
+        """A resident matrix (default X) as row-major [n_local, P] (a copy when tiled)."""
+        A = self.X if A is None else A
+        if not self.T:
+            return A
+        return A.permute(1, 0, 2).reshape(A.shape[1], self.P)
+
+    # ---------------------------------------------------------------- exchange + mix
     def _buffers(self, slot, width):
         """Send/halo buffers of one pipeline slot; chunks alternate between two slots so the
-        exchange of chunk j+1 never lands in the halo chunk j is being mixed from."""
+        exchange of chunk j+1 never lands in the halo chunk j is being mixed from.  Tiled: each
+        peer's halo block [width/T][rows][T] is one contiguous receive buffer, the blocks back to
+        back in one halo buffer (the kernel's n_halo_blocks table)."""
         key = (slot, width)
         if key not in self._bufs:
-            send = {q: torch.empty(len(r), width, device=self.device)
-                    for q, r in self.plan.send_to.items()}
-            halo = torch.empty(self.plan.n_halo, width, device=self.device)
-            recv = {q: halo[self.plan.halo_offset[q]:self.plan.halo_offset[q] + len(ids)]
-                    for q, ids in self.plan.halo_from.items()}
+            pl = self.plan
+            send = {q: torch.empty(self._shape(len(r), width), device=self.device)
+                    for q, r in pl.send_to.items()}
+            if self.T:
+                nt = width // self.T
+                halo = torch.empty(pl.n_halo * width, device=self.device)
+                recv = {q: halo[pl.halo_offset[q] * width:
+                                (pl.halo_offset[q] + len(ids)) * width].view(nt, len(ids), self.T)
+                        for q, ids in pl.halo_from.items()}
+            else:
+                halo = torch.empty(pl.n_halo, width, device=self.device)
+                recv = {q: halo[pl.halo_offset[q]:pl.halo_offset[q] + len(ids)]
+                        for q, ids in pl.halo_from.items()}
             self._bufs[key] = (send, halo, recv)
         return self._bufs[key]
 
     def pack(self, slot, c0, c1, G=None, lr=0.0):
         """Stepped boundary rows x - lr*g of columns [c0, c1) for every peer."""
         send, halo, recv = self._buffers(slot, c1 - c0)
-        Gc = G[:, c0:c1] if G is not None else None
+        Gc = self._cols(G, c0, c1) if G is not None else None
+        Xc = self._cols(self.X, c0, c1)
         for q, rows in self.send_rows.items():
-            self.ops.step_rows(self.X[:, c0:c1], rows, send[q], G=Gc, lr=lr)
+            self.ops.step_rows(Xc, rows, send[q], G=Gc, lr=lr)
         return send, halo, recv
 
+    def _mix(self, W, X, Y, G, lr, halo, lag):
+        self.ops.mix(W, X, Y, G=G, lr=lr, halo=halo, lag=lag,
+                     halo_blocks=self.halo_blocks if (self.T and halo is not None) else None)
+
     def mix_chunk(self, c0, c1, halo, G=None, lr=0.0, lag=None):
-        Gc = G[:, c0:c1] if G is not None else None
-        self.ops.mix(self.W, self.X[:, c0:c1], self.Y[:, c0:c1], G=Gc, lr=lr,
-                     halo=halo if self.plan.n_halo else None, lag=lag)
+        Gc = self._cols(G, c0, c1) if G is not None else None
+        self._mix(self.W, self._cols(self.X, c0, c1), self._cols(self.Y, c0, c1), Gc, lr,
+                  halo if self.plan.n_halo else None, lag)
 
     def chunks(self):
         return [(c, min(c + self.chunk, self.P)) for c in range(0, self.P, self.chunk)]
@@ -604,25 +703,27 @@ class HaloShard:
         send, halo, recv = self.pack(0, 0, self.P, G, lr)
         works = self.transport.exchange(send, recv)
         if ni > 0:
-            self.ops.mix(self.W_int, self.X, self.Y[:ni], G=G, lr=lr, lag=lag)
+            self._mix(self.W_int, self.X, self._rows(self.Y, 0, ni), G, lr, None, lag)
         for w in works:
             w.wait()
         if ni < n:
-            self.ops.mix(self.W_bnd, self.X[nd:], self.Y[ni:], G=None if G is None else G[nd:],
-                         lr=lr, halo=halo, lag=None if ni > 0 else lag)
+            self._mix(self.W_bnd, self._rows(self.X, nd), self._rows(self.Y, ni),
+                      None if G is None else self._rows(G, nd), lr, halo,
+                      None if ni > 0 else lag)
         self.X, self.Y = self.Y, self.X
 
     def _global_mean(self, X):
-        colsum = self.ops.column_sum(X)
+        colsum = self.ops.column_sum(self.rows(X))
         self.transport.all_reduce_(colsum, "sum")
         return colsum / float(self.n_total)
 
     def deviation(self):
         """Global ||x_a - mean||: column sums all-reduced into the global mean, then the local
         rows against it; returns (local dev_sq, global max deviation)."""
-        colsum = self.ops.column_sum(self.X)
+        X = self.rows()
+        colsum = self.ops.column_sum(X)
         self.transport.all_reduce_(colsum, "sum")
         mean = colsum / float(self.n_total)
-        dev_sq, dev_max = self.ops.deviation(self.X, mean)
+        dev_sq, dev_max = self.ops.deviation(X, mean)
         self.transport.all_reduce_(dev_max, "max")
         return dev_sq, dev_max

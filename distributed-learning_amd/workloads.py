@@ -161,6 +161,12 @@ class MLPConsensusSGD:
             raise ValueError("engine and model disagree on agents/params")
         import torch
         self.ann, self.eng = ann, eng
+        # an engine row order (GossipEngine(order=...), "auto" on plan-path-5 graphs) stores
+        # agent eng.order[s] in row s: every per-agent input follows it, so each row still
+        # trains on its own agent's batch (results per agent are those of agent order)
+        if eng.order is not None:
+            data = data.index_select(0, eng.order.to(data.device))
+            labels = labels.index_select(0, eng.order.to(labels.device))
         self.data, self.labels = data, labels
         self.lr, self.deviation = float(lr), bool(deviation)
         if emit == "auto":
@@ -178,8 +184,17 @@ class MLPConsensusSGD:
 
     @property
     def loss(self):
-        """Per-agent mean cross-entropy of the last step (device tensor [N])."""
+        """Per-row mean cross-entropy of the last step (device tensor [N]; row s is agent
+        ``eng.order[s]`` under an engine row order, see ``agent_loss``)."""
         return self.ann.loss
+
+    def agent_loss(self):
+        """Per-agent mean cross-entropy of the last step, in agent order."""
+        if self.eng.order is None:
+            return self.ann.loss
+        out = self._torch.empty_like(self.ann.loss)
+        out[self.eng.order] = self.ann.loss
+        return out
 
     @staticmethod
     def padded_params(csr, n_params, device):

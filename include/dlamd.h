@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define DLAMD_ABI_VERSION 7
+#define DLAMD_ABI_VERSION 8
 
 typedef void *dl_stream_t; /* hipStream_t; NULL = the legacy default stream */
 
@@ -111,9 +111,14 @@ typedef struct dl_mix_args {
     float *dev_max;     /* nullable [1]: max_a sqrt(dev_sq[a])          (n_halo > 0: see mean_prev) */
     float *mean;        /* nullable [n_params]: mean_b(y_b)              (needs n_halo == 0) */
     int32_t tile_cols;  /* 0: x, g, y row-major with ld*.  T > 0: x, g, y in the column-tiled
-                           layout [ceil(n_params/T)][n_rows][T] (each tile one contiguous block,
-                           last tile zero-padded; ld* ignored); T must be the plan's tile_cols
-                           (dl_mix_plan_query on the row-major args).  No halo rows. */
+                           layout [ceil(n_params/T)][rows][T] (each tile one contiguous block,
+                           last tile zero-padded); T must be the plan's tile_cols
+                           (dl_mix_plan_query on the row-major args).  (ABI 8) In this layout
+                           ldx / ldg / ldy are the ROWS of each operand's tiled blocks (tile
+                           stride ld*T floats), 0 = the default (n_local_src for x and g, n_rows
+                           for y): a partition row set passes x / g / y offset by whole rows into
+                           wider blocks.  ldh is ignored; the halo is n_halo_blocks tiled blocks
+                           (below). */
     /* Agent-partitioned rounds (n_halo > 0) with the deviation pipelined one round behind: the
      * global column mean of y needs every rank's rows, so this round's kernel publishes its
      * share of it and measures the PREVIOUS round's iterate -- its input x, staged anyway --
@@ -137,6 +142,22 @@ typedef struct dl_mix_args {
      * (dev_sq / dev_max / mean only as the lagged deviation, which is then per SOURCE row:
      * dev_sq[n_local_src]; workspace dl_mix_workspace_bytes(max(n_rows, n_local_src), ...)). */
     int32_t n_local_src;
+    /* (ABI 8) Halo rows in the column-tiled layout (tile_cols > 0, n_halo > 0): `halo` holds
+     * n_halo_blocks blocks back to back (0 = one block of n_halo rows), block b of
+     * halo_block_rows[b] rows laid out [ceil(n_params/T)][halo_block_rows[b]][T] -- one block per
+     * peer, so that each peer's halo is ONE contiguous receive buffer of the exchange.  Halo row
+     * h of the CSR (source row n_local_src + h) is row h - (rows of blocks before b) of block b.
+     * halo_block_rows is a HOST array of n_halo_blocks <= 16 positive counts summing to n_halo.
+     * The whole halo must span < 4 GiB.  Row-major layout: n_halo_blocks must be 0. */
+    int32_t n_halo_blocks;
+    const int32_t *halo_block_rows;
+    /* (ABI 8) Plan path 5 only (ignored elsewhere), a performance hint: the first n_hub_rows rows
+     * (<= 256; the longest ones first, as in a descending row-length order) are each folded by
+     * four lanes, one column each, instead of by one lane.  A Barabasi-Albert hub's CSR row is
+     * a serial fp32 fold (the reference's order); split by column it is four shorter scalar
+     * chains.  Any value gives the same bits (each column keeps its left fold); the kernel uses
+     * fewer rows when their register heads do not fit LDS. */
+    int32_t n_hub_rows;
 } dl_mix_args;
 
 /* Which kernel configuration dl_mix_round picks (introspection for tests and the bench). */
@@ -152,6 +173,9 @@ typedef struct dl_mix_plan {
     int32_t lds_bytes;  /* dynamic LDS per workgroup */
     int32_t n_tiles;
     int32_t regular;    /* 1 if every row has the same entry count (CSR row_ptr not staged) */
+    int32_t head;       /* (ABI 8) path 5: CSR entries per row kept in registers (2, 3 or 5);
+                           path 4: 5; else 0 */
+    int32_t tail_fmt;   /* (ABI 8) path 5: LDS tail entries of 8 B {weight, row} (2) or 6 B (1) */
 } dl_mix_plan;
 
 int dl_abi_version(void);
@@ -324,6 +348,14 @@ int dl_lds_slot_order(int32_t n_rows, int32_t degree, const int32_t *col, int32_
 int dl_step_rows(const float *x, int64_t ldx, const float *g, int64_t ldg, float lr,
                  const int32_t *rows, int32_t n_sel, int64_t n_params, float *out, int64_t ldo,
                  dl_stream_t stream);
+
+/* (ABI 8) The same in the column-tiled layout: x [ceil(n_params/T)][x_rows][T] and g (nullable)
+ * [..][g_rows][T] -> out [ceil(n_params/T)][n_sel][T] (one peer's halo block of dl_mix_args,
+ * padded columns included).  Packs a rank's boundary rows for one peer of the exchange; a column
+ * chunk of whole tiles is x / g / out offset to its first tile.  16-byte aligned pointers. */
+int dl_step_rows_tiled(const float *x, int32_t x_rows, const float *g, int32_t g_rows, float lr,
+                       const int32_t *rows, int32_t n_sel, int64_t n_params, int32_t tile_cols,
+                       float *out, dl_stream_t stream);
 
 /* Local optimizer step of config c5 (Man_Colab.ipynb cell 19: optimizer = optim.SGD,
  * {'momentum': 0.9, 'weight_decay': 5e-4}, lr 0.02), i.e. torch.optim.SGD.step (torch/optim/sgd.py,

@@ -1,6 +1,7 @@
 #!/bin/bash
 # c4-ba A/B of measurement builds: rounds/s and HBM fraction per variant, e.g. the tail caps of
-# profiles/r10/ba_tail_cap (scripts/build_variant.sh cap32 -DMIX_TAIL_CAP=32; ... cap0 -DMIX_TAIL_CAP=0)
+# profiles/r10/ba_tail_cap (built in r10 with a -DMIX_TAIL_CAP measurement knob, since removed from
+# the product source: those figures are recorded there; VARIANTS names other builds now)
 cd ${GRAFT_REPO_ROOT:-.}
 O=gpurun_out/bavar; mkdir -p $O
 r() { n=$1; shift; timeout -k 10 200 "$@" > $O/$n.log 2>&1 || exit $?; python -c "

@@ -21,13 +21,33 @@ class OracleOps:
         return OracleCsr(csr)
 
     def step_rows(self, X, rows, out, G=None, lr=0.0):
-        Xn = X.numpy()[rows.numpy()]
+        sel = (slice(None), rows.numpy()) if X.dim() == 3 else (rows.numpy(),)  # tiled: every tile
+        Xn = X.numpy()[sel]
         if G is not None:
-            Xn = M.sgd_step(Xn, G.numpy()[rows.numpy()], lr)
+            Xn = M.sgd_step(Xn, G.numpy()[sel], lr)
         out.copy_(torch.from_numpy(np.ascontiguousarray(Xn)))
         return out
 
-    def mix(self, W, X, Y, G=None, lr=0.0, halo=None, lag=None):
+    @staticmethod
+    def _rows(A):
+        """A column-tiled [tiles, rows, T] view as row-major [rows, tiles*T] numpy."""
+        return np.ascontiguousarray(A.numpy().transpose(1, 0, 2).reshape(A.shape[1], -1))
+
+    def mix(self, W, X, Y, G=None, lr=0.0, halo=None, lag=None, halo_blocks=None):
+        if X.dim() == 3:    # column-tiled operands: the same round on their row-major images
+            nt, T_ = X.shape[0], X.shape[2]
+            Hr = None
+            if halo is not None:
+                blocks, off = [], 0
+                for nb in (halo_blocks or [W.n_src - X.shape[1]]):
+                    blocks.append(halo[off:off + nt * nb * T_].view(nt, nb, T_))
+                    off += nt * nb * T_
+                Hr = torch.from_numpy(np.concatenate([self._rows(b) for b in blocks]))
+            Yr = torch.empty(Y.shape[1], nt * T_)
+            self.mix(W, torch.from_numpy(self._rows(X)), Yr,
+                     None if G is None else torch.from_numpy(self._rows(G)), lr, Hr, lag)
+            Y.copy_(Yr.reshape(Y.shape[1], nt, T_).permute(1, 0, 2))
+            return
         T = X.numpy()
         if lag is not None:     # lagged deviation of the input rows + sums of the stepped rows
             mean_prev, colsum, dsq = lag

@@ -265,3 +265,38 @@ def test_mlp_consensus_step_emission_matches_gradient_emission(cuda, layout):
             assert torch.equal(a, b_), emit
     assert MLPConsensusSGD(bann, engine.GossipEngine(csr, cols, device=cuda, layout=layout),
                            data, labels, lr=0.1).emit == "grad"
+
+
+@pytest.mark.parametrize("layout", ["rows", "tiled"])
+def test_mlp_consensus_follows_the_engine_row_order(cuda, layout):
+    """An engine row order (``GossipEngine(order=...)``; "auto" picks one on plan-path-5 graphs)
+    stores agent order[s] in row s.  MLPConsensusSGD permutes the per-agent batches with it, so
+    every agent still trains on its own data: parameters (``eng.rows()``), per-agent losses and
+    deviations equal those of the unpermuted engine bit for bit."""
+    from distributed_learning_amd import engine
+    from distributed_learning_amd.graph import from_edge_weights, random_regular_edges
+    from distributed_learning_amd.networks.batched_ann import BatchedANN
+    from distributed_learning_amd.workloads import MLPConsensusSGD
+    n, b = 48, 64
+    gen = torch.Generator(device=cuda).manual_seed(17)
+    bann = BatchedANN(n, b, 100, 60, 10, device=cuda)
+    P = bann.P
+    X0 = 0.1 * torch.randn(n, P, device=cuda, generator=gen)
+    data = torch.randn(n, b, 100, device=cuda, generator=gen)
+    labels = torch.randint(0, 10, (n, b), device=cuda, generator=gen, dtype=torch.int32)
+    edges = random_regular_edges(4, n, seed=8)
+    csr = from_edge_weights(edges, [0.2] * len(edges), list(range(n)))
+    cols = P if layout == "tiled" else MLPConsensusSGD.padded_params(csr, P, cuda)
+    perm = np.random.default_rng(3).permutation(n)
+    res = {}
+    for name, order in (("agents", None), ("perm", perm)):
+        eng = engine.GossipEngine(csr, cols, device=cuda, layout=layout, order=order,
+                                  X=torch.nn.functional.pad(X0, (0, cols - P)))
+        sgd = MLPConsensusSGD(bann, eng, data, labels, lr=0.1)
+        for _ in range(3):
+            sgd.step()
+        torch.cuda.synchronize()
+        res[name] = (eng.rows().clone(), sgd.agent_loss().clone(), eng.agent_dev_sq().clone())
+    assert torch.equal(res["agents"][0], res["perm"][0])
+    assert torch.equal(res["agents"][1], res["perm"][1])
+    torch.testing.assert_close(res["agents"][2], res["perm"][2], rtol=1e-5, atol=0)

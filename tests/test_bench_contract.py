@@ -20,7 +20,7 @@ def bench():
 
 def test_c2_headline_kernel_has_committed_traffic(bench):
     # c2: 1024 agents, column-tiled T = 16 (4 float4 chunks), fused local step and deviation
-    name = bench.kernel_name({"tile_cols": 16}, sgd=True, dev=True, n_src=1024)
+    name = bench.kernel_name({"tile_cols": 16, "path": 1}, sgd=True, dev=True, n_src=1024)
     traffic, src = bench.traffic_from_profile(name)
     assert traffic is not None, f"{name} not in the default PMC summary"
     # within 1 % of the algorithmic 12 * N * P bytes per round
@@ -60,3 +60,37 @@ def test_halo_probe_failure_carries_child_stderr(bench):
     assert "set_device" in rec["stderr_first_traceback"] or "cuda" in \
         rec["stderr_first_traceback"].lower(), rec
     assert "bench.py" in rec["cmd"]
+
+
+def test_multi_gpu_line_names_both_decompositions(bench):
+    """At N > 1 the c2 line's ``value`` is the column-stripe (P-split) upper bound and the agent
+    partition (the c4 RCCL halo child probe) is a first-class object: both are named."""
+    rec = {"config": {"parallelism": "column stripes x8"}}
+    h = {"status": "ok", "value": 321.0, "hbm": {"frac": 0.6}, "xgmi": {"frac": 0.4},
+         "plan": {"overlap": "split", "layout": "tiled"}}
+    bench.label_decompositions(rec, 8, h)
+    assert rec["decomposition"] == "P-split upper bound"
+    assert "P-split upper bound" in rec["config"]["parallelism"]
+    ap = rec["agent_partition"]
+    assert ap["rounds_per_s"] == 321.0 and ap["hbm_frac"] == 0.6 and ap["xgmi_frac"] == 0.4
+    assert ap["overlap"] == "split" and ap["layout"] == "tiled"
+    assert "agent partition" in ap["decomposition"]
+    assert rec["c4_halo_rounds_per_s"] == 321.0
+    # a failed child probe: the keys stay, with no figures
+    rec2 = {"config": {"parallelism": ""}}
+    bench.label_decompositions(rec2, 2, {"status": "exit 1"})
+    assert rec2["agent_partition"]["rounds_per_s"] is None
+    assert rec2["agent_partition"]["status"] == "exit 1"
+
+
+def test_kernel_names_follow_the_plan(bench):
+    """kernel_name builds the full instantiation rocprofv3 prints, from the plan (the
+    c4-ba instance was hardcoded): path 1, path 4 (register CSR, RD 5) and path 5 (head, tail)."""
+    p1 = bench.kernel_name({"path": 1, "tile_cols": 16}, True, True, 1024)
+    assert p1 == "mix_tile_kernel<4, 4, true, true, true, 0, true, 0, false, 0>(dl::TileArgs)"
+    p4 = bench.kernel_name({"path": 4, "tile_cols": 4, "head": 5, "tail_fmt": 0}, True, True, 4096)
+    assert p4 == "mix_tile_kernel<1, 4, true, true, true, 0, true, 5, false, 0>(dl::TileArgs)"
+    p5 = bench.kernel_name({"path": 5, "tile_cols": 4, "head": 2, "tail_fmt": 2}, True, True, 4096)
+    assert p5 == "mix_tile_kernel<1, 4, true, true, true, 0, true, 2, false, 2>(dl::TileArgs)"
+    h = bench.kernel_name({"path": 1, "tile_cols": 16}, True, False, 608, halo=2, lag=True)
+    assert h == "mix_tile_kernel<4, 4, true, false, true, 2, true, 0, true, 0>(dl::TileArgs)"

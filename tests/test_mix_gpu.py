@@ -254,6 +254,42 @@ def test_full_size_round_column_slices(cuda):
                                rtol=DEV_RTOL)
 
 
+def test_full_size_round_fdla_weights(cuda):
+    """BASELINE config c2 at full size with the mixing weights north_star names: the per-edge
+    FDLA weights of the c2 graph from utils/fast_averaging.py's SDP (the committed
+    tests/golden/fdla_rr4_1024.npz, the weights bench.py's fdla_probe times every run; W = I -
+    L(w), every row its own weights: shared_row_weights 0, all n(d + 1) weights staged).  Fused
+    local step + mix + deviation over 1024 agents x 2^20 params in the column-tiled layout:
+    column slices bit-exact against oracle/cref, the fused deviation within 1e-5 of the oracle's.
+    Reference: utils/fast_averaging.py:4-32 (weights), utils/consensus_simple/mixer.py:47."""
+    import os
+    from distributed_learning_amd.graph import first_appearance_vertices, from_edge_weights
+    E = eng_mod()
+    d = np.load(os.path.join(os.path.dirname(__file__), "golden", "fdla_rr4_1024.npz"))
+    edges = [tuple(int(x) for x in e) for e in d["edges"]]
+    csr = from_edge_weights(edges, d["w"], sorted(first_appearance_vertices(edges)))
+    n, P, lr = csr.n_rows, 1 << 20, 1e-3
+    assert n == 1024 and not csr.shared_row_weights and csr.doubly_stochastic
+    g = torch.Generator(device=cuda).manual_seed(12)
+    X = torch.randn(n, P, device=cuda, generator=g)
+    G = torch.randn(n, P, device=cuda, generator=g)
+    eng = E.GossipEngine(csr, P, device=cuda, X=X)
+    plan = eng.plan(deviation=True)
+    assert plan["path"] == 1 and eng.layout == "tiled"
+    eng.round(G=eng.layout_like(G), lr=lr, deviation=True)
+    torch.cuda.synchronize()
+    Y = eng.rows()
+    for c0, c1 in [(0, 4096), (P - 4096, P), (654321, 654321 + 777)]:
+        want = cref.mix_round(X[:, c0:c1].cpu().numpy(), csr.rowptr, csr.col, csr.w,
+                              G=G[:, c0:c1].cpu().numpy(), lr=lr)
+        assert np.array_equal(bits(Y[:, c0:c1].cpu().numpy()), bits(want)), (c0, c1)
+    want_dsq = cref.deviation_sq(Y.cpu().numpy())
+    np.testing.assert_allclose(np.sqrt(eng.dev_sq.cpu().numpy()), np.sqrt(want_dsq),
+                               rtol=DEV_RTOL)
+    assert float(eng.dev_max.item()) == pytest.approx(float(np.sqrt(want_dsq.max())),
+                                                      rel=DEV_RTOL)
+
+
 def test_full_size_c4_torus_column_slices(cuda):
     """BASELINE config c4 at full size on one GPU (64 x 64 torus, 4096 agents x 2^18 params,
     best-constant weights, fused local step + deviation, the engine's column-tiled layout):

@@ -238,3 +238,37 @@ def test_mixer_4096_irregular_models(cuda, times, eps):
     got = np.stack([torch.cat([p.data.reshape(-1) for p in models[i].parameters()]).cpu().numpy()
                     for i in range(n)])
     assert np.array_equal(bits(got), bits(want))
+
+
+def test_wrong_min_row_nnz_promise_stays_in_bounds(cuda):
+    """dlamd.h: a wrong dl_csr.min_row_nnz promise gives wrong, never out-of-bounds, results.
+    Here two rows (one in the middle, the last) have 2 entries while the CSR promises 5 -- the
+    promise still passes the host's global check (5 n <= nnz) -- so path 5 runs with a register
+    head longer than those rows: the kernel clamps every CSR index it derives into the CSR and
+    the LDS tail.  The launch completes, and the rows before the first short row
+    (their heads and tails are exact) still equal the oracle's fold bit for bit."""
+    from distributed_learning_amd.graph import Csr
+    E = eng_mod()
+    base = dense_irregular(3000, 4, 8, 9)
+    n, k = base.n_rows, 1500
+    rowptr, col, w = [0], [], []
+    for r in range(n):
+        e0, e1 = base.rowptr[r], base.rowptr[r + 1]
+        keep = 2 if r in (k, n - 1) else e1 - e0
+        col.extend(base.col[e0:e0 + keep])
+        w.extend(base.w[e0:e0 + keep])
+        rowptr.append(len(col))
+    csr = Csr(rowptr, col, w, keys=list(range(n)))
+    assert csr.min_row_nnz == 2 and 5 * n <= csr.nnz
+    W = E.DeviceCsr(csr, cuda)
+    W.min_row_nnz = 5                      # the wrong promise
+    assert E.plan_shape(W, 1024, deviation=False)["path"] == 5
+    P = 1024
+    rng = np.random.default_rng(5)
+    X = rng.standard_normal((n, P), dtype=np.float32)
+    Xd = torch.from_numpy(X).to(cuda)
+    Y = torch.zeros_like(Xd)
+    E.mix_round(W, Xd, Y)
+    torch.cuda.synchronize()
+    want = cref.mix_round(X, csr.rowptr, csr.col, csr.w)
+    assert np.array_equal(bits(Y[:k - 100].cpu().numpy()), bits(want[:k - 100]))

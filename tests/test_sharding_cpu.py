@@ -118,7 +118,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, P, chunk, out_dir, lag=False, overlap="chunks"):
+def _worker(rank, world, port, P, chunk, out_dir, lag=False, overlap="chunks", layout="rows"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -135,9 +135,10 @@ def _worker(rank, world, port, P, chunk, out_dir, lag=False, overlap="chunks"):
     # chunked case through the host-staged transport that gloo ranks sharing a GPU use
     tr = sharding.dist_transport() if chunk else sharding.DistTransport()
     sh = sharding.HaloShard(plan, P, "cpu", tr, chunk_cols=chunk,
-                            n_agents_total=64, ops=OracleOps(), overlap=overlap)
-    sh.X = torch.from_numpy(X[plan.local].copy())
-    Gl = torch.from_numpy(G[plan.local].copy())
+                            n_agents_total=64, ops=OracleOps(), overlap=overlap, layout=layout)
+    assert sh.layout == layout
+    sh.load_rows(torch.from_numpy(X[plan.local].copy()))
+    Gl = sh.layout_like(torch.from_numpy(G[plan.local].copy()))
     lagged = []
     for _ in range(3):
         lagged.append(sh.round(G=Gl, lr=0.05, deviation=lag))
@@ -146,24 +147,26 @@ def _worker(rank, world, port, P, chunk, out_dir, lag=False, overlap="chunks"):
         for i, (dsq, dmax) in enumerate(lagged):
             np.save(os.path.join(out_dir, f"lag{rank}_{i}.npy"), dsq.numpy())
             np.save(os.path.join(out_dir, f"lagmax{rank}_{i}.npy"), dmax.numpy())
-    np.save(os.path.join(out_dir, f"x{rank}.npy"), sh.X.numpy())
+    np.save(os.path.join(out_dir, f"x{rank}.npy"), sh.rows().numpy())
     np.save(os.path.join(out_dir, f"ids{rank}.npy"), plan.local)
     np.save(os.path.join(out_dir, f"dmax{rank}.npy"), dev_max.numpy())
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("layout", ["rows", "tiled"])
 @pytest.mark.parametrize("chunk,lag,overlap", [(None, False, "chunks"), (7, False, "chunks"),
                                                (None, True, "chunks"), (7, True, "chunks"),
                                                (None, False, "split"), (None, True, "split")])
-def test_halo_rounds_over_gloo_equal_single_process(tmp_path, chunk, lag, overlap):
+def test_halo_rounds_over_gloo_equal_single_process(tmp_path, chunk, lag, overlap, layout):
     """Real 2-rank gloo halo rounds equal the single-process oracle rounds bit for bit; with
     deviation=True each round also returns the (lagged) deviation of the iterate it started from
     -- measured inside the round, against the all-reduced column sums of the previous round's
     stepped inputs -- within 1e-5 relative of the oracle's deviation of that iterate.
     overlap="split": boundary-last plans, one exchange per round in flight while the interior
-    rows mix, then the boundary rows (same bits)."""
+    rows mix, then the boundary rows (same bits).  layout="tiled": X, Y, G column-tiled, each
+    peer's halo one tiled block (chunks of whole tiles)."""
     world, P = 2, 24
-    mp.spawn(_worker, args=(world, _free_port(), P, chunk, str(tmp_path), lag, overlap),
+    mp.spawn(_worker, args=(world, _free_port(), P, chunk, str(tmp_path), lag, overlap, layout),
              nprocs=world, join=True)
     csr = torus_csr(8, 8)
     rng = np.random.default_rng(0)
@@ -273,8 +276,8 @@ def test_lagged_mean_cleared_by_unlagged_rounds():
     def run(r):
         sh = sharding.HaloShard(plans[r], P, "cpu", tr.endpoint(r), n_agents_total=16,
                                 ops=OracleOps())
-        sh.X = torch.from_numpy(X[plans[r].local].copy())
-        Gl = torch.from_numpy(G[plans[r].local].copy())
+        sh.load_rows(torch.from_numpy(X[plans[r].local].copy()))
+        Gl = sh.layout_like(torch.from_numpy(G[plans[r].local].copy()))
         sh.round(G=Gl, lr=0.1, deviation=True)      # sets mean_prev
         assert sh.mean_prev is not None
         sh.round(G=Gl, lr=0.1, deviation=False)     # moves the mean (local step)

@@ -12,10 +12,11 @@ from distributed_learning_amd.graph import best_constant_weight, from_edge_weigh
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("layout", ["rows", "tiled"])
 @pytest.mark.parametrize("world,chunk,overlap", [(2, None, "chunks"), (4, 300, "chunks"),
                                                  (8, 1000, "chunks"), (2, None, "split"),
                                                  (4, None, "split"), (8, None, "split")])
-def test_virtual_ranks_equal_single_device(cuda, world, chunk, overlap):
+def test_virtual_ranks_equal_single_device(cuda, world, chunk, overlap, layout):
     from distributed_learning_amd import engine as E
     R, C, P = 16, 16, 2048
     edges = torus_edges(R, C)
@@ -33,10 +34,11 @@ def test_virtual_ranks_equal_single_device(cuda, world, chunk, overlap):
     shards = []
     for pl in plans:
         sh = sharding.HaloShard(pl, P, cuda, tr.endpoint(pl.rank), chunk_cols=chunk,
-                                n_agents_total=R * C, overlap=overlap)
+                                n_agents_total=R * C, overlap=overlap, layout=layout)
+        assert sh.layout == layout
         ids = torch.as_tensor(pl.local, device=cuda)
-        sh.X = X[ids].contiguous()
-        shards.append((sh, G[ids].contiguous(), ids))
+        sh.load_rows(X[ids])
+        shards.append((sh, sh.layout_like(G[ids]), ids))
     errs = []
 
     def run(sh, Gl):
@@ -55,24 +57,26 @@ def test_virtual_ranks_equal_single_device(cuda, world, chunk, overlap):
     torch.cuda.synchronize()
     full = ref.rows()
     for sh, _, ids in shards:
-        assert torch.equal(sh.X.view(torch.int32), full[ids].view(torch.int32))
+        assert torch.equal(sh.rows().view(torch.int32), full[ids].view(torch.int32))
     dsq, dmax = ref.deviation()
     for sh, _, ids in shards:
         assert float(sh.dev[1].item()) == pytest.approx(float(dmax.item()), rel=1e-5)
         np.testing.assert_allclose(sh.dev[0].cpu().numpy(), dsq[ids].cpu().numpy(), rtol=1e-5)
 
 
+@pytest.mark.parametrize("layout", ["rows", "tiled"])
 @pytest.mark.parametrize("world,chunk,overlap", [(2, None, "chunks"), (4, 300, "chunks"),
                                                  (8, 1000, "chunks"), (4, None, "split"),
                                                  (8, None, "split")])
-def test_lagged_deviation_in_the_halo_round(cuda, world, chunk, overlap):
+def test_lagged_deviation_in_the_halo_round(cuda, world, chunk, overlap, layout):
     """HaloShard.round(deviation=True): the kernel measures its input rows against the previous
     round's all-reduced mean and publishes the column sums of its stepped inputs (no HBM pass of
     its own).  Iterates stay bit-identical to the single-device round; round i returns the
     deviation of the iterate it started from within 1e-5 relative of ``GossipEngine.deviation``
     on that iterate (the mean differs only by summation order)."""
     from distributed_learning_amd import engine as E
-    R, C, P = 16, 16, 2048 + 36        # ragged tail tile
+    # rows: a ragged tail tile (guarded launch); tiled: whole tiles (the layout's requirement)
+    R, C, P = 16, 16, 2048 + (36 if layout == "rows" else 0)
     edges = torus_edges(R, C)
     verts = list(range(R * C))
     csr = from_edge_weights(edges, [best_constant_weight(edges, verts)] * len(edges), verts)
@@ -90,10 +94,11 @@ def test_lagged_deviation_in_the_halo_round(cuda, world, chunk, overlap):
     shards = []
     for pl in plans:
         sh = sharding.HaloShard(pl, P, cuda, tr.endpoint(pl.rank), chunk_cols=chunk,
-                                n_agents_total=R * C, overlap=overlap)
+                                n_agents_total=R * C, overlap=overlap, layout=layout)
+        assert sh.layout == layout
         ids = torch.as_tensor(pl.local, device=cuda)
-        sh.X = X[ids].contiguous()
-        shards.append((sh, G[ids].contiguous(), ids))
+        sh.load_rows(X[ids])
+        shards.append((sh, sh.layout_like(G[ids]), ids))
     errs = []
 
     def run(sh, Gl):
@@ -110,13 +115,13 @@ def test_lagged_deviation_in_the_halo_round(cuda, world, chunk, overlap):
     torch.cuda.synchronize()
     full = ref.rows()
     for sh, _, ids in shards:
-        assert torch.equal(sh.X.view(torch.int32), full[ids].view(torch.int32))
+        assert torch.equal(sh.rows().view(torch.int32), full[ids].view(torch.int32))
         for (dsq, dmax), (wsq, wmax) in zip(sh.got, want):
             np.testing.assert_allclose(dsq.cpu().numpy(), wsq[ids].cpu().numpy(), rtol=1e-5)
             assert float(dmax.item()) == pytest.approx(float(wmax.item()), rel=1e-5)
 
 
-def _gloo_worker(rank, world, port, chunk, out_dir, overlap="chunks"):
+def _gloo_worker(rank, world, port, chunk, out_dir, overlap="chunks", layout="auto"):
     """One rank of a real multi-process run on the shared GPU: torch.distributed gloo with the
     host-staged transport, the HIP halo path, checked against the single-device round."""
     import os
@@ -138,10 +143,10 @@ def _gloo_worker(rank, world, port, chunk, out_dir, overlap="chunks"):
     tr = sharding.dist_transport()
     assert isinstance(tr, sharding.StagedTransport)
     sh = sharding.HaloShard(plan, P, dev, tr, chunk_cols=chunk, n_agents_total=R * C,
-                            overlap=overlap)
+                            overlap=overlap, layout=layout)
     ids = torch.as_tensor(plan.local, device=dev)
-    sh.X = X[ids].contiguous()
-    Gl = G[ids].contiguous()
+    sh.load_rows(X[ids])
+    Gl = sh.layout_like(G[ids])
     for _ in range(3):
         sh.round(G=Gl, lr=0.01)
     dsq, dmax = sh.deviation()
@@ -150,17 +155,18 @@ def _gloo_worker(rank, world, port, chunk, out_dir, overlap="chunks"):
         ref.round(G=G, lr=0.01)
     rsq, rmax = ref.deviation()
     torch.cuda.synchronize()
-    ok = torch.equal(sh.X.view(torch.int32), ref.rows()[ids].view(torch.int32))
+    ok = torch.equal(sh.rows().view(torch.int32), ref.rows()[ids].view(torch.int32))
     ok = ok and abs(float(dmax.item()) - float(rmax.item())) <= 1e-5 * float(rmax.item())
     ok = ok and bool(torch.allclose(dsq, rsq[ids], rtol=1e-5, atol=0))
     with open(os.path.join(out_dir, f"ok{rank}"), "w") as f:
-        f.write(f"{int(ok)} halo={plan.n_halo} peers={sorted(plan.halo_from)}")
+        f.write(f"{int(ok)} halo={plan.n_halo} peers={sorted(plan.halo_from)} layout={sh.layout}")
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,chunk,overlap", [(2, None, "chunks"), (4, 700, "chunks"),
-                                                 (4, None, "split")])
-def test_processes_over_gloo_equal_single_device(cuda, tmp_path, world, chunk, overlap):
+@pytest.mark.parametrize("world,chunk,overlap,layout", [(2, None, "chunks", "rows"),
+                                                        (4, 700, "chunks", "tiled"),
+                                                        (4, None, "split", "tiled")])
+def test_processes_over_gloo_equal_single_device(cuda, tmp_path, world, chunk, overlap, layout):
     """world processes share the GPU and exchange halos through torch.distributed (gloo, staged
     through the host): the multi-process protocol of bench --workload c4 with the HIP kernels."""
     import socket
@@ -168,21 +174,22 @@ def test_processes_over_gloo_equal_single_device(cuda, tmp_path, world, chunk, o
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
-    mp.spawn(_gloo_worker, args=(world, port, chunk, str(tmp_path), overlap), nprocs=world,
-             join=True)
+    mp.spawn(_gloo_worker, args=(world, port, chunk, str(tmp_path), overlap, layout),
+             nprocs=world, join=True)
     for r in range(world):
         txt = (tmp_path / f"ok{r}").read_text()
         assert txt.startswith("1 "), (r, txt)
 
 
+@pytest.mark.parametrize("layout", ["rows", "tiled"])
 @pytest.mark.parametrize("overlap", ["chunks", "split"])
-def test_virtual_ranks_random_graph_bfs_partition(cuda, overlap):
+def test_virtual_ranks_random_graph_bfs_partition(cuda, overlap, layout):
     """A random 4-regular graph with per-edge weights, agents split by greedy BFS over 3 virtual
     ranks (irregular halos, every rank a different row-set shape): 3 rounds bit-identical to the
     single-device round, with the lagged deviation within 1e-5 of the exact one."""
     from distributed_learning_amd import engine as E
     from distributed_learning_amd.graph import random_regular_edges
-    n, P, world = 300, 1024 + 20, 3
+    n, P, world = 300, 1024 + (20 if layout == "rows" else 0), 3
     edges = random_regular_edges(4, n, seed=11)
     rng = np.random.default_rng(3)
     csr = from_edge_weights(edges, list(rng.uniform(0.05, 0.2, len(edges))), list(range(n)))
@@ -200,10 +207,12 @@ def test_virtual_ranks_random_graph_bfs_partition(cuda, overlap):
     shards = []
     for pl in plans:
         sh = sharding.HaloShard(pl, P, cuda, tr.endpoint(pl.rank), n_agents_total=n,
-                                overlap=overlap, chunk_cols=None if overlap == "split" else 512)
+                                overlap=overlap, chunk_cols=None if overlap == "split" else 512,
+                                layout=layout)
+        assert sh.layout == layout
         ids = torch.as_tensor(pl.local, device=cuda)
-        sh.X = X[ids].contiguous()
-        shards.append((sh, G[ids].contiguous(), ids))
+        sh.load_rows(X[ids])
+        shards.append((sh, sh.layout_like(G[ids]), ids))
     errs = []
 
     def run(sh, Gl):
@@ -220,7 +229,76 @@ def test_virtual_ranks_random_graph_bfs_partition(cuda, overlap):
     torch.cuda.synchronize()
     full = ref.rows()
     for sh, _, ids in shards:
-        assert torch.equal(sh.X.view(torch.int32), full[ids].view(torch.int32))
+        assert torch.equal(sh.rows().view(torch.int32), full[ids].view(torch.int32))
+        for (dsq, dmax), (wsq, wmax) in zip(sh.got, want):
+            np.testing.assert_allclose(dsq.cpu().numpy(), wsq[ids].cpu().numpy(), rtol=1e-5)
+            assert float(dmax.item()) == pytest.approx(float(wmax.item()), rel=1e-5)
+
+
+@pytest.mark.parametrize("overlap", ["chunks", "split"])
+def test_c4_eight_ranks_full_size_tiled(cuda, overlap):
+    """BASELINE config c4 at full size on one GPU: the 64 x 64 torus x 2^18 params split over 8
+    virtual ranks (32 x 16 blocks: 512 local + 96 halo rows each), column-tiled X / Y / G with
+    per-peer tiled halo blocks -- the per-rank kernel an 8-GPU run launches.  Three rounds with
+    the lagged deviation are bit-identical to the single-device round, which itself equals the
+    oracle's C restatement (oracle/cref) on a column slice; every lagged deviation is within 1e-5
+    of the exact one.  Reference: the neighbour exchange it replaces,
+    utils/consensus_asyncio.py:96-118 and consensus_tcp/agent.py:204-207."""
+    from distributed_learning_amd import engine as E
+    from distributed_learning_amd.graph import from_edge_weights as few
+    from oracle import cref
+    import math
+    rows = cols = 64
+    n, P, lr, world = rows * cols, 1 << 18, 1e-3, 8
+    edges = torus_edges(rows, cols)
+    wc = 2.0 / (2.0 - 2.0 * math.cos(2 * math.pi / cols) + 8.0)
+    csr = few(edges, [wc] * len(edges), list(range(n)))
+    g = torch.Generator(device=cuda).manual_seed(41)
+    X = torch.randn(n, P, device=cuda, generator=g)
+    G = torch.randn(n, P, device=cuda, generator=g)
+    cs = slice(1000, 1000 + 96)        # oracle column slice
+    Xs, Gs = X[:, cs].cpu().numpy(), G[:, cs].cpu().numpy()
+    ref = E.GossipEngine(csr, P, device=cuda, X=X)
+    assert ref.layout == "tiled"
+    Gt = ref.layout_like(G)
+    want = []
+    for _ in range(3):
+        want.append(tuple(t.clone() for t in ref.deviation()))
+        ref.round(G=Gt, lr=lr)
+        Xs = cref.mix_round(Xs, csr.rowptr, csr.col, csr.w, G=Gs, lr=lr)
+    del Gt
+    full = ref.rows()
+    assert np.array_equal(full[:, cs].cpu().numpy().view(np.uint32), Xs.view(np.uint32))
+    del ref
+    plans = (sharding.split_halo_plans if overlap == "split" else sharding.halo_plans)(
+        csr, sharding.torus_block_partition(rows, cols, world))
+    tr = sharding.LocalTransport(world)
+    shards = []
+    for pl in plans:
+        assert (pl.n_local, pl.n_halo, len(pl.halo_from)) == (512, 96, 3)
+        sh = sharding.HaloShard(pl, P, cuda, tr.endpoint(pl.rank), n_agents_total=n,
+                                overlap=overlap, chunk_cols=P // 8 if overlap == "chunks" else None)
+        assert sh.layout == "tiled" and sh.halo_blocks == [32, 32, 32]
+        ids = torch.as_tensor(pl.local, device=cuda)
+        sh.load_rows(X[ids])
+        shards.append((sh, sh.layout_like(G[ids]), ids))
+    del X, G
+    errs = []
+
+    def run(sh, Gl):
+        try:
+            sh.got = [sh.round(G=Gl, lr=lr, deviation=True) for _ in range(3)]
+        except Exception as e:  # pragma: no cover
+            errs.append(e)
+    ths = [threading.Thread(target=run, args=(sh, Gl)) for sh, Gl, _ in shards]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert not errs, errs
+    torch.cuda.synchronize()
+    for sh, _, ids in shards:
+        assert torch.equal(sh.rows().view(torch.int32), full[ids].view(torch.int32))
         for (dsq, dmax), (wsq, wmax) in zip(sh.got, want):
             np.testing.assert_allclose(dsq.cpu().numpy(), wsq[ids].cpu().numpy(), rtol=1e-5)
             assert float(dmax.item()) == pytest.approx(float(wmax.item()), rel=1e-5)

@@ -622,18 +622,60 @@ struct TracePlan {
     int32_t grid, chunks;
     int64_t n_steps;
     uint32_t csr_off, scratch_off, lds;
+    int32_t irr;   // 1: mix_trace_irr_kernel (one image, register head + LDS tail)
+    int32_t head;  // irr: CSR entries per row in registers
+    int32_t gm;    // irr: W not doubly stochastic, every round's mean from its outputs
 };
+
+// mix_trace_irr_kernel's configuration: one [N] float4 image, each row's first `head` entries in
+// registers and the rest as 8-byte {weight, row} pairs behind it, a 16 x float4 mean scratch.
+// The tail's u16 row map (setup only) lives in the image area.
+int plan_trace_irr(const dl_mix_args *a, TracePlan *tp) {
+    const dl_csr &W = a->W;
+    const int32_t N = W.n_rows;
+    if (N < 2 || N > 4 * dl::kTileThreads || W.nnz > 65535 + 5 * (int64_t)N)
+        return fail(DL_ERR_UNSUPPORTED, "dl_mix_rounds_trace: no traced kernel for %d agents "
+                                        "with %d CSR entries", N, W.nnz);
+    int head = dl::reg_head_rows(W.min_row_nnz);
+    int64_t ntail = (int64_t)W.nnz - (int64_t)head * N;
+    if (ntail > 65535 || ntail < 0) {
+        head = 0;
+        ntail = W.nnz;
+    }
+    const uint32_t img = (uint32_t)N * 16u;
+    const uint32_t tail = (uint32_t)align_up((size_t)ntail * 8);
+    if (ntail > 65535 || 2 * ntail > (int64_t)img || img + tail + 256u > (uint32_t)dl::kLdsBytes)
+        return fail(DL_ERR_UNSUPPORTED, "dl_mix_rounds_trace: the CSR of %d agents (%d entries) "
+                                        "does not fit LDS beside one image", N, W.nnz);
+    tp->irr = 1;
+    tp->head = head;
+    tp->gm = W.doubly_stochastic ? 0 : 1;
+    tp->chunks = 1;
+    tp->csr_off = img;
+    tp->scratch_off = img + tail;
+    tp->lds = img + tail + 256u;
+    tp->max_rounds = dl::irr_trace_rounds(dl::irr_trace_kv(N));
+    tp->n_steps = a->n_params / 4;
+    tp->grid = (int32_t)balanced_grid(tp->n_steps, device_cus());
+    return DL_OK;
+}
 
 int plan_trace(const dl_mix_args *a, TracePlan *tp) {
     const int32_t N = a->W.n_rows;
+    std::memset(tp, 0, sizeof *tp);
     if (a->n_halo > 0 || local_src(a) != a->W.n_rows)
         return fail(DL_ERR_UNSUPPORTED, "dl_mix_rounds_trace: halo rows need one exchange per "
                                         "round");
-    if (!a->W.doubly_stochastic)
-        return fail(DL_ERR_UNSUPPORTED, "dl_mix_rounds_trace: the per-round deviation needs a "
-                                        "doubly stochastic W (mean(W x) = mean(x))");
     if (a->g)
         return fail(DL_ERR_UNSUPPORTED, "dl_mix_rounds_trace: no local step (g must be NULL)");
+    if (a->n_params % 4)
+        return fail(DL_ERR_UNSUPPORTED, "dl_mix_rounds_trace: n_params must be a multiple of 4");
+    // a W that is not doubly stochastic (every round's mean from its outputs), or an irregular
+    // graph above 2048 agents: the one-image kernel with the register head + LDS tail CSR
+    if (!a->W.doubly_stochastic)
+        return plan_trace_irr(a, tp);
+    if (N > 2 * dl::kTileThreads && !(a->W.uniform_row_nnz == 5 && a->W.shared_row_weights))
+        return plan_trace_irr(a, tp);
     // one agent per thread up to 1024 agents; above, mix_trace_wide_kernel (one column chunk per
     // step, up to 4 agents per thread; the CSR in registers above 2048 agents)
     if (N < 2 || N > 4 * dl::kTileThreads)
@@ -645,8 +687,7 @@ int plan_trace(const dl_mix_args *a, TracePlan *tp) {
     const int32_t n_w = (reg && a->W.shared_row_weights) ? a->W.uniform_row_nnz : a->W.nnz;
     const bool in_regs = a->W.uniform_row_nnz == 5 && n_w == 5;
     const uint32_t csr = in_regs ? 0u : dl::csr_lds_bytes(N, a->W.nnz, reg, n_w);
-    if (!in_regs && csr == 0)
-        return fail(DL_ERR_UNSUPPORTED, "dl_mix_rounds_trace: CSR too large");
+    if (!in_regs && csr == 0) return plan_trace_irr(a, tp);
     const bool wide = N > dl::kTileThreads;
     if (wide && !in_regs && N > 2 * dl::kTileThreads)
         return fail(DL_ERR_UNSUPPORTED, "dl_mix_rounds_trace: above %d agents the traced pass "
@@ -669,9 +710,7 @@ int plan_trace(const dl_mix_args *a, TracePlan *tp) {
             break;
         }
     }
-    if (tp->chunks == 0)
-        return fail(DL_ERR_UNSUPPORTED, "dl_mix_rounds_trace: two column images of %d agents "
-                                        "do not fit LDS", N);
+    if (tp->chunks == 0) return plan_trace_irr(a, tp);   // two images do not fit: one image
     tp->max_rounds = dl::trace_max_rounds(N, in_regs, tp->chunks);
     tp->n_steps = nq / tp->chunks;
     tp->grid = (int32_t)balanced_grid(tp->n_steps, device_cus());
@@ -722,6 +761,8 @@ int dl_mix_rounds_trace(const dl_mix_args *args, int32_t rounds, float *trace, v
         return fail(DL_ERR_UNSUPPORTED, "dl_mix_rounds_trace: operands must be 16-byte aligned "
                                         "float4 rows");
     const int32_t N = args->W.n_rows;
+    if (tp.irr && t.tiled && args->tile_cols % 4)
+        return fail(DL_ERR_INVALID, "dl_mix_rounds_trace: tile_cols must be a multiple of 4");
     if (t.tiled) {
         const int64_t T = args->tile_cols;
         t.lchunks = (int32_t)(T / 4);
@@ -743,8 +784,11 @@ int dl_mix_rounds_trace(const dl_mix_args *args, int32_t rounds, float *trace, v
         return fail(DL_ERR_WORKSPACE, "dl_mix_rounds_trace: needs a 16-byte aligned workspace "
                                       "of %zu bytes (dl_mix_trace_workspace_bytes)", need);
     t.dev_partial = reinterpret_cast<float *>(ws);
-    hipError_t e = dl::launch_mix_trace(t, tp.chunks, rounds, tp.grid, (int)tp.lds, trace,
-                                        static_cast<hipStream_t>(stream));
+    hipError_t e = tp.irr ? dl::launch_mix_trace_irr(t, tp.head, tp.gm != 0, rounds, tp.grid,
+                                                      (int)tp.lds, trace,
+                                                      static_cast<hipStream_t>(stream))
+                          : dl::launch_mix_trace(t, tp.chunks, rounds, tp.grid, (int)tp.lds, trace,
+                                                 static_cast<hipStream_t>(stream));
     return e == hipSuccess ? DL_OK : hip_fail(e, "mix_trace_kernel launch");
 }
 

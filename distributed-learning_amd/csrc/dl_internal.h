@@ -132,6 +132,16 @@ inline int trace_max_rounds(int n_rows, bool in_regs, int chunks) {
 }
 hipError_t launch_mix_trace(const TileArgs &a, int chunks, int rounds, int grid, int lds,
                             float *trace_out, hipStream_t s);
+// mix_trace_irr_kernel (one image, register head + LDS tail of 8-byte pairs, one 4-column
+// chunk per step): irregular graphs of more than 2048 agents and W that are not doubly
+// stochastic (general_mean: every round's column mean from its outputs).  KV agents per thread,
+// irr_trace_rounds(KV) rounds per pass.
+constexpr int irr_trace_kv(int n_rows) {
+    return n_rows <= kTileThreads ? 1 : n_rows <= 2 * kTileThreads ? 2 : 4;
+}
+constexpr int irr_trace_rounds(int kv) { return kv == 1 ? 24 : kv == 2 ? 12 : 4; }
+hipError_t launch_mix_trace_irr(const TileArgs &a, int head, bool general_mean, int rounds,
+                                int grid, int lds, float *trace_out, hipStream_t s);
 // max_zeroed: an earlier launch on the stream already zeroed dev_max (TileArgs::dev_max_zero)
 hipError_t launch_dev_reduce(const float *partial, int nparts, int n_rows, float *dev_sq,
                              float *dev_max, hipStream_t s, bool max_zeroed = false);

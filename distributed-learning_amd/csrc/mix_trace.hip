@@ -546,6 +546,216 @@ __global__ void __launch_bounds__(kTileThreads) mix_trace_wide_kernel(TileArgs a
     }
 }
 
+// Traced passes for the graphs the double-buffered kernels above cannot hold: irregular graphs
+// of more than 2048 agents (Barabasi-Albert hubs, per-entry weights), and any W that is not
+// doubly stochastic (GM).  One LDS image [N] float4 (one 4-column chunk per step) and the CSR as
+// in plan path 5: each row's first RD entries in registers, the rest as 8-byte {weight, row}
+// pairs behind the image.  With one image a round folds every output into registers, waits for
+// all reads of the image, then writes it back (two barriers a round instead of one ping-pong
+// barrier).  GM: mean(W x) != mean(x), so every round's column mean is reduced from its outputs
+// (wave shuffles + a 16-entry scratch) before the deviations of that round -- what
+// Mixer._get_deviation_dict computes after every round (mixer.py:51-66).  The fold is the
+// reference's left fold in CSR order (head, then tail) as in the other kernels: bit-identical.
+// KV agents per thread (rows tid + k * 1024), KR rounds per pass (their deviations in VGPRs).
+template <int KV, int KR, int RD, bool GM>
+__global__ void __launch_bounds__(kTileThreads) mix_trace_irr_kernel(TileArgs a, int rounds) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int NT = kTileThreads;
+    const int tid = threadIdx.x;
+    const int N = a.n_rows;
+    const int nnz = a.nnz;
+    float4 *img = reinterpret_cast<float4 *>(smem);
+    float4 *scratch = reinterpret_cast<float4 *>(smem + a.scratch_off);   // [16]
+    uint2 *ltp = reinterpret_cast<uint2 *>(smem + a.csr_off);
+    const int ntail = nnz - RD * N;
+    constexpr int NRC = RD > 0 ? KV * RD : 1;
+    float rw[NRC];
+    uint32_t ri[(NRC + 1) / 2];
+    uint32_t rdesc[KV];   // row's LDS tail: start (low 16 bits), length (high 16 bits)
+#pragma unroll
+    for (int i = 0; i < (NRC + 1) / 2; ++i) ri[i] = 0u;
+#pragma unroll
+    for (int k = 0; k < KV; ++k) {
+        const int r = tid + k * NT;
+        const int rr = r < N ? r : 0;
+        const int e0 = a.rowptr[rr], e1 = a.rowptr[rr + 1];
+#pragma unroll
+        for (int e = 0; e < (RD > 0 ? RD : 0); ++e) {
+            const int j = k * RD + e;
+            // (clamped into the CSR: a wrong min_row_nnz promise gives wrong results only)
+            const int idx = min(max(e0 + e, 0), nnz - 1);
+            rw[j] = a.w[idx];
+            ri[j >> 1] |= (uint32_t)a.col[idx] << (16 * (j & 1));
+        }
+        const int st = min(max(e0 - RD * rr, 0), ntail);
+        const int ln = min(max(e1 - e0 - RD, 0), ntail - st);
+        rdesc[k] = r < N ? (uint32_t)st | ((uint32_t)ln << 16) : 0u;
+    }
+    {   // stage the tail: a row id per tail slot (u16, in the image area), then the pairs
+        uint16_t *trow = reinterpret_cast<uint16_t *>(smem);
+#pragma unroll
+        for (int k = 0; k < KV; ++k) {
+            const uint32_t t0 = rdesc[k] & 0xffffu, tn = rdesc[k] >> 16;
+            for (uint32_t t = 0; t < tn; ++t) trow[t0 + t] = (uint16_t)(tid + k * NT);
+        }
+        __syncthreads();
+        for (int t = tid; t < ntail; t += NT) {
+            const int e = min(t + RD * (trow[t] + 1), nnz - 1);
+            ltp[t] = make_uint2(__float_as_uint(a.w[e]), (uint32_t)a.col[e]);
+        }
+        __syncthreads();
+    }
+    // agent tid + k * 1024's output from the image: register head, then the LDS tail, four
+    // entries' reads issued per step
+    auto fold = [&](int k) {
+        f32x2 lo = {0.f, 0.f}, hi = {0.f, 0.f};
+#pragma unroll
+        for (int e = 0; e < (RD > 0 ? RD : 0); ++e) {
+            const int j = k * RD + e;
+            const uint32_t idx = (ri[j >> 1] >> (16 * (j & 1))) & 0xffffu;
+            fold2(lo, hi, rw[j], *reinterpret_cast<const f32x4 *>(img + idx));
+        }
+        uint32_t t = rdesc[k] & 0xffffu;
+        const uint32_t t1 = t + (rdesc[k] >> 16);
+        constexpr int TU = KV >= 4 ? 2 : 4;   // (4 agents' outputs and prefetch: fewer in flight)
+        for (; t + TU <= t1; t += TU) {
+            uint2 p4[TU];
+            f32x4 v4[TU];
+#pragma unroll
+            for (int u = 0; u < TU; ++u) p4[u] = ltp[t + u];
+#pragma unroll
+            for (int u = 0; u < TU; ++u) v4[u] = *reinterpret_cast<const f32x4 *>(img + p4[u].y);
+#pragma unroll
+            for (int u = 0; u < TU; ++u) fold2(lo, hi, __uint_as_float(p4[u].x), v4[u]);
+        }
+        for (; t < t1; ++t) {
+            const uint2 pr = ltp[t];
+            fold2(lo, hi, __uint_as_float(pr.x), *reinterpret_cast<const f32x4 *>(img + pr.y));
+        }
+        return make_float4(lo.x, lo.y, hi.x, hi.y);
+    };
+    // column mean of this step's chunk over every agent: per-thread sums -> wave -> scratch
+    auto reduce_mean = [&](float4 cs) {
+#pragma unroll
+        for (int m = 1; m < 64; m <<= 1) {
+            cs.x += __shfl_xor(cs.x, m);
+            cs.y += __shfl_xor(cs.y, m);
+            cs.z += __shfl_xor(cs.z, m);
+            cs.w += __shfl_xor(cs.w, m);
+        }
+        if ((tid & 63) == 0) scratch[tid >> 6] = cs;
+    };
+    auto read_mean = [&]() {
+        float4 m4 = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 2
+        for (int wv = 0; wv < NT / 64; ++wv) {
+            const float4 p = scratch[wv];
+            m4.x += p.x;
+            m4.y += p.y;
+            m4.z += p.z;
+            m4.w += p.w;
+        }
+        const float n = (float)N;
+        return make_float4(m4.x / n, m4.y / n, m4.z / n, m4.w / n);
+    };
+    const int lsh = __builtin_ctz((unsigned)a.lchunks);
+    const int64_t lmask = (int64_t)a.lchunks - 1;
+    auto off = [&](int64_t ts, int64_t row, int64_t q) {
+        return (q >> lsh) * ts + row + (q & lmask) * 16;
+    };
+    const char *xb = reinterpret_cast<const char *>(a.x);
+    char *yb = reinterpret_cast<char *>(a.y);
+    const int64_t nsteps = a.n_tiles;
+    float dacc[KV][KR];
+#pragma unroll
+    for (int k = 0; k < KV; ++k)
+#pragma unroll
+        for (int r = 0; r < KR; ++r) dacc[k][r] = 0.f;
+    float4 px[KV];
+    auto prefetch = [&](int64_t q) {
+#pragma unroll
+        for (int k = 0; k < KV; ++k) {
+            const int ag = tid + k * NT < N ? tid + k * NT : 0;   // ragged: row 0 (L1 hit)
+            px[k] = tr_load4(xb + off(a.xts, (int64_t)ag * a.xrs, q));
+        }
+    };
+    int64_t q = blockIdx.x;
+    if (q < nsteps) prefetch(q);
+    for (; q < nsteps; q += gridDim.x) {
+        float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int k = 0; k < KV; ++k) {
+            const int ag = tid + k * NT;
+            if (ag < N) {
+                img[ag] = px[k];
+                cs.x += px[k].x;
+                cs.y += px[k].y;
+                cs.z += px[k].z;
+                cs.w += px[k].w;
+            }
+        }
+        if (!GM) reduce_mean(cs);   // mean(W^r x) = mean(x): one mean per step
+        __syncthreads();
+        float4 mean = GM ? make_float4(0.f, 0.f, 0.f, 0.f) : read_mean();
+        // the next step's chunk lands during the rounds (at 4 agents per thread after them: the
+        // prefetch registers beside 4 agents' head CSR and outputs spill)
+        constexpr bool PF = KV < 4;
+        if (PF && q + gridDim.x < nsteps) prefetch(q + gridDim.x);
+#pragma unroll
+        for (int r = 0; r < KR; ++r) {
+            if (r < rounds) {
+                const bool last = r + 1 == rounds;
+                float4 y[KV];
+#pragma unroll
+                for (int k = 0; k < KV; ++k) {
+                    if (tid + k * NT < N) y[k] = fold(k);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                __syncthreads();   // every read of the image is done
+                float4 ys = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+                for (int k = 0; k < KV; ++k) {
+                    const int ag = tid + k * NT;
+                    if (ag < N) {
+                        if (!last)
+                            img[ag] = y[k];
+                        else
+                            tr_store4(y[k], yb + off(a.yts, (int64_t)ag * a.yrs, q));
+                        ys.x += y[k].x;
+                        ys.y += y[k].y;
+                        ys.z += y[k].z;
+                        ys.w += y[k].w;
+                    }
+                }
+                if (GM) {   // this round's column mean, from its outputs
+                    reduce_mean(ys);
+                    __syncthreads();   // (also: the image complete before the next round reads)
+                    mean = read_mean();
+                } else if (!last) {
+                    __syncthreads();   // the image complete before the next round reads it
+                }
+                const f32x2 mlo = {mean.x, mean.y}, mhi = {mean.z, mean.w};
+#pragma unroll
+                for (int k = 0; k < KV; ++k)
+                    if (tid + k * NT < N)
+                        dacc[k][r] += dev2(f32x2{y[k].x, y[k].y}, f32x2{y[k].z, y[k].w}, mlo, mhi);
+            }
+        }
+        // (GM) the last round's scratch reads finish before the next step writes scratch: that
+        // write comes after round 0's first barrier
+        if (!PF && q + gridDim.x < nsteps) prefetch(q + gridDim.x);
+    }
+#pragma unroll
+    for (int k = 0; k < KV; ++k) {
+        const int ag = tid + k * NT;
+        if (ag < N) {
+#pragma unroll
+            for (int r = 0; r < KR; ++r)
+                if (r < rounds) a.dev_partial[((int64_t)blockIdx.x * rounds + r) * N + ag] = dacc[k][r];
+        }
+    }
+}
+
 // out[r] = max_a sqrt(sum_b partial[b][r][a]) (fp64 sum in workgroup order, then float, as
 // dev_reduce's dev_sq); one workgroup per round.
 __global__ void __launch_bounds__(1024) trace_reduce_kernel(const float *__restrict__ partial,
@@ -633,7 +843,50 @@ hipError_t launch_wide(const TileArgs &a, int rounds, int grid, int lds, hipStre
     return hipGetLastError();
 }
 
+template <int KV, int RD, bool GM>
+hipError_t launch_irr3(const TileArgs &a, int rounds, int grid, int lds, hipStream_t s) {
+    constexpr int KR = irr_trace_rounds(KV);
+    auto k = mix_trace_irr_kernel<KV, KR, RD, GM>;
+    hipError_t e = allow_full_lds(reinterpret_cast<const void *>(k));
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k, dim3(grid), dim3(kTileThreads), lds, s, a, rounds);
+    return hipGetLastError();
+}
+
+template <int KV, bool GM>
+hipError_t launch_irr2(const TileArgs &a, int head, int rounds, int grid, int lds,
+                       hipStream_t s) {
+    switch (head) {
+        case 0: return launch_irr3<KV, 0, GM>(a, rounds, grid, lds, s);
+        case 2: return launch_irr3<KV, 2, GM>(a, rounds, grid, lds, s);
+        case 3: return launch_irr3<KV, 3, GM>(a, rounds, grid, lds, s);
+        case 5: return launch_irr3<KV, 5, GM>(a, rounds, grid, lds, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+template <bool GM>
+hipError_t launch_irr1(const TileArgs &a, int head, int rounds, int grid, int lds,
+                       hipStream_t s) {
+    if (a.n_rows <= kTileThreads) return launch_irr2<1, GM>(a, head, rounds, grid, lds, s);
+    if (a.n_rows <= 2 * kTileThreads) return launch_irr2<2, GM>(a, head, rounds, grid, lds, s);
+    return launch_irr2<4, GM>(a, head, rounds, grid, lds, s);
+}
+
 }  // namespace
+
+hipError_t launch_mix_trace_irr(const TileArgs &a, int head, bool general_mean, int rounds,
+                                int grid, int lds, float *trace_out, hipStream_t s) {
+    if (rounds < 1 || rounds > irr_trace_rounds(irr_trace_kv(a.n_rows)) || a.n_rows < 2 ||
+        a.n_rows > 4 * kTileThreads || a.lchunks < 1)
+        return hipErrorInvalidValue;
+    hipError_t e = general_mean ? launch_irr1<true>(a, head, rounds, grid, lds, s)
+                                : launch_irr1<false>(a, head, rounds, grid, lds, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(trace_reduce_kernel, dim3(rounds), dim3(1024), 0, s, a.dev_partial, grid,
+                       rounds, a.n_rows, trace_out);
+    return hipGetLastError();
+}
 
 hipError_t launch_mix_trace(const TileArgs &a, int chunks, int rounds, int grid, int lds,
                             float *trace_out, hipStream_t s) {

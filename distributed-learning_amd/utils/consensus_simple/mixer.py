@@ -206,14 +206,17 @@ class Mixer(object):
         P = X.shape[1]
         Pp = -(-P // 64) * 64
         cur = torch.nn.functional.pad(X, (0, Pp - P)) if Pp != P else X
+        nxt = torch.empty_like(cur)
+        # whether the traced kernel fits is decided before any layout copy: the
+        # row-major plan has the tiled one's depth (one 4-column chunk per step above 1024 agents)
+        K = min(_engine.trace_max_rounds(W, cur, nxt), self._TRACE_MAX_ROUNDS)
+        if K < min(self._TRACE_MIN_ROUNDS, self._TRACE_MAX_ROUNDS):
+            return X, 0, False
         tiled = None
         if W.n_rows > self._TRACE_TILED_ABOVE:
             tiled = (Pp, 4)
             cur = _engine.to_tiled(cur, 4)
-        nxt = torch.empty_like(cur)
-        K = min(_engine.trace_max_rounds(W, cur, nxt, tiled=tiled), self._TRACE_MAX_ROUNDS)
-        if K < min(self._TRACE_MIN_ROUNDS, self._TRACE_MAX_ROUNDS):
-            return X, 0, False
+            nxt = nxt.view(_engine.tiled_shape(W.n_rows, Pp, 4))   # same bytes, tiled shape
         trace = torch.empty(K, dtype=torch.float32, device=X.device)
         ws = self._wspace()
         done = 0
@@ -225,10 +228,13 @@ class Mixer(object):
                 max_dev = np.float32(d)
                 gap = abs(float(max_dev) - float(eps))
                 if gap <= 0.1 * abs(float(eps)):
-                    if floor is None:   # mean(W^k x) = mean(x): one column sum per call
-                        mean = _engine.column_sum(X) / X.shape[0]
+                    if floor is None:
+                        if W.doubly_stochastic:   # mean(W^k x) = mean(x): one column sum
+                            ref = (_engine.column_sum(X) / X.shape[0]).abs().max()
+                        else:   # a row-stochastic W keeps every mean inside X's entry range
+                            ref = X.abs().max()
                         floor = 8.0 * np.sqrt(P) * float(np.finfo(np.float32).eps) * \
-                            float(mean.abs().max().item())
+                            float(ref.item())
                     if gap <= self._TIE_RTOL * abs(float(eps)) + floor:
                         max_dev = self._recheck_deviation(W, cur, i + 1, P, tiled)
                 self.logger.debug('Mixer calculate max deviation= {}'.format(max_dev))

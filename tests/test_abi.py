@@ -196,3 +196,68 @@ def test_mix_until_validates_and_sizes():
     u.n_params = u.ldx = u.ldy = 1 << 20
     assert lib.dl_mix_until(ctypes.byref(u), None) == _lib.DL_ERR_UNSUPPORTED
     assert b"LDS" in lib.dl_last_error()
+
+
+def test_tiled_halo_arguments_validate_without_a_gpu():
+    """ABI 8 (column-tiled halo rounds): the per-peer block table, the tiled ld* (block rows)
+    and the whole-tile requirement are checked on the host, before any launch; the planner picks
+    a tile width for every source row (local + halo) that divides n_params and keeps the halo
+    kernel at <= 4 row passes per thread (runs without a GPU)."""
+    from distributed_learning_amd import _lib
+    lib = _lib.load()
+    pl = _lib.DlMixPlan()
+    # the c4 rank of 8: 512 local rows + 96 halo rows, 2^18 params -> T = 16 (608 x 16 x 16 B)
+    _lib.check(lib.dl_mix_plan_shape(512, 96, 1 << 18, 5 * 512, 5, 1, 1, -1, ctypes.byref(pl)),
+               "plan")
+    assert pl.path == 1 and pl.tile_cols == 16
+    # a width that does not divide n_params is halved until it does
+    _lib.check(lib.dl_mix_plan_shape(512, 96, 1000, 5 * 512, 5, 1, 1, -1, ctypes.byref(pl)),
+               "plan")
+    assert pl.tile_cols == 8
+    # more than 4 passes of 1024 threads at C chunks: a narrower tile (here 3000 + 100 rows)
+    _lib.check(lib.dl_mix_plan_shape(3000, 100, 1 << 16, 5 * 3000, 5, 1, 1, -1, ctypes.byref(pl)),
+               "plan")
+    assert (3100 * pl.tile_cols // 4) <= 4 * 1024
+
+    def args(**kw):
+        a = _lib.DlMixArgs()
+        a.x, a.y, a.halo = 1 << 20, 1 << 30, 1 << 34
+        a.n_params, a.tile_cols = 64, 16
+        a.W = _lib.DlCsr(16, 16, 16, 4, 20, 5, 1, 1, 5)
+        a.n_halo = 4
+        for k, v in kw.items():
+            setattr(a, k, v)
+        return a
+
+    def err(a):
+        rc = lib.dl_mix_round(ctypes.byref(a), None, 0, None)
+        return rc, lib.dl_last_error()
+
+    rows = (ctypes.c_int32 * 2)(1, 2)          # sums to 3, not n_halo = 4
+    rc, msg = err(args(n_halo_blocks=2, halo_block_rows=ctypes.cast(rows, ctypes.c_void_p)))
+    assert rc == _lib.DL_ERR_INVALID and b"sum" in msg
+    rc, msg = err(args(n_halo_blocks=2, halo_block_rows=None))
+    assert rc == _lib.DL_ERR_INVALID and b"halo_block_rows" in msg
+    rc, msg = err(args(n_halo_blocks=17))
+    assert rc == _lib.DL_ERR_INVALID and b"n_halo_blocks" in msg
+    zero = (ctypes.c_int32 * 2)(4, 0)
+    rc, msg = err(args(n_halo_blocks=2, halo_block_rows=ctypes.cast(zero, ctypes.c_void_p)))
+    assert rc == _lib.DL_ERR_INVALID and b"<= 0" in msg
+    rc, msg = err(args(n_params=72))           # not whole tiles of 16
+    assert rc == _lib.DL_ERR_INVALID and b"tile_cols" in msg
+    rc, msg = err(args(ldx=2))                  # block rows below the local rows
+    assert rc == _lib.DL_ERR_INVALID and b"ldx" in msg
+    rc, msg = err(args(tile_cols=0, ldx=64, ldy=64, ldh=64, n_halo_blocks=1))
+    assert rc == _lib.DL_ERR_INVALID and b"n_halo_blocks" in msg
+    rc, msg = err(args(y=(1 << 34) + 64))       # y inside the halo blocks
+    assert rc == _lib.DL_ERR_INVALID and b"halo" in msg
+    rc, msg = err(args(n_hub_rows=-1))
+    assert rc == _lib.DL_ERR_INVALID and b"n_hub_rows" in msg
+    # dl_step_rows_tiled: arguments before any launch
+    assert lib.dl_step_rows_tiled(None, 4, None, 0, 0.0, None, 2, 64, 16, None, None) == \
+        _lib.DL_ERR_INVALID
+    assert lib.dl_step_rows_tiled(1 << 20, 4, None, 0, 0.0, 1 << 22, 2, 64, 12, 1 << 24,
+                                  None) == _lib.DL_ERR_INVALID          # T not a power of 2
+    assert lib.dl_step_rows_tiled(1 << 20, 4, None, 0, 0.0, 1 << 22, 2, 64, 16,
+                                  (1 << 20) + 16, None) == _lib.DL_ERR_INVALID   # out overlaps x
+    assert b"overlaps" in lib.dl_last_error()

@@ -272,3 +272,41 @@ def test_wrong_min_row_nnz_promise_stays_in_bounds(cuda):
     torch.cuda.synchronize()
     want = cref.mix_round(X, csr.rowptr, csr.col, csr.w)
     assert np.array_equal(bits(Y[:k - 100].cpu().numpy()), bits(want[:k - 100]))
+
+
+@pytest.mark.parametrize("times,eps", [(1, 0.3), (5, 0.02)])
+def test_mixer_traced_row_stochastic_4096(cuda, monkeypatch, times, eps):
+    """Mixer.mix(times, eps) over 4096 models whose topology is row- but not column-stochastic
+    (the graph of test_row_stochastic_two_pass_deviation: the reference Mixer takes any
+    dict-of-dicts weights, mixer.py:47, and tests eps after every round, :27-32, 40-41).  The
+    loop runs as traced passes (dl_mix_rounds_trace on the one-image kernel, every round's column
+    mean reduced from its outputs) -- not one launch and readback per round -- and returns the
+    reference loop's round count and bits."""
+    import logging
+    from oracle import mixer_ref as M
+    from distributed_learning_amd.utils.consensus_simple import Mixer
+    from distributed_learning_amd.utils.consensus_simple import mixer as mixer_mod
+    csr = dense_irregular(4096, 4, 9, 7, row_stochastic=True)
+    n = csr.n_rows
+    topo = {i: {int(csr.col[e]): float(csr.w[e]) for e in range(csr.rowptr[i], csr.rowptr[i + 1])}
+            for i in range(n)}
+    torch.manual_seed(9)
+    models = {i: torch.nn.Linear(24, 8).to(cuda) for i in range(n)}
+    X0 = np.stack([torch.cat([p.data.reshape(-1) for p in models[i].parameters()]).cpu().numpy()
+                   for i in range(n)])
+    rp, cl, w = M.topology_to_csr(topo)
+    want, want_n = M.mixer_mix(X0, rp, cl, w, times=times, eps=eps)
+    assert want_n >= 3                 # several rounds, so the passes are what runs
+    calls = []
+    real = mixer_mod._engine.mix_rounds_trace
+
+    def traced(*a, **k):
+        calls.append(a[3])
+        return real(*a, **k)
+    monkeypatch.setattr(mixer_mod._engine, "mix_rounds_trace", traced)
+    m = Mixer(models, topo, logging.getLogger("rowstoch4096"))
+    assert m.mix(times=times, eps=eps) == want_n
+    assert calls and all(k == 4 for k in calls), calls
+    got = np.stack([torch.cat([p.data.reshape(-1) for p in models[i].parameters()]).cpu().numpy()
+                    for i in range(n)])
+    assert np.array_equal(bits(got), bits(want))

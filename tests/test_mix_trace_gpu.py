@@ -67,10 +67,20 @@ def torus_csr(side):
 # metropolis rows (irregular) the chunk-major planes kernel.  Above 1024 agents the wide kernel
 # (one column chunk per step, 2 or 4 agents per thread): rr4 2048 (FULL, CSR in registers), rr4
 # 3000 (ragged, 4 per thread), the c4 torus (4096, FULL), sparse Metropolis 1500 (CSR in LDS)
+# The one-image kernel (mix_trace_irr_kernel: register head + LDS tail CSR, one 4-column chunk
+# per step) takes the rest: Barabasi-Albert 4096 (irregular above 2048 agents, 3-entry head) and
+# W that are row- but not column-stochastic at 300 / 1500 / 4096 agents (1 / 2 / 4 per thread;
+# every round's column mean reduced from its outputs).
 CASES = [("rr4", 64, 4096, 0), ("rr4", 1024, 256, 1), ("metro", 50, 1000, 2),
          ("metro", 7, 4, 3), ("rr4", 16, 65536, 4), ("rr4", 300, 512, 5), ("rr4", 1000, 128, 6),
          ("rr4", 256, 1024, 7), ("rr4", 512, 512, 8), ("rr4", 2048, 256, 9),
-         ("rr4", 3000, 128, 10), ("torus", 4096, 256, 11), ("metro_sparse", 1500, 192, 12)]
+         ("rr4", 3000, 128, 10), ("torus", 4096, 256, 11), ("metro_sparse", 1500, 192, 12),
+         ("ba", 4096, 256, 13), ("rowstoch", 4096, 128, 14), ("rowstoch", 300, 256, 15),
+         ("rowstoch", 1500, 128, 16)]
+T_TILED = 16
+# the column-tiled layout needs whole tiles: widths that are not a multiple of T run row-major only
+LAYOUT_CASES = [(c, lay) for c in CASES for lay in ("rows", "tiled")
+                if lay == "rows" or c[2] % T_TILED == 0]
 
 
 def make(kind, n, seed):
@@ -78,24 +88,28 @@ def make(kind, n, seed):
         return rr_csr(n, seed)
     if kind == "torus":
         return torus_csr(int(round(n ** 0.5)))
+    if kind == "ba":
+        from distributed_learning_amd.graph import barabasi_albert_metropolis
+        return barabasi_albert_metropolis(n, 2, seed)
+    if kind == "rowstoch":
+        from test_mix_ragged_gpu import dense_irregular
+        return dense_irregular(n, 4, 9, seed, row_stochastic=True)
     return metropolis_csr(n, 3.0 / n if kind == "metro_sparse" else 0.1, seed)
 
 
-@pytest.mark.parametrize("kind,n,P,seed", CASES)
-@pytest.mark.parametrize("layout", ["rows", "tiled"])
-def test_trace_pass_matches_round_by_round(cuda, kind, n, P, seed, layout):
+@pytest.mark.parametrize("case,layout", LAYOUT_CASES)
+def test_trace_pass_matches_round_by_round(cuda, case, layout):
+    kind, n, P, seed = case
     e = E()
     csr = make(kind, n, seed)
-    assert csr.doubly_stochastic
+    assert csr.doubly_stochastic == (kind != "rowstoch")
     rng = np.random.default_rng(seed)
     X = rng.standard_normal((n, P), dtype=np.float32)
     W = e.DeviceCsr(csr, cuda)
     Xd = torch.from_numpy(X).to(cuda)
     tiled = None
     if layout == "tiled":
-        T = 16
-        if P % T:
-            pytest.skip("tiled layout needs whole tiles here")
+        T = T_TILED
         Xd = e.to_tiled(Xd, T)
         tiled = (P, T)
     Yd = torch.full_like(Xd, float("nan"))
@@ -107,12 +121,13 @@ def test_trace_pass_matches_round_by_round(cuda, kind, n, P, seed, layout):
     e.mix_rounds_trace(W, Xd, Yd, K, trace, tiled=tiled)
     assert torch.equal(Xd, X0)                     # the pass input is left intact
     got = (e.from_tiled(Yd, P) if tiled else Yd).cpu().numpy()
-    Z, ref = X, []
+    Z, ref, floor = X, [], []
     for _ in range(K):
         Z = M.mix_once(Z, csr.rowptr, csr.col, csr.w)
         ref.append(M.deviation(Z).max())
+        floor.append(noise_floor(Z))    # (row-stochastic W: the mean moves every round)
     assert np.array_equal(bits(got), bits(Z))
-    np.testing.assert_allclose(trace.cpu().numpy(), ref, rtol=1e-5, atol=noise_floor(X))
+    np.testing.assert_allclose(trace.cpu().numpy(), ref, rtol=1e-5, atol=max(floor))
 
 
 @pytest.mark.parametrize("n", [1024, 300])
@@ -141,15 +156,22 @@ def test_trace_plan_rejects_unsupported(cuda):
     e = E()
     X = torch.randn(8, 64, device=cuda)
     Y = torch.empty_like(X)
-    # random directed neighbours: not doubly stochastic -> the round loop takes over
-    assert e.trace_max_rounds(e.DeviceCsr(graph_csr(8, 3, seed=0), cuda), X, Y) == 0
+    # random directed neighbours: not doubly stochastic -> the one-image kernel (per-round means)
+    assert e.trace_max_rounds(e.DeviceCsr(graph_csr(8, 3, seed=0), cuda), X, Y) == 24
     big = torch.randn(4100, 64, device=cuda)       # above 4096 agents
     assert e.trace_max_rounds(e.DeviceCsr(rr_csr(4100, 0), cuda), big, torch.empty_like(big)) == 0
-    # above 2048 agents the CSR must be register-cached (regular degree 4, shared weights)
+    # above 2048 agents: register-cached regular graphs keep the double-buffered wide kernel (8
+    # rounds), irregular ones the one-image kernel (4 rounds at 4 agents per thread)
     mid = torch.randn(3000, 64, device=cuda)
     assert e.trace_max_rounds(e.DeviceCsr(metropolis_csr(3000, 1.0 / 3000, 1), cuda), mid,
-                              torch.empty_like(mid)) == 0
+                              torch.empty_like(mid)) == 4
     assert e.trace_max_rounds(e.DeviceCsr(rr_csr(3000, 0), cuda), mid, torch.empty_like(mid)) == 8
+    # an irregular graph whose CSR does not fit LDS beside one image: no traced pass
+    from test_mix_ragged_gpu import dense_irregular
+    dense = dense_irregular(4096, 14, 20, 2)
+    assert dense.nnz - 5 * 4096 > 65535 // 8
+    assert e.trace_max_rounds(e.DeviceCsr(dense, cuda), torch.randn(4096, 64, device=cuda),
+                              torch.empty(4096, 64, device=cuda)) == 0
     W = e.DeviceCsr(rr_csr(8, 0), cuda)
     k = e.trace_max_rounds(W, X, Y)
     with pytest.raises(ValueError, match="rounds must be"):

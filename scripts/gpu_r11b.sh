@@ -6,6 +6,6 @@ export TMPDIR=/tmp
 O=gpurun_out/r11b; mkdir -p $O
 step() { local name=$1 t=$2; shift 2; echo "=== $name"; timeout -k 10 "$t" "$@" > $O/$name.log 2>&1; local rc=$?;
          echo "=== $name rc=$rc"; tail -4 $O/$name.log; if [ $rc -ne 0 ]; then exit $rc; fi; }
-step tests 900 python -u -m pytest tests/test_mix_trace_gpu.py tests/test_mix_ragged_gpu.py tests/test_batched_ann_gpu.py -x -v -m gpu --timeout 300 --timeout-method thread
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 bash scripts/gpu_profile.sh r11b/c4rank --workload c4-rank --steps 20 --warmup 3 || exit $?
 bash scripts/gpu_profile.sh r11b/c4ba --workload c4-ba --steps 20 --warmup 3 --no-cpu || exit $?

@@ -106,3 +106,57 @@ def test_trace_round_caps(n, want):
     k = ctypes.c_int32(0)
     _lib.check(lib.dl_mix_trace_plan(ctypes.byref(args), ctypes.byref(k)), "trace plan")
     assert k.value == want
+
+
+def test_hub_rows_of_a_row_length_order(monkeypatch):
+    """engine.hub_rows (dl_mix_args.n_hub_rows for plan path 5): the leading rows of a
+    descending row-length order whose LDS tails exceed 32 entries -- the Barabasi-Albert hubs --
+    capped at 256; DLAMD_HUB_ROWS overrides it.  The plan reports the register head it is
+    measured against (ABI 8 dl_mix_plan.head / tail_fmt)."""
+    csr = graph.barabasi_albert_metropolis(4096, 2, 1)
+    p = plan(csr)
+    assert p["path"] == 5 and p["head"] == 3 and p["tail_fmt"] == 2
+    order = graph.row_length_order(csr)
+    pc = graph.permuted(csr, order)
+    lens = np.diff(pc.rowptr)
+    assert np.all(np.diff(lens) <= 0)               # descending
+    h = engine.hub_rows(pc, p["head"])
+    assert 0 < h <= 256 and np.all(lens[:h] - 3 > 32) and lens[h] - 3 <= 32
+    assert engine.hub_rows(csr, p["head"]) < h or lens[0] == np.diff(csr.rowptr)[0]
+    monkeypatch.setenv("DLAMD_HUB_ROWS", "0")
+    assert engine.hub_rows(pc, 3) == 0
+    monkeypatch.setenv("DLAMD_HUB_ROWS", "999")
+    assert engine.hub_rows(pc, 3) == 256
+    # a hub-free irregular graph has none
+    monkeypatch.delenv("DLAMD_HUB_ROWS")
+    deg = graph.random_irregular_metropolis(4096, 2, 6, 1)
+    pd = graph.permuted(deg, graph.row_length_order(deg))
+    assert engine.hub_rows(pd, plan(deg)["head"]) == 0
+
+
+def test_traced_plan_takes_any_topology_that_fits():
+    """dl_mix_trace_plan (ABI 8): a row-stochastic W or an irregular graph above 2048 agents
+    runs traced passes on the one-image kernel (24 / 12 / 4 rounds per pass at <= 1024 / 2048 /
+    4096 agents); a CSR too large for LDS beside one image is refused."""
+    lib = _lib.load()
+
+    def trace_rounds(csr, P=256):
+        a = _lib.DlMixArgs()
+        a.x, a.y = 1 << 20, 1 << 36
+        a.ldx = a.ldy = P
+        a.n_params = P
+        W = engine.DeviceCsr(csr, "cpu")   # sizes and flags; the pointers are never read here
+        a.W = _lib.DlCsr(16, 16, 16, W.n_rows, W.nnz, W.uniform_row_nnz, W.doubly_stochastic,
+                         W.shared_row_weights, W.min_row_nnz)
+        k = ctypes.c_int32(0)
+        rc = lib.dl_mix_trace_plan(ctypes.byref(a), ctypes.byref(k))
+        return k.value if rc == 0 else -rc
+    ba = graph.barabasi_albert_metropolis(4096, 2, 1)
+    assert ba.doubly_stochastic and trace_rounds(ba) == 4
+    rs = graph.Csr([0, 2, 4, 6], [0, 1, 1, 2, 0, 2], [0.7, 0.3, 0.4, 0.6, 0.5, 0.5])
+    assert not rs.doubly_stochastic and trace_rounds(rs) == 24
+    rr = graph.from_edge_weights(graph.random_regular_edges(4, 1500, seed=1),
+                                 [0.2] * 3000, list(range(1500)))
+    assert trace_rounds(rr) == 16        # doubly stochastic: the double-buffered wide kernel
+    dense = graph.random_irregular_metropolis(4096, 14, 20, 2)
+    assert trace_rounds(dense) == -_lib.DL_ERR_UNSUPPORTED

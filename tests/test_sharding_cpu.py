@@ -166,6 +166,18 @@ def test_halo_rounds_over_gloo_equal_single_process(tmp_path, chunk, lag, overla
     rows mix, then the boundary rows (same bits).  layout="tiled": X, Y, G column-tiled, each
     peer's halo one tiled block (chunks of whole tiles)."""
     world, P = 2, 24
+    _run_gloo(tmp_path, world, P, chunk, lag, overlap, layout)
+
+
+@pytest.mark.parametrize("overlap", ["chunks", "split"])
+def test_tiled_halo_rounds_four_gloo_ranks(tmp_path, overlap):
+    """Four gloo ranks (2 x 2 torus blocks: every rank has two peers, one of them across the
+    wrap), column-tiled operands and per-peer tiled halo blocks, the lagged deviation: bit-exact
+    with the single-process oracle rounds (the driver's N = 4 agent partition, on the CPU)."""
+    _run_gloo(tmp_path, 4, 32, 16 if overlap == "chunks" else None, True, overlap, "tiled")
+
+
+def _run_gloo(tmp_path, world, P, chunk, lag, overlap, layout):
     mp.spawn(_worker, args=(world, _free_port(), P, chunk, str(tmp_path), lag, overlap, layout),
              nprocs=world, join=True)
     csr = torus_csr(8, 8)

@@ -61,6 +61,8 @@ def parse():
                             "c4-gather", "c4-ba", "c5"])
     p.add_argument("--rank-of", type=int, default=8,
                    help="c4-rank: the GPU count of the partition whose rank 0 is measured alone")
+    p.add_argument("--halo-tile-cols", type=int, default=0,
+                   help="c4-rank: column-tiled width of the rank's operands (0 = the planner's)")
     p.add_argument("--irregular", default="ba2", choices=["ba2", "ba1", "deg"],
                    help="c4-ba: Barabasi-Albert m=2 (the headline), m=1, or a hub-free random "
                         "graph of degree 2..6 (graph.random_irregular_metropolis)")
@@ -839,7 +841,8 @@ def run_c4rank(args, dev, rank, world):
         rp = (sharding.split_halo_plans if overlap == "split" else sharding.halo_plans)(
             csr, parts)[0]
         shard = sharding.HaloShard(rp, P, dev, sharding.ResidentHaloTransport(),
-                                   chunk_cols=chunk, n_agents_total=n, overlap=overlap)
+                                   chunk_cols=chunk, n_agents_total=n, overlap=overlap,
+                                   tile_cols=args.halo_tile_cols or None)
         shard.X.normal_(generator=gen)
         if G is None:   # synthetic gradient rows, shared by every scheme (same shape and layout)
             G = engine.staggered_zeros(shard._shape(rp.n_local), 2, dev).normal_(generator=gen)

@@ -133,6 +133,8 @@ SIGNATURES = {
     "dl_max_column_std": (_i32, [_vp, _i64, _i32, _i64, _vp, _vp]),
     "dl_step_rows": (_i32, [_vp, _i64, _vp, _i64, _f32, _vp, _i32, _i64, _vp, _i64, _vp]),
     "dl_step_rows_tiled": (_i32, [_vp, _i32, _vp, _i32, _f32, _vp, _i32, _i64, _i32, _vp, _vp]),
+    "dl_step_rows_tiled_peers": (_i32, [_vp, _i32, _vp, _i32, _f32, _vp, _i32, _vp, _vp, _i64,
+                                        _i32, _vp]),
     "dl_stream_copy": (_i32, [_vp, _vp, _i64, _i32, _vp]),
     "dl_sgd_step": (_i32, [ctypes.POINTER(DlSgdArgs), _vp]),
     "dl_mlp_grad": (_i32, [ctypes.POINTER(DlMlpArgs), _vp]),

@@ -88,24 +88,37 @@ __global__ void __launch_bounds__(256) step_rows_kernel(const float *__restrict_
     }
 }
 
-// Column-tiled form: thread (i, cc) of the x dimension owns float4 chunk cc of selected row i in
-// every tile t = blockIdx.y, blockIdx.y + gridDim.y, ... (row index and offsets computed once; no
-// division in the loop), four tiles' loads in flight before their stores.  x / g tiles are
-// [x_rows][T] / [g_rows][T] blocks, out tiles [n_sel][T]: each output tile is one contiguous
-// block, the reads are T*4-byte row segments.
+// Column-tiled form, every peer of a halo exchange in one launch: thread (i, cc) of the x
+// dimension owns float4 chunk cc of selected row i (rows of all peers concatenated, peer b's in
+// [row0[b], row0[b+1])) in every tile t = blockIdx.y, blockIdx.y + gridDim.y, ... (peer, row
+// and offsets computed once; no division in the loop), four tiles' loads in flight before
+// their stores.  x / g tiles are [x_rows][T] / [g_rows][T] blocks; peer b's output is its own
+// contiguous block [n_tiles][n_b][T] (one RCCL send buffer).  The reads are T*4-byte row
+// segments.
 __global__ void __launch_bounds__(256) step_rows_tiled_kernel(
     const float4 *__restrict__ x, int x_rows, const float4 *__restrict__ g, int g_rows, float lr,
-    const int32_t *__restrict__ rows, int n_sel, int64_t n_tiles, int tcq,
-    float4 *__restrict__ out) {
+    const int32_t *__restrict__ rows, PackPeers pp, int64_t n_tiles, int tcq) {
     const int q = blockIdx.x * 256 + threadIdx.x;
+    const int n_sel = pp.row0[pp.n];
     if (q >= n_sel * tcq) return;
     const int i = q / tcq, cc = q - (q / tcq) * tcq;
+    // this row's peer: an unrolled select over the <= kMaxPackPeers table (kernel arguments
+    // are not indexed dynamically)
+    float4 *ob = pp.out[0];
+    int r0 = 0, nb = pp.row0[1];
+#pragma unroll
+    for (int b = 1; b < kMaxPackPeers; ++b) {
+        if (b < pp.n && i >= pp.row0[b]) {
+            ob = pp.out[b];
+            r0 = pp.row0[b];
+            nb = pp.row0[b + 1] - pp.row0[b];
+        }
+    }
     const int64_t r = rows[i];
-    const int64_t xs = (int64_t)x_rows * tcq, gs = (int64_t)g_rows * tcq,
-                  os = (int64_t)n_sel * tcq;
+    const int64_t xs = (int64_t)x_rows * tcq, gs = (int64_t)g_rows * tcq, os = (int64_t)nb * tcq;
     const float4 *xp = x + r * tcq + cc;
     const float4 *gp = g ? g + r * tcq + cc : nullptr;
-    float4 *op = out + q;
+    float4 *op = ob + (int64_t)(i - r0) * tcq + cc;
     constexpr int U = 4;
     int64_t t = blockIdx.y;
     const int64_t gy = gridDim.y;
@@ -388,12 +401,12 @@ hipError_t launch_step_rows(const float *x, int64_t ldx, const float *g, int64_t
 }
 
 hipError_t launch_step_rows_tiled(const float *x, int x_rows, const float *g, int g_rows,
-                                  float lr, const int32_t *rows, int n_sel, int64_t n_tiles,
-                                  int tile_cols, float *out, hipStream_t s) {
+                                  float lr, const int32_t *rows, const PackPeers &pp,
+                                  int64_t n_tiles, int tile_cols, hipStream_t s) {
     const int tcq = tile_cols / 4;
-    const int64_t lanes = (int64_t)n_sel * tcq;
+    const int64_t lanes = (int64_t)pp.row0[pp.n] * tcq;
     const int64_t bx = (lanes + 255) / 256;
-    if (bx > 65535) return hipErrorInvalidValue;
+    if (bx > 65535 || pp.n < 1 || pp.n > kMaxPackPeers) return hipErrorInvalidValue;
     // about 2048 resident threads per CU over 256 CUs; each thread walks >= 4 tiles
     int64_t gy = (256 * 2048) / (bx * 256);
     const int64_t gmax = (n_tiles + 3) / 4;
@@ -402,8 +415,7 @@ hipError_t launch_step_rows_tiled(const float *x, int x_rows, const float *g, in
     if (gy < 1) gy = 1;
     hipLaunchKernelGGL(step_rows_tiled_kernel, dim3((unsigned)bx, (unsigned)gy), dim3(256), 0, s,
                        reinterpret_cast<const float4 *>(x), x_rows,
-                       reinterpret_cast<const float4 *>(g), g_rows, lr, rows, n_sel, n_tiles, tcq,
-                       reinterpret_cast<float4 *>(out));
+                       reinterpret_cast<const float4 *>(g), g_rows, lr, rows, pp, n_tiles, tcq);
     return hipGetLastError();
 }
 

@@ -267,12 +267,13 @@ int plan_mix(const dl_mix_args *a, Plan *pl) {
                                         "(%d rows); query dl_mix_plan_query on row-major args",
                         a->tile_cols, R);
         const int64_t n_tiles = (a->n_params + a->tile_cols - 1) / a->tile_cols;
-        // two 1024-thread workgroups per CU when LDS allows, except at C = 4, where the second
-        // workgroup's LDS traffic (4 rows of 64 B per 16 lanes: the most bank conflicts of any
-        // C) costs more than its extra loads in flight (measured 5.5 vs 5.8 TB/s at N = 1024)
+        // two 1024-thread workgroups per CU when LDS allows, except for C = 4 tiles of 64 KiB
+        // (c2's 1024 agents), where the second workgroup's LDS traffic (4 rows of 64 B per 16
+        // lanes: the most bank conflicts of any C) costs more than its extra loads in flight
+        // (measured 5.5 vs 5.8 TB/s at N = 1024)
         int bpc = (int)(dl::kLdsBytes / lds);
         if (bpc > wg_per_cu_cap()) bpc = wg_per_cu_cap();
-        if (c == 4) bpc = 1;
+        if (c == 4 && tile >= 65536) bpc = 1;
         const int64_t grid =
             balanced_grid(n_tiles, (int64_t)device_cus() * (bpc < 1 ? 1 : bpc) * grid_mult());
         pl->pub.path = 1;
@@ -625,6 +626,7 @@ struct TracePlan {
     int32_t irr;   // 1: mix_trace_irr_kernel (one image, register head + LDS tail)
     int32_t head;  // irr: CSR entries per row in registers
     int32_t gm;    // irr: W not doubly stochastic, every round's mean from its outputs
+    int32_t narrow;  // irr: 2-column steps, 6-byte tail entries
 };
 
 // mix_trace_irr_kernel's configuration: one [N] float4 image, each row's first `head` entries in
@@ -642,20 +644,32 @@ int plan_trace_irr(const dl_mix_args *a, TracePlan *tp) {
         head = 0;
         ntail = W.nnz;
     }
-    const uint32_t img = (uint32_t)N * 16u;
-    const uint32_t tail = (uint32_t)align_up((size_t)ntail * 8);
-    if (ntail > 65535 || 2 * ntail > (int64_t)img || img + tail + 256u > (uint32_t)dl::kLdsBytes)
-        return fail(DL_ERR_UNSUPPORTED, "dl_mix_rounds_trace: the CSR of %d agents (%d entries) "
-                                        "does not fit LDS beside one image", N, W.nnz);
+    if (ntail > 65535)
+        return fail(DL_ERR_UNSUPPORTED, "dl_mix_rounds_trace: %lld CSR entries past the register "
+                                        "heads (> 65535)", (long long)ntail);
+    // 4-column steps with 8-byte {weight, row} tail pairs (the tail's row map in the image), or
+    // 2-column steps with 6-byte tail entries when that does not fit
+    bool narrow = false;
+    uint32_t img = (uint32_t)N * 16u;
+    uint32_t tail = (uint32_t)align_up((size_t)ntail * 8);
+    if (2 * ntail > (int64_t)img || img + tail + 256u > (uint32_t)dl::kLdsBytes) {
+        narrow = true;
+        img = (uint32_t)align_up((size_t)N * 8u);
+        tail = (uint32_t)align_up((size_t)ntail * 6);
+        if (img + tail + 256u > (uint32_t)dl::kLdsBytes)
+            return fail(DL_ERR_UNSUPPORTED, "dl_mix_rounds_trace: the CSR of %d agents (%d "
+                                            "entries) does not fit LDS beside one image", N, W.nnz);
+    }
     tp->irr = 1;
     tp->head = head;
     tp->gm = W.doubly_stochastic ? 0 : 1;
+    tp->narrow = narrow ? 1 : 0;
     tp->chunks = 1;
     tp->csr_off = img;
     tp->scratch_off = img + tail;
     tp->lds = img + tail + 256u;
     tp->max_rounds = dl::irr_trace_rounds(dl::irr_trace_kv(N));
-    tp->n_steps = a->n_params / 4;
+    tp->n_steps = a->n_params / (narrow ? 2 : 4);
     tp->grid = (int32_t)balanced_grid(tp->n_steps, device_cus());
     return DL_OK;
 }
@@ -784,7 +798,8 @@ int dl_mix_rounds_trace(const dl_mix_args *args, int32_t rounds, float *trace, v
         return fail(DL_ERR_WORKSPACE, "dl_mix_rounds_trace: needs a 16-byte aligned workspace "
                                       "of %zu bytes (dl_mix_trace_workspace_bytes)", need);
     t.dev_partial = reinterpret_cast<float *>(ws);
-    hipError_t e = tp.irr ? dl::launch_mix_trace_irr(t, tp.head, tp.gm != 0, rounds, tp.grid,
+    hipError_t e = tp.irr ? dl::launch_mix_trace_irr(t, tp.head, tp.gm != 0, tp.narrow != 0,
+                                                      rounds, tp.grid,
                                                       (int)tp.lds, trace,
                                                       static_cast<hipStream_t>(stream))
                           : dl::launch_mix_trace(t, tp.chunks, rounds, tp.grid, (int)tp.lds, trace,
@@ -1347,25 +1362,62 @@ int dl_step_rows(const float *x, int64_t ldx, const float *g, int64_t ldg, float
     return e == hipSuccess ? DL_OK : hip_fail(e, "step_rows launch");
 }
 
+namespace {
+int step_rows_tiled_peers(const float *x, int32_t x_rows, const float *g, int32_t g_rows, float lr,
+                          const int32_t *rows, int32_t n_peers, const int32_t *row0,
+                          float *const *outs, int64_t n_params, int32_t tile_cols,
+                          dl_stream_t stream, const char *who) {
+    if (!x || !rows || !row0 || !outs || n_peers < 1 || n_peers > dl::kMaxPackPeers ||
+        n_params <= 0 || x_rows <= 0 || (g && g_rows <= 0) || tile_cols < 4 ||
+        tile_cols > 4 * dl::kMaxChunks || (tile_cols & (tile_cols - 1)))
+        return fail(DL_ERR_INVALID, "%s: bad arguments", who);
+    if (!aligned16(x) || (g && !aligned16(g)))
+        return fail(DL_ERR_INVALID, "%s: operands must be 16-byte aligned", who);
+    const int64_t n_tiles = (n_params + tile_cols - 1) / tile_cols;
+    dl::PackPeers pp{};
+    pp.n = n_peers;
+    if (row0[0] != 0) return fail(DL_ERR_INVALID, "%s: row0[0] must be 0", who);
+    for (int b = 0; b < n_peers; ++b) {
+        const int32_t nb = row0[b + 1] - row0[b];
+        if (nb < 0 || row0[b + 1] > 65535)
+            return fail(DL_ERR_INVALID, "%s: row0 must be non-decreasing, <= 65535", who);
+        if (nb > 0 && (!outs[b] || !aligned16(outs[b])))
+            return fail(DL_ERR_INVALID, "%s: out[%d] must be a 16-byte aligned pointer", who, b);
+        const size_t ob = (size_t)n_tiles * nb * tile_cols * 4;
+        if (nb > 0 && (overlaps(outs[b], ob, x, (size_t)n_tiles * x_rows * tile_cols * 4) ||
+                       (g && overlaps(outs[b], ob, g, (size_t)n_tiles * g_rows * tile_cols * 4))))
+            return fail(DL_ERR_INVALID, "%s: out[%d] overlaps x or g", who, b);
+        pp.row0[b] = row0[b];
+        pp.out[b] = reinterpret_cast<float4 *>(outs[b]);
+    }
+    pp.row0[n_peers] = row0[n_peers];
+    if (row0[n_peers] == 0) return DL_OK;
+    hipError_t e = dl::launch_step_rows_tiled(x, x_rows, g, g_rows, lr, rows, pp, n_tiles,
+                                              tile_cols, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? DL_OK : hip_fail(e, "step_rows_tiled launch");
+}
+}  // namespace
+
 int dl_step_rows_tiled(const float *x, int32_t x_rows, const float *g, int32_t g_rows, float lr,
                        const int32_t *rows, int32_t n_sel, int64_t n_params, int32_t tile_cols,
                        float *out, dl_stream_t stream) {
     g_err.clear();
     if (n_sel == 0) return DL_OK;
-    if (!x || !rows || !out || n_sel < 0 || n_sel > 65535 || n_params <= 0 || x_rows <= 0 ||
-        (g && g_rows <= 0) || tile_cols < 4 || tile_cols > 4 * dl::kMaxChunks ||
-        (tile_cols & (tile_cols - 1)))
+    if (n_sel < 0 || n_sel > 65535 || !out)
         return fail(DL_ERR_INVALID, "dl_step_rows_tiled: bad arguments");
-    if (!aligned16(x) || !aligned16(out) || (g && !aligned16(g)))
-        return fail(DL_ERR_INVALID, "dl_step_rows_tiled: operands must be 16-byte aligned");
-    const int64_t n_tiles = (n_params + tile_cols - 1) / tile_cols;
-    const size_t ob = (size_t)n_tiles * n_sel * tile_cols * 4;
-    if (overlaps(out, ob, x, (size_t)n_tiles * x_rows * tile_cols * 4) ||
-        (g && overlaps(out, ob, g, (size_t)n_tiles * g_rows * tile_cols * 4)))
-        return fail(DL_ERR_INVALID, "dl_step_rows_tiled: out overlaps x or g");
-    hipError_t e = dl::launch_step_rows_tiled(x, x_rows, g, g_rows, lr, rows, n_sel, n_tiles,
-                                              tile_cols, out, static_cast<hipStream_t>(stream));
-    return e == hipSuccess ? DL_OK : hip_fail(e, "step_rows_tiled launch");
+    const int32_t row0[2] = {0, n_sel};
+    float *outs[1] = {out};
+    return step_rows_tiled_peers(x, x_rows, g, g_rows, lr, rows, 1, row0, outs, n_params,
+                                 tile_cols, stream, "dl_step_rows_tiled");
+}
+
+int dl_step_rows_tiled_peers(const float *x, int32_t x_rows, const float *g, int32_t g_rows,
+                             float lr, const int32_t *rows, int32_t n_peers, const int32_t *row0,
+                             float *const *outs, int64_t n_params, int32_t tile_cols,
+                             dl_stream_t stream) {
+    g_err.clear();
+    return step_rows_tiled_peers(x, x_rows, g, g_rows, lr, rows, n_peers, row0, outs, n_params,
+                                 tile_cols, stream, "dl_step_rows_tiled_peers");
 }
 
 int dl_sgd_step(const dl_sgd_args *a, dl_stream_t stream) {

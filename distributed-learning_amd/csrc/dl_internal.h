@@ -140,8 +140,9 @@ constexpr int irr_trace_kv(int n_rows) {
     return n_rows <= kTileThreads ? 1 : n_rows <= 2 * kTileThreads ? 2 : 4;
 }
 constexpr int irr_trace_rounds(int kv) { return kv == 1 ? 24 : kv == 2 ? 12 : 4; }
-hipError_t launch_mix_trace_irr(const TileArgs &a, int head, bool general_mean, int rounds,
-                                int grid, int lds, float *trace_out, hipStream_t s);
+// narrow: 2-column steps (8-byte image entries) and a 6-byte LDS tail, for larger CSRs
+hipError_t launch_mix_trace_irr(const TileArgs &a, int head, bool general_mean, bool narrow,
+                                int rounds, int grid, int lds, float *trace_out, hipStream_t s);
 // max_zeroed: an earlier launch on the stream already zeroed dev_max (TileArgs::dev_max_zero)
 hipError_t launch_dev_reduce(const float *partial, int nparts, int n_rows, float *dev_sq,
                              float *dev_max, hipStream_t s, bool max_zeroed = false);
@@ -159,9 +160,16 @@ hipError_t launch_max_column_std(const float *x, int64_t ldx, int n_rows, int64_
 hipError_t launch_step_rows(const float *x, int64_t ldx, const float *g, int64_t ldg, float lr,
                             const int32_t *rows, int n_sel, int64_t n_params, float *out,
                             int64_t ldo, hipStream_t s);
+// a halo pack's peers: peer b's rows are rows[row0[b], row0[b+1]), its tiled block goes to out[b]
+constexpr int kMaxPackPeers = 16;
+struct PackPeers {
+    int32_t n;
+    int32_t row0[kMaxPackPeers + 1];
+    float4 *out[kMaxPackPeers];
+};
 hipError_t launch_step_rows_tiled(const float *x, int x_rows, const float *g, int g_rows,
-                                  float lr, const int32_t *rows, int n_sel, int64_t n_tiles,
-                                  int tile_cols, float *out, hipStream_t s);
+                                  float lr, const int32_t *rows, const PackPeers &pp,
+                                  int64_t n_tiles, int tile_cols, hipStream_t s);
 hipError_t launch_sgd_step(const float *x, int64_t ldx, const float *g, int64_t ldg, float *buf,
                            int64_t ldb, float *out, int64_t ldo, int n_rows, int64_t n_params,
                            float lr, float mu, float damp, float wd, int first, int nesterov,

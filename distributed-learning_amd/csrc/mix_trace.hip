@@ -19,6 +19,7 @@
 #include "dl_internal.h"
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace dl {
 namespace {
@@ -548,26 +549,32 @@ __global__ void __launch_bounds__(kTileThreads) mix_trace_wide_kernel(TileArgs a
 
 // Traced passes for the graphs the double-buffered kernels above cannot hold: irregular graphs
 // of more than 2048 agents (Barabasi-Albert hubs, per-entry weights), and any W that is not
-// doubly stochastic (GM).  One LDS image [N] float4 (one 4-column chunk per step) and the CSR as
-// in plan path 5: each row's first RD entries in registers, the rest as 8-byte {weight, row}
-// pairs behind the image.  With one image a round folds every output into registers, waits for
-// all reads of the image, then writes it back (two barriers a round instead of one ping-pong
-// barrier).  GM: mean(W x) != mean(x), so every round's column mean is reduced from its outputs
-// (wave shuffles + a 16-entry scratch) before the deviations of that round -- what
-// Mixer._get_deviation_dict computes after every round (mixer.py:51-66).  The fold is the
-// reference's left fold in CSR order (head, then tail) as in the other kernels: bit-identical.
-// KV agents per thread (rows tid + k * 1024), KR rounds per pass (their deviations in VGPRs).
-template <int KV, int KR, int RD, bool GM>
+// doubly stochastic (GM).  One LDS image [N] of one column chunk per step and the CSR as in plan
+// path 5: each row's first RD entries in registers, the rest behind the image.  With one image
+// a round folds every output into registers, waits for all reads of the image, then writes it
+// back (two barriers a round instead of one ping-pong barrier).  GM: mean(W x) != mean(x), so
+// every round's column mean is reduced from its outputs (wave shuffles + a 16-entry scratch)
+// before the deviations of that round -- what Mixer._get_deviation_dict computes after every
+// round (mixer.py:51-66).  The fold is the reference's left fold in CSR order (head, then tail)
+// as in the other kernels: bit-identical.  KV agents per thread (rows tid + k * 1024), KR rounds
+// per pass (their deviations in VGPRs).
+// NW (narrow): 2-column chunks (8-byte image entries) and a 6-byte tail (fp32 weights, then u16
+// rows) for CSRs that do not fit LDS beside a 16-byte image with 8-byte pairs (a row-stochastic
+// graph of 4096 agents and 41k entries: 32 KiB image + 123 KiB tail).
+template <int KV, int KR, int RD, bool GM, bool NW>
 __global__ void __launch_bounds__(kTileThreads) mix_trace_irr_kernel(TileArgs a, int rounds) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int NT = kTileThreads;
+    typedef typename std::conditional<NW, f32x2, f32x4>::type vec;
     const int tid = threadIdx.x;
     const int N = a.n_rows;
     const int nnz = a.nnz;
-    float4 *img = reinterpret_cast<float4 *>(smem);
+    vec *img = reinterpret_cast<vec *>(smem);
     float4 *scratch = reinterpret_cast<float4 *>(smem + a.scratch_off);   // [16]
-    uint2 *ltp = reinterpret_cast<uint2 *>(smem + a.csr_off);
     const int ntail = nnz - RD * N;
+    uint2 *ltp = reinterpret_cast<uint2 *>(smem + a.csr_off);                        // !NW
+    float *ltw = reinterpret_cast<float *>(smem + a.csr_off);                        // NW
+    uint16_t *ltc = reinterpret_cast<uint16_t *>(smem + a.csr_off + 4u * (uint32_t)ntail);
     constexpr int NRC = RD > 0 ? KV * RD : 1;
     float rw[NRC];
     uint32_t ri[(NRC + 1) / 2];
@@ -591,48 +598,96 @@ __global__ void __launch_bounds__(kTileThreads) mix_trace_irr_kernel(TileArgs a,
         const int ln = min(max(e1 - e0 - RD, 0), ntail - st);
         rdesc[k] = r < N ? (uint32_t)st | ((uint32_t)ln << 16) : 0u;
     }
-    {   // stage the tail: a row id per tail slot (u16, in the image area), then the pairs
-        uint16_t *trow = reinterpret_cast<uint16_t *>(smem);
+    {   // stage the tail: a row id per tail slot (u16), then the entries
+        // (!NW: the map in the image area; NW: in the upper half of the weights array, so
+        // batches of reads, a barrier, then writes: weight t lands on map slot 2t - ntail < t,
+        // already read)
+        uint16_t *trow = NW ? reinterpret_cast<uint16_t *>(smem + a.csr_off + 2u * (uint32_t)ntail)
+                            : reinterpret_cast<uint16_t *>(smem);
 #pragma unroll
         for (int k = 0; k < KV; ++k) {
             const uint32_t t0 = rdesc[k] & 0xffffu, tn = rdesc[k] >> 16;
             for (uint32_t t = 0; t < tn; ++t) trow[t0 + t] = (uint16_t)(tid + k * NT);
         }
         __syncthreads();
-        for (int t = tid; t < ntail; t += NT) {
-            const int e = min(t + RD * (trow[t] + 1), nnz - 1);
-            ltp[t] = make_uint2(__float_as_uint(a.w[e]), (uint32_t)a.col[e]);
+        if constexpr (NW) {
+            for (int base = 0; base < ntail; base += 4 * NT) {
+                int rid[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int t = base + u * NT + tid;
+                    rid[u] = t < ntail ? trow[t] : 0;
+                }
+                __syncthreads();
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int t = base + u * NT + tid;
+                    if (t < ntail) {
+                        const int e = min(t + RD * (rid[u] + 1), nnz - 1);
+                        ltw[t] = a.w[e];
+                        ltc[t] = (uint16_t)a.col[e];
+                    }
+                }
+                __syncthreads();
+            }
+        } else {
+            for (int t = tid; t < ntail; t += NT) {
+                const int e = min(t + RD * (trow[t] + 1), nnz - 1);
+                ltp[t] = make_uint2(__float_as_uint(a.w[e]), (uint32_t)a.col[e]);
+            }
+            __syncthreads();
         }
-        __syncthreads();
     }
-    // agent tid + k * 1024's output from the image: register head, then the LDS tail, four
+    // (lo, hi) += w * v: the pair fold of the 16-byte image; lo += w * v on the 8-byte one
+    auto fold1 = [&](f32x2 &lo, f32x2 &hi, float w, const vec &v) {
+        if constexpr (NW) {
+            const f32x2 w2 = {w, w};
+            lo = lo + w2 * v;
+        } else {
+            fold2(lo, hi, w, v);
+        }
+    };
+    auto entry = [&](uint32_t i, float &w, uint32_t &ci) {
+        if constexpr (NW) {
+            w = ltw[i];
+            ci = ltc[i];
+        } else {
+            const uint2 pr = ltp[i];
+            w = __uint_as_float(pr.x);
+            ci = pr.y;
+        }
+    };
+    // agent tid + k * 1024's output from the image: register head, then the LDS tail, TU
     // entries' reads issued per step
-    auto fold = [&](int k) {
-        f32x2 lo = {0.f, 0.f}, hi = {0.f, 0.f};
+    auto fold = [&](int k, f32x2 &lo, f32x2 &hi) {
+        lo = f32x2{0.f, 0.f};
+        hi = f32x2{0.f, 0.f};
 #pragma unroll
         for (int e = 0; e < (RD > 0 ? RD : 0); ++e) {
             const int j = k * RD + e;
             const uint32_t idx = (ri[j >> 1] >> (16 * (j & 1))) & 0xffffu;
-            fold2(lo, hi, rw[j], *reinterpret_cast<const f32x4 *>(img + idx));
+            fold1(lo, hi, rw[j], img[idx]);
         }
         uint32_t t = rdesc[k] & 0xffffu;
         const uint32_t t1 = t + (rdesc[k] >> 16);
-        constexpr int TU = KV >= 4 ? 2 : 4;   // (4 agents' outputs and prefetch: fewer in flight)
+        constexpr int TU = KV >= 4 ? 1 : 4;   // (4 agents' outputs: fewer in flight)
         for (; t + TU <= t1; t += TU) {
-            uint2 p4[TU];
-            f32x4 v4[TU];
+            float w4[TU];
+            uint32_t c4[TU];
+            vec v4[TU];
 #pragma unroll
-            for (int u = 0; u < TU; ++u) p4[u] = ltp[t + u];
+            for (int u = 0; u < TU; ++u) entry(t + u, w4[u], c4[u]);
 #pragma unroll
-            for (int u = 0; u < TU; ++u) v4[u] = *reinterpret_cast<const f32x4 *>(img + p4[u].y);
+            for (int u = 0; u < TU; ++u) v4[u] = img[c4[u]];
 #pragma unroll
-            for (int u = 0; u < TU; ++u) fold2(lo, hi, __uint_as_float(p4[u].x), v4[u]);
+            for (int u = 0; u < TU; ++u) fold1(lo, hi, w4[u], v4[u]);
         }
         for (; t < t1; ++t) {
-            const uint2 pr = ltp[t];
-            fold2(lo, hi, __uint_as_float(pr.x), *reinterpret_cast<const f32x4 *>(img + pr.y));
+            float w;
+            uint32_t ci;
+            entry(t, w, ci);
+            fold1(lo, hi, w, img[ci]);
         }
-        return make_float4(lo.x, lo.y, hi.x, hi.y);
     };
     // column mean of this step's chunk over every agent: per-thread sums -> wave -> scratch
     auto reduce_mean = [&](float4 cs) {
@@ -640,8 +695,10 @@ __global__ void __launch_bounds__(kTileThreads) mix_trace_irr_kernel(TileArgs a,
         for (int m = 1; m < 64; m <<= 1) {
             cs.x += __shfl_xor(cs.x, m);
             cs.y += __shfl_xor(cs.y, m);
-            cs.z += __shfl_xor(cs.z, m);
-            cs.w += __shfl_xor(cs.w, m);
+            if (!NW) {
+                cs.z += __shfl_xor(cs.z, m);
+                cs.w += __shfl_xor(cs.w, m);
+            }
         }
         if ((tid & 63) == 0) scratch[tid >> 6] = cs;
     };
@@ -660,8 +717,10 @@ __global__ void __launch_bounds__(kTileThreads) mix_trace_irr_kernel(TileArgs a,
     };
     const int lsh = __builtin_ctz((unsigned)a.lchunks);
     const int64_t lmask = (int64_t)a.lchunks - 1;
+    // byte offset of (agent row, step q): 16-byte chunks, or (NW) 8-byte halves of them
     auto off = [&](int64_t ts, int64_t row, int64_t q) {
-        return (q >> lsh) * ts + row + (q & lmask) * 16;
+        const int64_t c4 = NW ? q >> 1 : q;
+        return (c4 >> lsh) * ts + row + (c4 & lmask) * 16 + (NW ? (q & 1) * 8 : 0);
     };
     const char *xb = reinterpret_cast<const char *>(a.x);
     char *yb = reinterpret_cast<char *>(a.y);
@@ -671,27 +730,39 @@ __global__ void __launch_bounds__(kTileThreads) mix_trace_irr_kernel(TileArgs a,
     for (int k = 0; k < KV; ++k)
 #pragma unroll
         for (int r = 0; r < KR; ++r) dacc[k][r] = 0.f;
-    float4 px[KV];
+    vec px[KV];
+    // (lane ids laundered per step: hoisted out of the step loop, the KV agents' 64-bit load and
+    // store addresses took 16 VGPRs and spilled)
+    int ltid = tid;
     auto prefetch = [&](int64_t q) {
 #pragma unroll
         for (int k = 0; k < KV; ++k) {
-            const int ag = tid + k * NT < N ? tid + k * NT : 0;   // ragged: row 0 (L1 hit)
-            px[k] = tr_load4(xb + off(a.xts, (int64_t)ag * a.xrs, q));
+            const int ag = ltid + k * NT < N ? ltid + k * NT : 0;   // ragged: row 0 (L1 hit)
+            px[k] = __builtin_nontemporal_load(
+                reinterpret_cast<const vec *>(xb + off(a.xts, (int64_t)ag * a.xrs, q)));
         }
+    };
+    auto comps = [](const vec &v) {   // as float4 (NW: z = w = 0)
+        if constexpr (NW)
+            return make_float4(v.x, v.y, 0.f, 0.f);
+        else
+            return make_float4(v.x, v.y, v.z, v.w);
     };
     int64_t q = blockIdx.x;
     if (q < nsteps) prefetch(q);
     for (; q < nsteps; q += gridDim.x) {
+        asm volatile("" : "+v"(ltid));
         float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
         for (int k = 0; k < KV; ++k) {
             const int ag = tid + k * NT;
             if (ag < N) {
                 img[ag] = px[k];
-                cs.x += px[k].x;
-                cs.y += px[k].y;
-                cs.z += px[k].z;
-                cs.w += px[k].w;
+                const float4 v = comps(px[k]);
+                cs.x += v.x;
+                cs.y += v.y;
+                cs.z += v.z;
+                cs.w += v.w;
             }
         }
         if (!GM) reduce_mean(cs);   // mean(W^r x) = mean(x): one mean per step
@@ -701,14 +772,16 @@ __global__ void __launch_bounds__(kTileThreads) mix_trace_irr_kernel(TileArgs a,
         // prefetch registers beside 4 agents' head CSR and outputs spill)
         constexpr bool PF = KV < 4;
         if (PF && q + gridDim.x < nsteps) prefetch(q + gridDim.x);
-#pragma unroll
-        for (int r = 0; r < KR; ++r) {
-            if (r < rounds) {
+        // (the round loop stays rolled: unrolled, four agents' folds of every round were
+        // interleaved and spilled; a round's deviations go to their slot by predicated adds)
+#pragma unroll 1
+        for (int r = 0; r < rounds; ++r) {
+            {
                 const bool last = r + 1 == rounds;
-                float4 y[KV];
+                f32x2 ylo[KV], yhi[KV];
 #pragma unroll
                 for (int k = 0; k < KV; ++k) {
-                    if (tid + k * NT < N) y[k] = fold(k);
+                    if (tid + k * NT < N) fold(k, ylo[k], yhi[k]);
                     __builtin_amdgcn_sched_barrier(0);
                 }
                 __syncthreads();   // every read of the image is done
@@ -717,14 +790,20 @@ __global__ void __launch_bounds__(kTileThreads) mix_trace_irr_kernel(TileArgs a,
                 for (int k = 0; k < KV; ++k) {
                     const int ag = tid + k * NT;
                     if (ag < N) {
-                        if (!last)
-                            img[ag] = y[k];
+                        vec y;
+                        if constexpr (NW)
+                            y = ylo[k];
                         else
-                            tr_store4(y[k], yb + off(a.yts, (int64_t)ag * a.yrs, q));
-                        ys.x += y[k].x;
-                        ys.y += y[k].y;
-                        ys.z += y[k].z;
-                        ys.w += y[k].w;
+                            y = f32x4{ylo[k].x, ylo[k].y, yhi[k].x, yhi[k].y};
+                        if (!last)
+                            img[ag] = y;
+                        else
+                            *reinterpret_cast<vec *>(
+                                yb + off(a.yts, (int64_t)(ltid + k * NT) * a.yrs, q)) = y;
+                        ys.x += ylo[k].x;
+                        ys.y += ylo[k].y;
+                        ys.z += NW ? 0.f : yhi[k].x;
+                        ys.w += NW ? 0.f : yhi[k].y;
                     }
                 }
                 if (GM) {   // this round's column mean, from its outputs
@@ -736,9 +815,19 @@ __global__ void __launch_bounds__(kTileThreads) mix_trace_irr_kernel(TileArgs a,
                 }
                 const f32x2 mlo = {mean.x, mean.y}, mhi = {mean.z, mean.w};
 #pragma unroll
-                for (int k = 0; k < KV; ++k)
-                    if (tid + k * NT < N)
-                        dacc[k][r] += dev2(f32x2{y[k].x, y[k].y}, f32x2{y[k].z, y[k].w}, mlo, mhi);
+                for (int k = 0; k < KV; ++k) {
+                    float d = 0.f;
+                    if (tid + k * NT < N) {
+                        if constexpr (NW) {
+                            const f32x2 dd = ylo[k] - mlo, q2 = dd * dd;
+                            d = q2.x + q2.y;
+                        } else {
+                            d = dev2(ylo[k], yhi[k], mlo, mhi);
+                        }
+                    }
+#pragma unroll
+                    for (int j = 0; j < KR; ++j) dacc[k][j] += j == r ? d : 0.f;
+                }
             }
         }
         // (GM) the last round's scratch reads finish before the next step writes scratch: that
@@ -844,9 +933,11 @@ hipError_t launch_wide(const TileArgs &a, int rounds, int grid, int lds, hipStre
 }
 
 template <int KV, int RD, bool GM>
-hipError_t launch_irr3(const TileArgs &a, int rounds, int grid, int lds, hipStream_t s) {
+hipError_t launch_irr3(const TileArgs &a, bool narrow, int rounds, int grid, int lds,
+                       hipStream_t s) {
     constexpr int KR = irr_trace_rounds(KV);
-    auto k = mix_trace_irr_kernel<KV, KR, RD, GM>;
+    auto k = narrow ? mix_trace_irr_kernel<KV, KR, RD, GM, true>
+                    : mix_trace_irr_kernel<KV, KR, RD, GM, false>;
     hipError_t e = allow_full_lds(reinterpret_cast<const void *>(k));
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k, dim3(grid), dim3(kTileThreads), lds, s, a, rounds);
@@ -854,34 +945,36 @@ hipError_t launch_irr3(const TileArgs &a, int rounds, int grid, int lds, hipStre
 }
 
 template <int KV, bool GM>
-hipError_t launch_irr2(const TileArgs &a, int head, int rounds, int grid, int lds,
+hipError_t launch_irr2(const TileArgs &a, int head, bool narrow, int rounds, int grid, int lds,
                        hipStream_t s) {
     switch (head) {
-        case 0: return launch_irr3<KV, 0, GM>(a, rounds, grid, lds, s);
-        case 2: return launch_irr3<KV, 2, GM>(a, rounds, grid, lds, s);
-        case 3: return launch_irr3<KV, 3, GM>(a, rounds, grid, lds, s);
-        case 5: return launch_irr3<KV, 5, GM>(a, rounds, grid, lds, s);
+        case 0: return launch_irr3<KV, 0, GM>(a, narrow, rounds, grid, lds, s);
+        case 2: return launch_irr3<KV, 2, GM>(a, narrow, rounds, grid, lds, s);
+        case 3: return launch_irr3<KV, 3, GM>(a, narrow, rounds, grid, lds, s);
+        case 5: return launch_irr3<KV, 5, GM>(a, narrow, rounds, grid, lds, s);
         default: return hipErrorInvalidValue;
     }
 }
 
 template <bool GM>
-hipError_t launch_irr1(const TileArgs &a, int head, int rounds, int grid, int lds,
+hipError_t launch_irr1(const TileArgs &a, int head, bool narrow, int rounds, int grid, int lds,
                        hipStream_t s) {
-    if (a.n_rows <= kTileThreads) return launch_irr2<1, GM>(a, head, rounds, grid, lds, s);
-    if (a.n_rows <= 2 * kTileThreads) return launch_irr2<2, GM>(a, head, rounds, grid, lds, s);
-    return launch_irr2<4, GM>(a, head, rounds, grid, lds, s);
+    if (a.n_rows <= kTileThreads)
+        return launch_irr2<1, GM>(a, head, narrow, rounds, grid, lds, s);
+    if (a.n_rows <= 2 * kTileThreads)
+        return launch_irr2<2, GM>(a, head, narrow, rounds, grid, lds, s);
+    return launch_irr2<4, GM>(a, head, narrow, rounds, grid, lds, s);
 }
 
 }  // namespace
 
-hipError_t launch_mix_trace_irr(const TileArgs &a, int head, bool general_mean, int rounds,
-                                int grid, int lds, float *trace_out, hipStream_t s) {
+hipError_t launch_mix_trace_irr(const TileArgs &a, int head, bool general_mean, bool narrow,
+                                int rounds, int grid, int lds, float *trace_out, hipStream_t s) {
     if (rounds < 1 || rounds > irr_trace_rounds(irr_trace_kv(a.n_rows)) || a.n_rows < 2 ||
         a.n_rows > 4 * kTileThreads || a.lchunks < 1)
         return hipErrorInvalidValue;
-    hipError_t e = general_mean ? launch_irr1<true>(a, head, rounds, grid, lds, s)
-                                : launch_irr1<false>(a, head, rounds, grid, lds, s);
+    hipError_t e = general_mean ? launch_irr1<true>(a, head, narrow, rounds, grid, lds, s)
+                                : launch_irr1<false>(a, head, narrow, rounds, grid, lds, s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(trace_reduce_kernel, dim3(rounds), dim3(1024), 0, s, a.dev_partial, grid,
                        rounds, a.n_rows, trace_out);

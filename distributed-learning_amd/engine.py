@@ -408,6 +408,31 @@ def step_rows(X, rows, out, G=None, lr=0.0):
     return out
 
 
+def step_rows_tiled_peers(X, rows, row0, outs, G=None, lr=0.0):
+    """dl_step_rows_tiled_peers: every peer's halo block in one launch -- peer b's rows are
+    rows[row0[b]:row0[b+1]] (one int32 device tensor, peers concatenated), its block
+    outs[b] = [tiles, n_b, T] (contiguous)."""
+    lib = _lib.load()
+    tiles, _, T = X.shape
+    if rows.dtype != torch.int32 or rows.device != X.device:
+        raise ValueError("rows must be a device int32 tensor (every entry < X.shape[1]: checked "
+                         "once by the caller, a bad row faults the GPU)")
+    n = len(outs)
+    if len(row0) != n + 1 or row0[0] != 0 or row0[-1] != rows.numel():
+        raise ValueError("row0 must be [0, ..., rows.numel()] with one entry per peer + 1")
+    xl = _tiled_ld(X, "X", X.shape[1], tiles * T, T, X.device)
+    gl = _tiled_ld(G, "G", G.shape[1], tiles * T, T, X.device) if G is not None else 0
+    for b, o in enumerate(outs):
+        _check_tiled(o, f"outs[{b}]", (tiles, row0[b + 1] - row0[b], T), X.device)
+    r0 = (ctypes.c_int32 * (n + 1))(*row0)
+    op = (ctypes.c_void_p * n)(*[o.data_ptr() for o in outs])
+    _lib.check(lib.dl_step_rows_tiled_peers(_lib.ptr(X), xl, _lib.ptr(G), gl, float(lr),
+                                            _lib.ptr(rows), n, r0, op, tiles * T, T,
+                                            _lib.stream_handle(X.device)),
+               "dl_step_rows_tiled_peers")
+    return outs
+
+
 def step_rows_tiled(X, rows, out, G=None, lr=0.0):
     """Column-tiled dl_step_rows_tiled: out[t, i] = X[t, rows[i]] - lr * G[t, rows[i]] for every
     tile t -- one peer's halo block [tiles, n_sel, T] (X, G: [tiles, rows, T] or tile views)."""

@@ -441,6 +441,10 @@ class HipOps:
             return self.E.step_rows_tiled(X, rows, out, G=G, lr=lr)
         return self.E.step_rows(X, rows, out, G=G, lr=lr)
 
+    def step_rows_peers(self, X, rows, row0, outs, G=None, lr=0.0):
+        """Every peer's column-tiled halo block in one launch (dl_step_rows_tiled_peers)."""
+        return self.E.step_rows_tiled_peers(X, rows, row0, outs, G=G, lr=lr)
+
     def mix(self, W, X, Y, G=None, lr=0.0, halo=None, lag=None, halo_blocks=None):
         """lag = (mean_prev, colsum_out, dev_sq): the lagged deviation of a halo round.
         Column-tiled operands are 3-D [tiles, rows, T] (views), the halo then a flat buffer of
@@ -530,6 +534,13 @@ class HaloShard:
                 raise ValueError(f"send rows for peer {q} index past the {plan.n_local} local rows")
         self.send_rows = {q: torch.as_tensor(rows.astype(np.int32), device=self.device)
                           for q, rows in plan.send_to.items()}
+        # the tiled pack of every peer in one launch: rows concatenated in peer order
+        self.send_peers = sorted(plan.send_to)
+        self.send_row0 = np.concatenate(
+            [[0], np.cumsum([len(plan.send_to[q]) for q in self.send_peers])]).astype(int).tolist()
+        self.send_rows_cat = torch.as_tensor(
+            np.concatenate([plan.send_to[q] for q in self.send_peers]).astype(np.int32)
+            if self.send_peers else np.zeros(0, np.int32), device=self.device)
         # per-peer halo blocks in halo_offset order (dl_mix_args.n_halo_blocks)
         self.halo_blocks = [len(plan.halo_from[q]) for q in
                             sorted(plan.halo_from, key=lambda q: plan.halo_offset[q])]
@@ -609,6 +620,10 @@ class HaloShard:
         send, halo, recv = self._buffers(slot, c1 - c0)
         Gc = self._cols(G, c0, c1) if G is not None else None
         Xc = self._cols(self.X, c0, c1)
+        if self.T and self.send_peers and hasattr(self.ops, "step_rows_peers"):
+            self.ops.step_rows_peers(Xc, self.send_rows_cat, self.send_row0,
+                                     [send[q] for q in self.send_peers], G=Gc, lr=lr)
+            return send, halo, recv
         for q, rows in self.send_rows.items():
             self.ops.step_rows(Xc, rows, send[q], G=Gc, lr=lr)
         return send, halo, recv

@@ -446,13 +446,15 @@ class HipOps:
         return self.E.step_rows_tiled_peers(X, rows, row0, outs, G=G, lr=lr)
 
     def mix(self, W, X, Y, G=None, lr=0.0, halo=None, lag=None, halo_blocks=None):
-        """lag = (mean_prev, colsum_out, dev_sq): the lagged deviation of a halo round.
+        """lag = (mean_prev, colsum_out, dev_sq[, dev_max]): the lagged deviation of a halo
+        round (dev_max, nullable: max sqrt(dev_sq) from the same launch's reduce).
         Column-tiled operands are 3-D [tiles, rows, T] (views), the halo then a flat buffer of
         per-peer tiled blocks of ``halo_blocks`` rows."""
         tiled = (X.shape[0] * X.shape[2], X.shape[2]) if X.dim() == 3 else None
-        mean_prev, colsum, dsq = lag if lag is not None else (None, None, None)
-        self.E.mix_round(W, X, Y, G=G, lr=lr, halo=halo, dev_sq=dsq, mean_prev=mean_prev,
-                         colsum_out=colsum, workspace=self.ws, tiled=tiled,
+        mean_prev, colsum, dsq, dmax = (tuple(lag) + (None,))[:4] if lag is not None else \
+            (None, None, None, None)
+        self.E.mix_round(W, X, Y, G=G, lr=lr, halo=halo, dev_sq=dsq, dev_max=dmax,
+                         mean_prev=mean_prev, colsum_out=colsum, workspace=self.ws, tiled=tiled,
                          halo_blocks=halo_blocks)
 
     def column_sum(self, X):
@@ -669,9 +671,13 @@ class HaloShard:
             colsum = torch.empty(self.P, dtype=torch.float32, device=self.device)
             parts = torch.empty(len(chunks), self.plan.n_local, dtype=torch.float32,
                                 device=self.device)
-            lag = (self.mean_prev, colsum, parts)
+            # one launch measures every local row (one chunk, or the split's interior launch):
+            # its reduce also gives the max, no torch kernels of its own
+            one = split or len(chunks) == 1
+            dmax = torch.empty(1, dtype=torch.float32, device=self.device) if one else None
+            lag = (self.mean_prev, colsum, parts, dmax)
         if split:
-            self._split_round(G, lr, None if lag is None else (lag[0], lag[1], lag[2][0]))
+            self._split_round(G, lr, None if lag is None else (lag[0], lag[1], lag[2][0], lag[3]))
         else:
             self._mix_all(chunks, G, lr, lag)
         if lag is None:
@@ -679,10 +685,13 @@ class HaloShard:
             # step moved the mean): the next lagged round recomputes it
             self.mean_prev = None
             return None
-        dev_sq = parts.sum(0)
+        if dmax is not None:
+            dev_sq, dev_max = parts[0], dmax
+        else:
+            dev_sq = parts.sum(0)
+            dev_max = torch.sqrt(dev_sq.max()).reshape(1)
         self.transport.all_reduce_(colsum, "sum")
         self.mean_prev = colsum / float(self.n_total)
-        dev_max = torch.sqrt(dev_sq.max()).reshape(1)
         self.transport.all_reduce_(dev_max, "max")
         return dev_sq, dev_max
 
@@ -703,7 +712,7 @@ class HaloShard:
             works, halo = pend
             for w in works:
                 w.wait()
-            cl = None if lag is None else (lag[0][c0:c1], lag[1][c0:c1], lag[2][j])
+            cl = None if lag is None else (lag[0][c0:c1], lag[1][c0:c1], lag[2][j], lag[3])
             self.mix_chunk(c0, c1, halo, G, lr, cl)
             pend = nxt
         self.X, self.Y = self.Y, self.X

@@ -8,7 +8,7 @@ O=gpurun_out/r11b; mkdir -p $O
 step() { local name=$1 t=$2; shift 2; echo "=== $name"; timeout -k 10 "$t" "$@" > $O/$name.log 2>&1; local rc=$?;
          echo "=== $name rc=$rc"; tail -3 $O/$name.log | cut -c1-400;
          if [ $rc -ne 0 ] && ! { [ "${SOFT:-0}" = 1 ] && [ $rc -eq 1 ]; }; then exit $rc; fi; }
-SOFT=1 step tests 600 python -u -m pytest tests/test_sharding_gpu.py -v -m gpu --timeout 300 --timeout-method thread
+SOFT=1 step tests 600 python -u -m pytest tests/test_sharding_gpu.py tests/test_mix_trace_gpu.py tests/test_mix_ragged_gpu.py -v -m gpu --timeout 300 --timeout-method thread
 if grep -q -i -E "hipError|illegal|memory access fault|HSA_STATUS_ERROR|Aborted" $O/tests.log; then
     echo "device error in the tests: stopping"; exit 4; fi
 B="python bench.py --workload c4-rank --steps 50 --warmup 5"

@@ -50,9 +50,11 @@ class OracleOps:
             return
         T = X.numpy()
         if lag is not None:     # lagged deviation of the input rows + sums of the stepped rows
-            mean_prev, colsum, dsq = lag
+            mean_prev, colsum, dsq = lag[:3]
             D = (T - mean_prev.numpy()).astype(np.float64)
             dsq.copy_(torch.from_numpy((D * D).sum(1).astype(np.float32)))
+            if len(lag) > 3 and lag[3] is not None:   # the launch's max as well
+                lag[3].copy_(torch.sqrt(dsq.max()).reshape(1))
         if G is not None:
             T = M.sgd_step(T, G.numpy(), lr)
         if lag is not None:

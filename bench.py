@@ -596,6 +596,7 @@ def run_gather(args, dev, rank, world):
                               order="auto" if args.order == "auto" else None)
     G = eng.layout_like(torch.randn(n, P, device=dev, generator=gen))
     plan = eng.plan(deviation=True)
+    plan["hub_rows"] = int(eng.W.hub_rows)       # rows folded by four column lanes (path 5)
     kname = kernel_name(plan, True, True, n)     # the instance this plan launches
     elapsed, launch_ms = timed(lambda: eng.round(G=G, lr=lr, deviation=True))
     del eng, G
@@ -660,8 +661,8 @@ def _halo_schemes(args, dev, rank, world, csr, parts, P, lr, gen):
     schemes = {}
     names = ["chunks", "split"] if args.halo_overlap == "both" else [args.halo_overlap]
     for name in names:
-        rp = (sharding.split_halo_plans if name == "split" else sharding.halo_plans)(
-            csr, parts)[rank]
+        # boundary-last row order for both schemes (the pack reads one contiguous run of rows)
+        rp = sharding.split_halo_plans(csr, parts)[rank]
         shard = sharding.HaloShard(rp, P, dev, sharding.dist_transport(),
                                    chunk_cols=P // 8 if name == "chunks" else None,
                                    n_agents_total=n, overlap=name)
@@ -838,8 +839,10 @@ def run_c4rank(args, dev, rank, world):
     names = {"whole": ("chunks", None), "chunks": ("chunks", P // 8), "split": ("split", None)}
     G = kern = None
     for name, (overlap, chunk) in names.items():
-        rp = (sharding.split_halo_plans if overlap == "split" else sharding.halo_plans)(
-            csr, parts)[0]
+        # boundary-last row order for every scheme: the rows the peers read are then one
+        # contiguous run of each tile block, so the pack reads whole cache lines (the torus
+        # block's left / right columns are every 16th row in partition order)
+        rp = sharding.split_halo_plans(csr, parts)[0]
         shard = sharding.HaloShard(rp, P, dev, sharding.ResidentHaloTransport(),
                                    chunk_cols=chunk, n_agents_total=n, overlap=overlap,
                                    tile_cols=args.halo_tile_cols or None)

@@ -923,6 +923,11 @@ template <int C>
 hipError_t launch_fast_c(const TileArgs &a, int kv, bool sgd, bool dev, bool mix, int grid,
                          int lds, hipStream_t s) {
     if (kv <= 2) return launch_mode<C, 2, true>(a, sgd, dev, mix, grid, lds, s);
+    // a column-tiled halo round of 2..3 row passes (c4 at 8 GPUs: 512 + 96 rows at C = 4) runs
+    // three passes instead of four: the fourth would only re-read row 0 (45 % of the staging
+    // loads dead at 608 rows)
+    if (kv == 3 && a.tiled && a.n_src > a.n_loc && C >= 2 && C <= 8)
+        return launch_part<C, 3, true, 2>(a, sgd, grid, lds, s);
     if (kv <= 4) return launch_mode<C, 4, true>(a, sgd, dev, mix, grid, lds, s);
     return launch_mode<C, 8, true>(a, sgd, dev, mix, grid, lds, s);
 }
@@ -993,7 +998,9 @@ hipError_t launch_mix_tile_reg(const TileArgs &a, int chunks, int head, int tail
 hipError_t launch_mix_tile(const TileArgs &a, int chunks, bool sgd, bool dev, bool mix, int grid,
                            int lds, bool fast, hipStream_t s) {
     if (fast) {
-        const int kv = tile_passes(chunks, a.n_src, true);
+        int kv = tile_passes(chunks, a.n_src, true);
+        const int need = (a.n_src + kTileThreads / chunks - 1) / (kTileThreads / chunks);
+        if (need == 3 && mix && a.tiled && a.n_src > a.n_loc) kv = 3;   // (launch_fast_c)
         switch (chunks) {
             case 1: return launch_fast_c<1>(a, kv, sgd, dev, mix, grid, lds, s);
             case 2: return launch_fast_c<2>(a, kv, sgd, dev, mix, grid, lds, s);

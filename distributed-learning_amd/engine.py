@@ -473,14 +473,17 @@ def perron_round(Y, rowptr, col, eps, conv_eps, weight=None, mean_weight=1.0, ma
     return int(iters.item())
 
 
-HUB_TAIL = 32   # plan path 5: rows with more tail entries than this are folded by column lanes
+HUB_TAIL = 0   # plan path 5: rows with more tail entries than this are folded by column lanes
 
 
 def hub_rows(csr, head, tail=HUB_TAIL, cap=256):
     """dl_mix_args.n_hub_rows for plan path 5: the leading rows (a descending row-length order
-    puts the longest first) whose LDS tails exceed ``tail`` entries, at most ``cap``.  Measured:
-    a Barabasi-Albert hub's serial fold bounds the tile (irregular graphs).
-    DLAMD_HUB_ROWS=k overrides it (0 = off; measurements)."""
+    puts the longest first) whose LDS tails exceed ``tail`` entries, at most ``cap`` -- 256 rows
+    = every thread of the workgroup folds one column of one of them.  Measured on c4-ba
+    (Barabasi-Albert m = 2, 4096 x 2^18): 440 rounds/s with 256 such rows against 387 with none
+    and 380 with only the 24 rows of more than 32 tail entries (profiles/r11/session_b): the
+    4-way split pays when it spreads over the whole workgroup.  DLAMD_HUB_ROWS=k overrides it
+    (0 = off; measurements)."""
     env = os.environ.get("DLAMD_HUB_ROWS")
     if env is not None:
         return max(0, min(int(env), cap, csr.n_rows))

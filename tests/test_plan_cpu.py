@@ -110,8 +110,8 @@ def test_trace_round_caps(n, want):
 
 def test_hub_rows_of_a_row_length_order(monkeypatch):
     """engine.hub_rows (dl_mix_args.n_hub_rows for plan path 5): the leading rows of a
-    descending row-length order whose LDS tails exceed 32 entries -- the Barabasi-Albert hubs --
-    capped at 256; DLAMD_HUB_ROWS overrides it.  The plan reports the register head it is
+    descending row-length order with LDS tails (more than ``tail`` entries, default 0), capped
+    at 256; DLAMD_HUB_ROWS overrides it.  The plan reports the register head it is
     measured against (ABI 8 dl_mix_plan.head / tail_fmt)."""
     csr = graph.barabasi_albert_metropolis(4096, 2, 1)
     p = plan(csr)
@@ -121,17 +121,16 @@ def test_hub_rows_of_a_row_length_order(monkeypatch):
     lens = np.diff(pc.rowptr)
     assert np.all(np.diff(lens) <= 0)               # descending
     h = engine.hub_rows(pc, p["head"])
-    assert 0 < h <= 256 and np.all(lens[:h] - 3 > 32) and lens[h] - 3 <= 32
+    assert h == 256 and np.all(lens[:h] - 3 > 0)
     assert engine.hub_rows(csr, p["head"]) < h or lens[0] == np.diff(csr.rowptr)[0]
     monkeypatch.setenv("DLAMD_HUB_ROWS", "0")
     assert engine.hub_rows(pc, 3) == 0
     monkeypatch.setenv("DLAMD_HUB_ROWS", "999")
     assert engine.hub_rows(pc, 3) == 256
-    # a hub-free irregular graph has none
+    # a graph whose longest rows fit the register head has none
     monkeypatch.delenv("DLAMD_HUB_ROWS")
-    deg = graph.random_irregular_metropolis(4096, 2, 6, 1)
-    pd = graph.permuted(deg, graph.row_length_order(deg))
-    assert engine.hub_rows(pd, plan(deg)["head"]) == 0
+    short = graph.Csr([0, 2, 4, 6], [0, 1, 1, 2, 0, 2], [0.5] * 6)
+    assert engine.hub_rows(short, 2) == 0
 
 
 def test_traced_plan_takes_any_topology_that_fits():

@@ -109,8 +109,9 @@ def parse():
                         "per-edge FDLA SDP weights of the c2 graph, tests/golden/fdla_rr4_1024.npz)")
     p.add_argument("--no-fdla-probe", action="store_true",
                    help="c2 at N=1: skip the second measurement with per-edge FDLA weights")
-    p.add_argument("--halo-overlap", default="both", choices=["both", "chunks", "split"],
-                   help="c4 at N>1: halo overlap scheme(s) to time (sharding.HaloShard)")
+    p.add_argument("--halo-overlap", default="both", choices=["both", "whole", "chunks", "split"],
+                   help="c4 at N>1: halo overlap scheme(s) to time (sharding.HaloShard; both = "
+                        "all three)")
     p.add_argument("--dist-backend", default="nccl",
                    help="nccl (= RCCL, default) or gloo (multi-rank rehearsal on one GPU)")
     return p.parse_args()
@@ -228,6 +229,8 @@ def kernel_name(plan, sgd, dev, n_src, halo=0, lag=False):
     c = plan["tile_cols"] // 4
     need = -(-n_src // (1024 // c))
     kv = 2 if need <= 2 else 4 if need <= 4 else 8
+    if halo == 2 and need == 3 and 2 <= c <= 8:   # the three-pass tiled halo instantiation
+        kv = 3
     b = lambda v: "true" if v else "false"  # noqa: E731
     rd = plan.get("head", 0) if plan["path"] in (4, 5) else 0
     rag = plan.get("tail_fmt", 0) if plan["path"] == 5 else 0
@@ -238,14 +241,21 @@ def kernel_name(plan, sgd, dev, n_src, halo=0, lag=False):
 PROFILE_C2 = os.path.join(ROOT, "profiles", "r11", "c2", "summary.json")
 
 
-def traffic_from_profile(kname, path=PROFILE_C2):
+def traffic_from_profile(kname, path=PROFILE_C2, bytes_hint=None):
     """HBM bytes per launch of this kernel from the committed rocprofv3 PMC summary
-    (FETCH_SIZE x 2 + WRITE_SIZE, gfx950 correction), or None if it was not profiled."""
+    (FETCH_SIZE x 2 + WRITE_SIZE, gfx950 correction), or None if it was not profiled.  A kernel
+    profiled at several launch sizes (``size_classes``: a whole round and its column chunks)
+    gives the class nearest ``bytes_hint`` (the algorithmic bytes of the launch timed here)."""
     try:
         with open(path) as f:
-            kernels = json.load(f)["kernels"]
+            summ = json.load(f)
+        kernels = summ["kernels"]
     except (OSError, ValueError, KeyError):
         return None, None
+    for name, classes in summ.get("size_classes", {}).items():
+        if kname in name and bytes_hint:
+            c = min(classes, key=lambda c: abs(c["hbm_bytes_per_launch"] - bytes_hint))
+            return c["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
     for name, e in kernels.items():
         if kname in name and "hbm_bytes_per_launch" in e:
             return e["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
@@ -659,13 +669,17 @@ def _halo_schemes(args, dev, rank, world, csr, parts, P, lr, gen):
     n = csr.n_rows
     G = None
     schemes = {}
-    names = ["chunks", "split"] if args.halo_overlap == "both" else [args.halo_overlap]
+    # "whole": one exchange, then one launch (no overlap, no per-chunk launches); "chunks": 8
+    # column chunks, the exchange of one overlapping the mix of the previous; "split": the
+    # interior rows mix while the one exchange is in flight
+    names = ["whole", "chunks", "split"] if args.halo_overlap == "both" else [args.halo_overlap]
     for name in names:
-        # boundary-last row order for both schemes (the pack reads one contiguous run of rows)
+        # boundary-last row order for every scheme (the pack reads one contiguous run of rows)
         rp = sharding.split_halo_plans(csr, parts)[rank]
         shard = sharding.HaloShard(rp, P, dev, sharding.dist_transport(),
                                    chunk_cols=P // 8 if name == "chunks" else None,
-                                   n_agents_total=n, overlap=name)
+                                   n_agents_total=n, overlap="split" if name == "split" else
+                                   "chunks")
         shard.X.normal_(generator=gen)
         if G is None:   # synthetic gradient rows, shared by both schemes (same shape and layout)
             G = engine.staggered_zeros(shard._shape(rp.n_local), 2, dev).normal_(generator=gen)
@@ -905,7 +919,7 @@ def run_c4rank(args, dev, rank, world):
         v["round_hbm_frac"] = v["round_hbm_bytes"] / (v["round_ms"] / 1e3) / 1e9 / HBM_PEAK_GBS
     achieved = kern["mix_bytes"] / (kern["mix_ms"] / 1e3) / 1e9
     traffic, src = traffic_from_profile(kern["kernel_instance"], os.path.join(
-        ROOT, "profiles", "r11", "c4rank", "summary.json"))
+        ROOT, "profiles", "r11", "c4rank", "summary.json"), bytes_hint=kern["mix_bytes"])
     rec = {
         "metric": f"c4 per-rank halo round, one rank of {args.rank_of} alone (64x64 torus, "
                   f"4096 agents x 2^18 fp32 params)",

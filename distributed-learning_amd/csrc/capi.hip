@@ -267,13 +267,13 @@ int plan_mix(const dl_mix_args *a, Plan *pl) {
                                         "(%d rows); query dl_mix_plan_query on row-major args",
                         a->tile_cols, R);
         const int64_t n_tiles = (a->n_params + a->tile_cols - 1) / a->tile_cols;
-        // two 1024-thread workgroups per CU when LDS allows, except for C = 4 tiles of 64 KiB
-        // (c2's 1024 agents), where the second workgroup's LDS traffic (4 rows of 64 B per 16
-        // lanes: the most bank conflicts of any C) costs more than its extra loads in flight
-        // (measured 5.5 vs 5.8 TB/s at N = 1024)
+        // two 1024-thread workgroups per CU when LDS allows, except at C = 4, where the second
+        // workgroup's LDS traffic (4 rows of 64 B per 16 lanes: the most bank conflicts of any
+        // C) costs more than its extra loads in flight (measured 5.5 vs 5.8 TB/s at N = 1024;
+        // the c4 rank of 8's 608-row halo round: 69.1 vs 70.1 % of spec, profiles/r11/session_c)
         int bpc = (int)(dl::kLdsBytes / lds);
         if (bpc > wg_per_cu_cap()) bpc = wg_per_cu_cap();
-        if (c == 4 && tile >= 65536) bpc = 1;
+        if (c == 4) bpc = 1;
         const int64_t grid =
             balanced_grid(n_tiles, (int64_t)device_cus() * (bpc < 1 ? 1 : bpc) * grid_mult());
         pl->pub.path = 1;

@@ -30,6 +30,43 @@ def counters(path, name):
     return {k: sum(v) / len(v) for k, v in per.items()}
 
 
+def per_launch(path, name):
+    """kernel -> [counter value of its 1st, 2nd, ... launch] (dispatch order)."""
+    per = collections.defaultdict(list)
+    rows = [r for r in csv.DictReader(open(path)) if r["Counter_Name"] == name]
+    for r in sorted(rows, key=lambda r: int(r["Dispatch_Id"])):
+        per[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+    return per
+
+
+def size_classes(trace_path, fetch_path, write_path):
+    """One kernel launched at several sizes (e.g. a whole round and its column chunks): its
+    launches grouped by HBM bytes (2 x FETCH_SIZE + WRITE_SIZE, two significant digits), each
+    class with its launch count, bytes and the average duration of the same launches in the
+    trace pass (the program is deterministic: the k-th launch of a kernel is the same launch in
+    every pass)."""
+    durs = collections.defaultdict(list)
+    rows = list(csv.DictReader(open(trace_path)))
+    for t in sorted(rows, key=lambda t: int(t["Start_Timestamp"])):
+        durs[t["Kernel_Name"]].append((int(t["End_Timestamp"]) - int(t["Start_Timestamp"])) / 1e3)
+    fe, wr = per_launch(fetch_path, "FETCH_SIZE"), per_launch(write_path, "WRITE_SIZE")
+    out = {}
+    for k in fe:
+        n = min(len(fe[k]), len(wr.get(k, [])), len(durs.get(k, [])))
+        if n == 0:
+            continue
+        cls = collections.defaultdict(list)
+        for i in range(n):
+            b = 2 * fe[k][i] * 1024 + wr[k][i] * 1024
+            cls[float(f"{b:.2g}")].append((b, durs[k][i]))
+        if len(cls) < 2:
+            continue
+        out[k] = [{"launches": len(v), "hbm_bytes_per_launch": sum(x[0] for x in v) / len(v),
+                   "avg_us": sum(x[1] for x in v) / len(v)}
+                  for _, v in sorted(cls.items(), reverse=True)]
+    return out
+
+
 def main(src, dst, note):
     os.makedirs(dst, exist_ok=True)
     stats = one(f"{src}/trace/**/*kernel_stats.csv")
@@ -53,6 +90,10 @@ def main(src, dst, note):
             e["hbm_bytes_per_launch"] = e["hbm_read_bytes_corrected"] + e["hbm_write_bytes"]
         kernels[r["Name"]] = e
     out = {"note": note, "kernels": kernels}
+    sc = size_classes(trace, one(f"{src}/fetch/**/*counter_collection.csv"),
+                      one(f"{src}/write/**/*counter_collection.csv"))
+    if sc:
+        out["size_classes"] = sc
     last = int(os.environ.get("LAST", "0"))
     if last:   # the timed steps: the last LAST launches of every kernel launched that often
         per = collections.defaultdict(list)

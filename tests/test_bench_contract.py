@@ -93,4 +93,16 @@ def test_kernel_names_follow_the_plan(bench):
     p5 = bench.kernel_name({"path": 5, "tile_cols": 4, "head": 2, "tail_fmt": 2}, True, True, 4096)
     assert p5 == "mix_tile_kernel<1, 4, true, true, true, 0, true, 2, false, 2>(dl::TileArgs)"
     h = bench.kernel_name({"path": 1, "tile_cols": 16}, True, False, 608, halo=2, lag=True)
-    assert h == "mix_tile_kernel<4, 4, true, false, true, 2, true, 0, true, 0>(dl::TileArgs)"
+    assert h == "mix_tile_kernel<4, 3, true, false, true, 2, true, 0, true, 0>(dl::TileArgs)"
+
+
+def test_c4_rank_kernel_has_committed_traffic(bench):
+    """The one-rank-of-8 c4 line's roofline cites the committed rocprofv3 PMC summary of its own
+    kernel instance: the whole-round launches' class (the profile also holds the 8-chunk
+    scheme's launches of the same instance), within 1 % of the algorithmic bytes."""
+    alg = 4 * 2 ** 18 * (3 * 512 + 96) + 8 * 2 ** 18
+    name = bench.kernel_name({"path": 1, "tile_cols": 16}, True, False, 608, halo=2, lag=True)
+    traffic, src = bench.traffic_from_profile(
+        name, os.path.join(ROOT, "profiles", "r11", "c4rank", "summary.json"), bytes_hint=alg)
+    assert traffic is not None and src.startswith("profiles/")
+    assert abs(traffic / alg - 1) < 0.01

@@ -106,3 +106,15 @@ def test_c4_rank_kernel_has_committed_traffic(bench):
         name, os.path.join(ROOT, "profiles", "r11", "c4rank", "summary.json"), bytes_hint=alg)
     assert traffic is not None and src.startswith("profiles/")
     assert abs(traffic / alg - 1) < 0.01
+
+
+def test_c4_ba_kernel_has_committed_traffic(bench):
+    """The c4-ba line (plan path 5: register head of 3, packed LDS tail, 256 hub rows) finds its
+    kernel instance in the committed profile, within 1 % of the algorithmic 12 B per element."""
+    alg = 12 * 4096 * 2 ** 18
+    name = bench.kernel_name({"path": 5, "tile_cols": 4, "head": 3, "tail_fmt": 2}, True, True,
+                             4096)
+    traffic, src = bench.traffic_from_profile(
+        name, os.path.join(ROOT, "profiles", "r11", "c4ba", "summary.json"))
+    assert traffic is not None and src.startswith("profiles/")
+    assert abs(traffic / alg - 1) < 0.01

@@ -126,6 +126,10 @@ def test_register_head_lds_tail(cuda, monkeypatch, case, layout):
     assert np.array_equal(bits(eng.rows().cpu().numpy()), bits(want))
     check_dev(want, eng.agent_dev_sq().cpu().numpy(), float(eng.dev_max.item()),
               mean.cpu().numpy())
+    if head < 5:
+        # the result above ran with the leading rows' tails folded four column lanes each
+        # (dl_mix_args.n_hub_rows: every leading row with a tail, up to 256)
+        assert 0 < eng.W.hub_rows <= 256, eng.W.hub_rows
     # plain mix (no local step, no deviation) through the same path, rows in agent order
     # instead of the engine's default row-length order: the same bits
     eng2 = E.GossipEngine(csr, P, device=cuda, X=torch.from_numpy(X).to(cuda), layout=layout,
@@ -183,11 +187,33 @@ def test_reference_fixture_b_through_path5(cuda, golden, monkeypatch, rounds):
             eng = E.GossipEngine(csr, X0.shape[1], device=cuda,
                                  X=torch.from_numpy(X0).to(cuda), layout=layout)
             assert eng.plan()["path"] == path, (tag, layout, eng.plan())
+            if path == 5:
+                assert eng.W.hub_rows > 0   # the leading rows' tails on four lanes each
             for _ in range(rounds):
                 eng.round()
             torch.cuda.synchronize()
             assert np.array_equal(bits(eng.rows().cpu().numpy()), bits(d[f"{tag}_X{rounds}"])), \
                 (tag, layout)
+
+
+@pytest.mark.parametrize("hubs", [0, 5, 64])
+def test_fixture_b_hub_row_counts(cuda, golden, monkeypatch, hubs):
+    """dl_mix_args.n_hub_rows (DLAMD_HUB_ROWS override) only moves which lanes fold the leading
+    rows' LDS tails (one column each, CSR order): none, some, and every row of fixture B --
+    including rows whose tail is empty -- give the reference's bits after 10 rounds."""
+    from distributed_learning_amd.graph import Csr
+    E = eng_mod()
+    d = golden("mix_rr4_n64.npz")
+    monkeypatch.setenv("DLAMD_FORCE_REG", "1")
+    monkeypatch.setenv("DLAMD_HUB_ROWS", str(hubs))
+    csr = Csr(d["b_rowptr"], d["b_cols"], d["b_w"])
+    X0 = d["b_X0"]
+    eng = E.GossipEngine(csr, X0.shape[1], device=cuda, X=torch.from_numpy(X0).to(cuda))
+    assert eng.plan()["path"] == 5 and eng.W.hub_rows == hubs
+    for _ in range(10):
+        eng.round()
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(eng.rows().cpu().numpy()), bits(d["b_X10"]))
 
 
 def test_plan_csr_reports_path5_and_refuses_bad_promise(cuda):

@@ -15,6 +15,8 @@ bash scripts/gpu_steps.sh \
   "evidence/c4_trace8|200|python bench.py --workload c2-gossip --graph torus --agents 4096 --params 262144 --trace --rounds 8 --relabel 0 --steps 10 --warmup 2 --no-cpu" \
   "evidence/c4_gather|200|python bench.py --workload c4-gather --steps 20 --warmup 3 --no-cpu" \
   "evidence/c4_ba|200|python bench.py --workload c4-ba --steps 20 --warmup 3 --no-cpu" \
+  "evidence/c4_ba1|200|python bench.py --workload c4-ba --irregular ba1 --steps 20 --warmup 3 --no-cpu" \
+  "evidence/c4_rank|200|python bench.py --workload c4-rank --steps 50 --warmup 5" \
   "evidence/c1|200|python bench.py --workload c1 --steps 4000 --warmup 1" \
   "evidence/mixer_eps|200|python scripts/mixer_eps_probe.py" \
   "evidence/c5|600|python bench.py --workload c5 --steps 10 --warmup 3"

@@ -229,7 +229,7 @@ def kernel_name(plan, sgd, dev, n_src, halo=0, lag=False):
     c = plan["tile_cols"] // 4
     need = -(-n_src // (1024 // c))
     kv = 2 if need <= 2 else 4 if need <= 4 else 8
-    if halo == 2 and need == 3 and 2 <= c <= 8:   # the three-pass tiled halo instantiation
+    if halo == 2 and need == 3 and c <= 8:   # the three-pass tiled halo instantiation
         kv = 3
     b = lambda v: "true" if v else "false"  # noqa: E731
     rd = plan.get("head", 0) if plan["path"] in (4, 5) else 0

@@ -923,10 +923,10 @@ template <int C>
 hipError_t launch_fast_c(const TileArgs &a, int kv, bool sgd, bool dev, bool mix, int grid,
                          int lds, hipStream_t s) {
     if (kv <= 2) return launch_mode<C, 2, true>(a, sgd, dev, mix, grid, lds, s);
-    // a column-tiled halo round of 2..3 row passes (c4 at 8 GPUs: 512 + 96 rows at C = 4) runs
-    // three passes instead of four: the fourth would only re-read row 0 (45 % of the staging
-    // loads dead at 608 rows)
-    if (kv == 3 && a.tiled && a.n_src > a.n_loc && C >= 2 && C <= 8)
+    // a column-tiled halo round of 2..3 row passes (c4 at 8 GPUs: 512 + 96 rows at C = 4; at 2
+    // GPUs 2048 + 128 rows at C = 1) runs three passes instead of four: the fourth would only
+    // re-read row 0 (45 % of the staging loads dead at 608 rows, 47 % at 2176)
+    if (kv == 3 && a.tiled && a.n_src > a.n_loc && C <= 8)
         return launch_part<C, 3, true, 2>(a, sgd, grid, lds, s);
     if (kv <= 4) return launch_mode<C, 4, true>(a, sgd, dev, mix, grid, lds, s);
     return launch_mode<C, 8, true>(a, sgd, dev, mix, grid, lds, s);

@@ -205,7 +205,9 @@ def halo_plans(csr: Csr, parts):
 
     Entry order within a row is preserved (so the fp32 fold is identical to the single-device
     round); remote columns are renumbered into the halo block of their owner, blocks ordered by
-    peer rank and, inside a block, by global id."""
+    peer rank and, inside a block, in the owner's row order -- so a peer's send rows are its
+    local rows in increasing order, and a plan whose send sets are contiguous row ranges
+    (split_halo_plans) packs every peer's block from one contiguous run of rows."""
     world = len(parts)
     owner = np.empty(csr.n_rows, np.int64)
     pos = np.empty(csr.n_rows, np.int64)
@@ -225,7 +227,7 @@ def halo_plans(csr: Csr, parts):
         off = 0
         for q in range(world):
             if need[r][q]:
-                ids = np.asarray(sorted(need[r][q]), np.int64)
+                ids = np.asarray(sorted(need[r][q], key=lambda b: pos[b]), np.int64)
                 halo_from[q] = ids
                 halo_offset[q] = off
                 for i, b in enumerate(ids):
@@ -240,22 +242,55 @@ def halo_plans(csr: Csr, parts):
             rowptr.append(len(col))
         local_csr = Csr(rowptr, col, w, keys=[csr.keys[a] for a in p] if csr.keys else [],
                         n_src=len(p) + off)
-        send_to = {q: pos[np.asarray(sorted(need[q][r]), np.int64)]
+        send_to = {q: np.sort(pos[np.asarray(sorted(need[q][r]), np.int64)])
                    for q in range(world) if need[q][r]}
         plans.append(RankPlan(r, np.asarray(p), local_csr, halo_from, send_to, halo_offset,
                               doubly_stochastic=bool(csr.doubly_stochastic)))
     return plans
 
 
+def _peer_grouped(rows, sig):
+    """Order boundary rows so that every peer's send set is one contiguous run: rows grouped by
+    their signature (the set of peers that read them), the groups in an order where the groups
+    holding any one peer are consecutive -- e.g. a 32 x 16 torus block's [left column | top-left
+    corner | top and bottom rows | top-right corner | right column] -- found by search over
+    the group orders when there are at most 8 groups (the torus blocks have 3 or 5), else by
+    the groups' smallest peer.  Rows keep the partition's order inside a group."""
+    groups = {}
+    for r in rows:
+        groups.setdefault(sig[r], []).append(r)
+    keys = sorted(groups, key=lambda k: (min(k) if k else -1, len(k), sorted(k)))
+    peers = sorted(set().union(*keys)) if keys else []
+
+    def runs(order):
+        tot = 0
+        for p in peers:
+            inside = [p in k for k in order]
+            tot += sum(1 for i, v in enumerate(inside) if v and (i == 0 or not inside[i - 1]))
+        return tot
+
+    if 2 < len(keys) <= 8 and runs(keys) > len(peers):
+        import itertools
+        best = min(itertools.permutations(keys), key=runs)
+        keys = list(best)
+    return np.asarray([r for k in keys for r in groups[k]], np.int64)
+
+
 def split_halo_plans(csr: Csr, parts):
     """halo_plans with every rank's agents in boundary-last order: [interior rows no boundary row
-    reads | interior rows a boundary row reads | boundary rows (they read halo rows)], each group
-    in the partition's order.  The interior rows then mix while the halo is in flight, and the
+    reads | interior rows a boundary row reads | boundary rows (they read halo rows)], the first
+    two groups in the partition's order, the boundary rows grouped by the peers that read them
+    so that each peer's send rows are one contiguous run (the halo pack then reads whole
+    segments: ``_peer_grouped``).  The interior rows mix while the halo is in flight, and the
     boundary rows read only the window [n_deep, n_local) of local rows plus the halo
     (RankPlan.row_sets).  Entry order within every row is kept (bit-identical rounds)."""
     first = halo_plans(csr, parts)
     new_parts, counts = [], []
     for pl in first:
+        sig = [frozenset() for _ in range(pl.n_local)]
+        for q, rows in pl.send_to.items():
+            for r in rows:
+                sig[int(r)] = sig[int(r)] | {q}
         c, n = pl.csr, pl.n_local
         row_of = np.repeat(np.arange(n), np.diff(c.rowptr))
         bnd = np.zeros(n, bool)
@@ -264,7 +299,8 @@ def split_halo_plans(csr: Csr, parts):
         adj[c.col[bnd[row_of] & (c.col < n)]] = True
         adj &= ~bnd
         deep = ~bnd & ~adj
-        order = np.concatenate([np.flatnonzero(deep), np.flatnonzero(adj), np.flatnonzero(bnd)])
+        order = np.concatenate([np.flatnonzero(deep), np.flatnonzero(adj),
+                                _peer_grouped(np.flatnonzero(bnd), sig)])
         new_parts.append(pl.local[order])
         counts.append((int(deep.sum()), int(deep.sum() + adj.sum())))
     plans = halo_plans(csr, new_parts)

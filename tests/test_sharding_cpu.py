@@ -74,6 +74,25 @@ def test_halo_plans_reconstruct_the_graph(kind):
             assert np.array_equal(pl.local[rows], plans[q].halo_from[pl.rank])
 
 
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_split_plans_send_runs_are_contiguous(world):
+    """c4's torus blocks in boundary-last order: every peer's send rows are one contiguous run of
+    local rows (boundary rows grouped by the peers that read them, corners between their two
+    edges), and each receiver's halo block lists them in the sender's row order -- so the halo
+    pack reads whole segments and the receive order matches the send order."""
+    rows = cols = 64
+    plans = sharding.split_halo_plans(torus_csr(rows, cols),
+                                      sharding.torus_block_partition(rows, cols, world))
+    by_rank = {pl.rank: pl for pl in plans}
+    for pl in plans:
+        for q, send in pl.send_to.items():
+            send = np.asarray(send)
+            assert np.array_equal(send, np.arange(send[0], send[0] + len(send))), (world, q)
+            assert send[0] >= pl.n_interior          # boundary rows only
+            # the receiver's halo block from me = my rows in my order
+            assert np.array_equal(by_rank[q].halo_from[pl.rank], pl.local[send])
+
+
 @pytest.mark.parametrize("kind", ["torus", "rr4", "bfs"])
 def test_split_plans_row_sets(kind):
     """split_halo_plans orders every rank's rows [deep interior | interior read by the boundary |

@@ -235,11 +235,17 @@ def test_virtual_ranks_random_graph_bfs_partition(cuda, overlap, layout):
             assert float(dmax.item()) == pytest.approx(float(wmax.item()), rel=1e-5)
 
 
+C4_RANK_SHAPES = {8: (512, 96, [32, 32, 32]), 4: (1024, 128, [64, 64]), 2: (2048, 128, [128])}
+
+
 @pytest.mark.parametrize("overlap", ["chunks", "split"])
-def test_c4_eight_ranks_full_size_tiled(cuda, overlap):
+@pytest.mark.parametrize("world", [8, 4, 2])
+def test_c4_ranks_full_size_tiled(cuda, overlap, world):
     """BASELINE config c4 at full size on one GPU: the 64 x 64 torus x 2^18 params split over 8
-    virtual ranks (32 x 16 blocks: 512 local + 96 halo rows each), column-tiled X / Y / G with
-    per-peer tiled halo blocks -- the per-rank kernel an 8-GPU run launches.  Three rounds with
+    virtual ranks (32 x 16 blocks: 512 local + 96 halo rows each; at 4 ranks 1024 + 128 rows from
+    two peers, at 2 ranks 2048 + 128 from one -- T = 16 / 8 / 4, three row passes each),
+    column-tiled X / Y / G with per-peer tiled halo blocks -- the per-rank kernel an N-GPU run
+    launches.  Three rounds with
     the lagged deviation are bit-identical to the single-device round, which itself equals the
     oracle's C restatement (oracle/cref) on a column slice; every lagged deviation is within 1e-5
     of the exact one.  Reference: the neighbour exchange it replaces,
@@ -249,7 +255,8 @@ def test_c4_eight_ranks_full_size_tiled(cuda, overlap):
     from oracle import cref
     import math
     rows = cols = 64
-    n, P, lr, world = rows * cols, 1 << 18, 1e-3, 8
+    n, P, lr = rows * cols, 1 << 18, 1e-3
+    n_local, n_halo, blocks = C4_RANK_SHAPES[world]
     edges = torus_edges(rows, cols)
     wc = 2.0 / (2.0 - 2.0 * math.cos(2 * math.pi / cols) + 8.0)
     csr = few(edges, [wc] * len(edges), list(range(n)))
@@ -275,10 +282,10 @@ def test_c4_eight_ranks_full_size_tiled(cuda, overlap):
     tr = sharding.LocalTransport(world)
     shards = []
     for pl in plans:
-        assert (pl.n_local, pl.n_halo, len(pl.halo_from)) == (512, 96, 3)
+        assert (pl.n_local, pl.n_halo, len(pl.halo_from)) == (n_local, n_halo, len(blocks))
         sh = sharding.HaloShard(pl, P, cuda, tr.endpoint(pl.rank), n_agents_total=n,
                                 overlap=overlap, chunk_cols=P // 8 if overlap == "chunks" else None)
-        assert sh.layout == "tiled" and sh.halo_blocks == [32, 32, 32]
+        assert sh.layout == "tiled" and sh.halo_blocks == blocks
         ids = torch.as_tensor(pl.local, device=cuda)
         sh.load_rows(X[ids])
         shards.append((sh, sh.layout_like(G[ids]), ids))

@@ -175,7 +175,9 @@ __device__ __forceinline__ void split4(const f32x4 &x, bf16x4 &h, bf16x4 &m, bf1
     l = bf16x4{l0[0], l0[1], l1[0], l1[1]};
 }
 
-template <bool DMA>
+// BLK: x and W1 slice-blocked ([25][64][32] and [25][150][32] per agent, the last slice zero
+// padded; b1 after W1's blocks): every slice of either operand is one contiguous block
+template <bool DMA, bool BLK = false>
 __global__ void __launch_bounds__(NT) l1_ws(const float *__restrict__ X, long ldx,
                                             const float *__restrict__ data, float *__restrict__ H) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -183,7 +185,7 @@ __global__ void __launch_bounds__(NT) l1_ws(const float *__restrict__ X, long ld
     f32x4 *raw = reinterpret_cast<f32x4 *>(smem + 2 * IMGB);  // DMA: two raw slots
     const int a = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const float *W1 = X + (long)a * ldx;
-    const float *x = data + (long)a * MB * DIN;
+    const float *x = data + (long)a * (BLK ? 25 * MB * BK : MB * DIN);
     const int ns = (DIN + BK - 1) / BK, din = DIN, dh = DH;
     if (wave >= 4) {
         const int pt = tid - NT / 2;
@@ -251,14 +253,17 @@ __global__ void __launch_bounds__(NT) l1_ws(const float *__restrict__ X, long ld
 #pragma unroll
                 for (int i = 0; i < 2; ++i) {
                     const int e = pt + i * 256, r = e / 8, c = 4 * (e % 8);
-                    rx[set][i] = *reinterpret_cast<const f32x4 *>(
-                        x + (long)r * din + (k0 + c < din ? k0 + c : din - 4));
+                    rx[set][i] = BLK ? *reinterpret_cast<const f32x4 *>(x + ((long)sl * MB + r) * BK + c)
+                                     : *reinterpret_cast<const f32x4 *>(
+                                           x + (long)r * din + (k0 + c < din ? k0 + c : din - 4));
                 }
 #pragma unroll
                 for (int i = 0; i < 5; ++i) {
                     const int e = pt + i * 256, r = e / 8, c = 4 * (e % 8);
-                    rw[set][i] = *reinterpret_cast<const f32x4 *>(
-                        W1 + (long)(r < dh ? r : dh - 1) * din + (k0 + c < din ? k0 + c : din - 4));
+                    const int rr = r < dh ? r : dh - 1;
+                    rw[set][i] = BLK ? *reinterpret_cast<const f32x4 *>(W1 + ((long)sl * dh + rr) * BK + c)
+                                     : *reinterpret_cast<const f32x4 *>(
+                                           W1 + (long)rr * din + (k0 + c < din ? k0 + c : din - 4));
                 }
             };
             auto store = [&](int set, int sl, char *img) {
@@ -293,7 +298,7 @@ __global__ void __launch_bounds__(NT) l1_ws(const float *__restrict__ X, long ld
 #pragma unroll
         for (int t = 0; t < 10; ++t) {
             const int n = 16 * t + (lane & 15);
-            bv[t] = n < dh ? W1[dh * din + n] : 0.f;
+            bv[t] = n < dh ? W1[BLK ? 25 * dh * BK + n : dh * din + n] : 0.f;
         }
         const int m = wave * 16 + (lane & 15), hq = lane >> 4;
         auto compute = [&](const char *img) {
@@ -331,10 +336,10 @@ __global__ void __launch_bounds__(NT) l1_ws(const float *__restrict__ X, long ld
     }
 }
 
-template <bool DMA>
+template <bool DMA, bool BLK = false>
 int run_ws(const char *name, float *X, long ld, float *D, float *H, int N,
            const std::vector<float> &ref) {
-    auto k = l1_ws<DMA>;
+    auto k = l1_ws<DMA, BLK>;
     const int lds = 2 * IMGB + (DMA ? 2 * RAW_F4 * 16 : 0);
     CHECK(hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     CHECK(hipMemset(H, 0, (long)N * MB * DH * 4));
@@ -479,5 +484,28 @@ int main() {
     rc |= run_ws<true>("warp-specialised, DMA producers", X, ld, D, H, N, ref);
     rc |= run_ws<false>("warp-specialised, register producers", X, ld, D, H, N, ref);
     rc |= run_ws<true>("warp-specialised, DMA producers", X, ld, D, H, N, ref);
+    // slice-blocked copies of the same x and W1 (+ b1)
+    {
+        const long ldb = ((long)25 * DH * BK + DH + 63) / 64 * 64;
+        std::vector<float> hxb(N * ldb, 0.f), hdb((long)N * 25 * MB * BK, 0.f);
+        for (int a = 0; a < N; ++a) {
+            for (int n = 0; n < DH; ++n)
+                for (int kk = 0; kk < DIN; ++kk)
+                    hxb[a * ldb + ((long)(kk / BK) * DH + n) * BK + kk % BK] = hx[a * ld + (long)n * DIN + kk];
+            for (int n = 0; n < DH; ++n) hxb[a * ldb + 25L * DH * BK + n] = hx[a * ld + (long)DH * DIN + n];
+            for (int m = 0; m < MB; ++m)
+                for (int kk = 0; kk < DIN; ++kk)
+                    hdb[(long)a * 25 * MB * BK + ((long)(kk / BK) * MB + m) * BK + kk % BK] =
+                        hd[((long)a * MB + m) * DIN + kk];
+        }
+        float *Xb, *Db;
+        CHECK(hipMalloc(&Xb, hxb.size() * 4));
+        CHECK(hipMalloc(&Db, hdb.size() * 4));
+        CHECK(hipMemcpy(Xb, hxb.data(), hxb.size() * 4, hipMemcpyHostToDevice));
+        CHECK(hipMemcpy(Db, hdb.data(), hdb.size() * 4, hipMemcpyHostToDevice));
+        rc |= run_ws<false, true>("warp-specialised, register, BLOCKED", Xb, ldb, Db, H, N, ref);
+        rc |= run_ws<false, false>("warp-specialised, register producers", X, ld, D, H, N, ref);
+        rc |= run_ws<false, true>("warp-specialised, register, BLOCKED", Xb, ldb, Db, H, N, ref);
+    }
     return rc;
 }

@@ -359,7 +359,8 @@ int dl_step_rows_tiled(const float *x, int32_t x_rows, const float *g, int32_t g
 /* (ABI 8) The same for every peer of an exchange in ONE launch: peer b's rows are
  * rows[row0[b] .. row0[b+1]) and its block [ceil(n_params/T)][row0[b+1] - row0[b]][T] goes to
  * outs[b].  row0 (n_peers + 1 entries, row0[0] = 0) and outs (n_peers device pointers) are HOST
- * arrays; n_peers <= 16. */
+ * arrays; n_peers <= 16.  Both tiled packs store non-temporally (the blocks are read once, by the
+ * peers' receives). */
 int dl_step_rows_tiled_peers(const float *x, int32_t x_rows, const float *g, int32_t g_rows,
                              float lr, const int32_t *rows, int32_t n_peers, const int32_t *row0,
                              float *const *outs, int64_t n_params, int32_t tile_cols,

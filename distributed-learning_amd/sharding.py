@@ -271,8 +271,14 @@ def _peer_grouped(rows, sig):
 
     if 2 < len(keys) <= 8 and runs(keys) > len(peers):
         import itertools
-        best = min(itertools.permutations(keys), key=runs)
-        keys = list(best)
+        best, best_runs = keys, runs(keys)
+        for perm in itertools.permutations(keys):
+            r = runs(perm)
+            if r < best_runs:
+                best, best_runs = list(perm), r
+                if r == len(peers):     # every peer one run: cannot do better
+                    break
+        keys = best
     return np.asarray([r for k in keys for r in groups[k]], np.int64)
 
 

@@ -453,12 +453,13 @@ def run_c3(args, dev, rank, world):
     gbs = mix_bytes / (mix_ms / 1e3) / 1e9
     if rank != 0:
         return
-    # HBM bytes per launch from the committed PMC passes of this workload (profiles/r10/c3, r09
-    # before it), and the kernel's rocprofv3 average over the same command's timed graph steps
-    c3_path = os.path.join(ROOT, "profiles", "r10", "c3" if sgd.emit == "grad" else "c3_step",
-                           "summary.json")
+    # HBM bytes per launch from the committed PMC passes of this workload (profiles/r11/c3: the
+    # round-4 build; the local-step emission's from r10), and the kernel's rocprofv3 average over
+    # the same command's timed graph steps
+    c3_path = (os.path.join(ROOT, "profiles", "r11", "c3", "summary.json") if sgd.emit == "grad"
+               else os.path.join(ROOT, "profiles", "r10", "c3_step", "summary.json"))
     if not os.path.exists(c3_path) and sgd.emit == "grad":
-        c3_path = os.path.join(ROOT, "profiles", "r09", "c3", "summary.json")
+        c3_path = os.path.join(ROOT, "profiles", "r10", "c3", "summary.json")
     prof_us = None
     try:
         with open(c3_path) as f:
@@ -470,8 +471,9 @@ def run_c3(args, dev, rank, world):
     c3_grad_traffic, c3_src = (traffic_from_profile("mlp_fused_kernel", c3_path)
                                if ann.path == "fused" and args.c3_layout == "rows"
                                else (None, None))
-    c3_mix_traffic, _ = (traffic_from_profile("mix_tile_kernel<", c3_path)
-                         if args.c3_layout == "rows" else (None, None))
+    c3_mix_traffic, _ = (traffic_from_profile(
+        kernel_name(eng.plan(deviation=True), True, True, eng.n), c3_path)
+        if args.c3_layout == "rows" else (None, None))
     grad_roof = {"bound": "mfma", "achieved": tflops, "peak": FP32_MFMA_PEAK_TFLOPS,
                  "unit": "TFLOP/s", "frac": tflops / FP32_MFMA_PEAK_TFLOPS,
                  "traffic": c3_grad_traffic, "traffic_source": c3_src if c3_grad_traffic else None,
@@ -780,9 +782,11 @@ def run_c4(args, dev, rank, world):
     if rank != 0:
         return
     achieved = bytes_per_round / (launch_ms / 1e3) / 1e9
-    # single GPU: HBM bytes per launch from the committed PMC passes (profiles/r05/c4)
+    # single GPU: HBM bytes per launch from the committed PMC passes of this kernel instance
+    # (profiles/r11/c4)
     c4_traffic, c4_src = (traffic_from_profile(
-        "mix_tile_kernel<", os.path.join(ROOT, "profiles", "r05", "c4", "summary.json"))
+        kernel_name(plan, True, True, n), os.path.join(ROOT, "profiles", "r11", "c4",
+                                                       "summary.json"))
         if world == 1 else (None, None))
     xgmi = _halo_xgmi(schemes, plan["overlap"], P, launch_ms) if world > 1 else None
     rec = {

@@ -118,3 +118,16 @@ def test_c4_ba_kernel_has_committed_traffic(bench):
         name, os.path.join(ROOT, "profiles", "r11", "c4ba", "summary.json"))
     assert traffic is not None and src.startswith("profiles/")
     assert abs(traffic / alg - 1) < 0.01
+
+
+@pytest.mark.parametrize("workload,plan,n,alg", [
+    ("c3", {"path": 1, "tile_cols": 128}, 256, 12 * 256 * 164608),
+    ("c4", {"path": 1, "tile_cols": 4}, 4096, 12 * 4096 * 2 ** 18)])
+def test_c3_c4_round_kernels_have_committed_traffic(bench, workload, plan, n, alg):
+    """The c3 and c4 lines' round kernels (full instance names from the plan) are in the round-4
+    profiles, within 1 % of the algorithmic 12 B per element."""
+    traffic, src = bench.traffic_from_profile(
+        bench.kernel_name(plan, True, True, n),
+        os.path.join(ROOT, "profiles", "r11", workload, "summary.json"))
+    assert traffic is not None and src.startswith("profiles/r11/")
+    assert abs(traffic / alg - 1) < 0.01

@@ -153,7 +153,8 @@ __global__ void __launch_bounds__(256) step_rows_tiled_kernel(
             v.z = v.z - lr * w.z;
             v.w = v.w - lr * w.w;
         }
-        op[t * os] = v;
+        typedef float f4 __attribute__((ext_vector_type(4)));
+        __builtin_nontemporal_store(f4{v.x, v.y, v.z, v.w}, reinterpret_cast<f4 *>(op + t * os));
     }
 }
 

@@ -180,6 +180,17 @@ class Mixer(object):
     # re-evaluated with the row-order two-pass deviation (dl_column_sum, as dl_mix_until does).
     _TIE_RTOL = 2e-5
 
+    # The one-image traced kernel at 4 agents per thread (mix_trace_irr_kernel: irregular graphs,
+    # or a W that is not doubly stochastic, above 2048 agents; 4 rounds per pass) keeps four
+    # agents' register heads and spills, so per round it costs more than one fused round launch
+    # once the columns outweigh the launch: 4096 agents, scripts/trace_irr_probe.py
+    # (profiles/r11/trace_irr_probe.log), traced / loop rounds per second: Barabasi-Albert 3532 /
+    # 5552 at 2^14 columns and 247 / 514 at 2^18, a row-stochastic graph 3536 / 3851 and 245 / 314
+    # (the loop's fixed cost ~65 us a round against ~31, its per-column cost 11.9 ns against 15.4:
+    # even near 9.7k columns).  Above this many columns such graphs take the round loop.
+    _TRACE_IRR4_MAX_COLS = 8192
+    _TRACE_IRR4_ROUNDS = 4
+
     # above this many agents the traced pass (mix_trace_wide_kernel: one 4-column chunk per step)
     # runs on a column-tiled copy of X: a row-major step reads a 16-byte segment of every row
     # (c4 torus, 4096 x 2^18: 486 rounds/s row-major against 2179 tiled, profiles/r10/trace4096)
@@ -211,6 +222,9 @@ class Mixer(object):
         # row-major plan has the tiled one's depth (one 4-column chunk per step above 1024 agents)
         K = min(_engine.trace_max_rounds(W, cur, nxt), self._TRACE_MAX_ROUNDS)
         if K < min(self._TRACE_MIN_ROUNDS, self._TRACE_MAX_ROUNDS):
+            return X, 0, False
+        if (W.n_rows > 2048 and K == self._TRACE_IRR4_ROUNDS and
+                Pp > self._TRACE_IRR4_MAX_COLS):
             return X, 0, False
         tiled = None
         if W.n_rows > self._TRACE_TILED_ABOVE:

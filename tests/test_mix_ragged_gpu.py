@@ -336,3 +336,38 @@ def test_mixer_traced_row_stochastic_4096(cuda, monkeypatch, times, eps):
     got = np.stack([torch.cat([p.data.reshape(-1) for p in models[i].parameters()]).cpu().numpy()
                     for i in range(n)])
     assert np.array_equal(bits(got), bits(want))
+
+
+def test_mixer_row_stochastic_4096_wide_models_take_the_round_loop(cuda, monkeypatch):
+    """The same 4096-model row-stochastic topology with 9696 parameters per model: above
+    Mixer._TRACE_IRR4_MAX_COLS columns the one-image traced kernel at 4 agents per thread is
+    slower than one fused round per launch (scripts/trace_irr_probe.py), so Mixer.mix(times, eps)
+    runs the round loop -- the reference loop's round count and bits either way."""
+    import logging
+    from oracle import mixer_ref as M
+    from distributed_learning_amd.utils.consensus_simple import Mixer
+    from distributed_learning_amd.utils.consensus_simple import mixer as mixer_mod
+    csr = dense_irregular(4096, 4, 9, 7, row_stochastic=True)
+    n = csr.n_rows
+    topo = {i: {int(csr.col[e]): float(csr.w[e]) for e in range(csr.rowptr[i], csr.rowptr[i + 1])}
+            for i in range(n)}
+    torch.manual_seed(10)
+    models = {i: torch.nn.Linear(100, 96).to(cuda) for i in range(n)}
+    X0 = np.stack([torch.cat([p.data.reshape(-1) for p in models[i].parameters()]).cpu().numpy()
+                   for i in range(n)])
+    assert X0.shape[1] > Mixer._TRACE_IRR4_MAX_COLS
+    rp, cl, w = M.topology_to_csr(topo)
+    want, want_n = M.mixer_mix(X0, rp, cl, w, times=3, eps=0.05)
+    calls = []
+    real = mixer_mod._engine.mix_rounds_trace
+
+    def traced(*a, **k):
+        calls.append(a[3])
+        return real(*a, **k)
+    monkeypatch.setattr(mixer_mod._engine, "mix_rounds_trace", traced)
+    m = Mixer(models, topo, logging.getLogger("rowstoch4096wide"))
+    assert m.mix(times=3, eps=0.05) == want_n
+    assert not calls, calls
+    got = np.stack([torch.cat([p.data.reshape(-1) for p in models[i].parameters()]).cpu().numpy()
+                    for i in range(n)])
+    assert np.array_equal(bits(got), bits(want))

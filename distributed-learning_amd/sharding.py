@@ -342,6 +342,17 @@ class DistTransport:
         self.dist.all_reduce(t, op=o, group=self.group)
         return t
 
+    def all_reduce_async(self, t, op="sum"):
+        """all_reduce_ posted without ordering the current stream after it; ``.wait()`` on the
+        returned handle does (RCCL: a stream wait, the host does not block)."""
+        o = self.dist.ReduceOp.SUM if op == "sum" else self.dist.ReduceOp.MAX
+        return self.dist.all_reduce(t, op=o, group=self.group, async_op=True)
+
+
+class _Done:
+    def wait(self):
+        pass
+
 
 class _StagedWork:
     def __init__(self, works, host, dev):
@@ -371,6 +382,10 @@ class StagedTransport(DistTransport):
         super().all_reduce_(h, op)
         t.copy_(h)
         return t
+
+    def all_reduce_async(self, t, op="sum"):
+        self.all_reduce_(t, op)
+        return _Done()
 
 
 def dist_transport(backend=None, group=None):
@@ -448,6 +463,10 @@ class _LocalEndpoint:
             acc = acc + x if op == "sum" else torch.maximum(acc, x)
         t.copy_(acc)
         return t
+
+    def all_reduce_async(self, t, op="sum"):
+        self.all_reduce_(t, op)
+        return _Done()
 
 
 class ResidentHaloTransport:
@@ -594,6 +613,9 @@ class HaloShard:
         self.Y = staggered_zeros(self._shape(plan.n_local), 1, self.device)
         self._bufs = {}
         self.mean_prev = None      # global column mean of X (lagged deviation), once known
+        # (all-reduce handle, column sums): the previous round's sums still being all-reduced;
+        # the next round's pack and exchange are posted before the mix waits for them
+        self._pending_sums = None
         # the lagged deviation needs sum(W t) = sum(t): W doubly stochastic over ALL agents.
         # One rank cannot see the global column sums, so halo_plans records them on the plan;
         # an explicit argument may only narrow that (False), never assert it.
@@ -626,7 +648,22 @@ class HaloShard:
     def load_rows(self, X):
         """Set this rank's iterate from row-major [n_local, P] rows (forgets the lagged mean)."""
         self.X.copy_(self.layout_like(X))
+        self._forget_mean()
+
+    def _forget_mean(self):
+        if self._pending_sums is not None:   # an all-reduce in flight: finish it, drop it
+            self._pending_sums[0].wait()
+            self._pending_sums = None
         self.mean_prev = None
+
+    def _mean_ready(self):
+        """Turn the previous round's all-reduced column sums into mean_prev (the current stream
+        waits for that all-reduce here, after this round's pack and exchange were posted)."""
+        if self._pending_sums is not None:
+            work, sums, mp = self._pending_sums
+            work.wait()
+            torch.div(sums, float(self.n_total), out=mp)
+            self._pending_sums = None
 
     def rows(self, A=None):
         """A resident matrix (default X) as row-major [n_local, P] (a copy when tiled)."""
@@ -704,8 +741,8 @@ class HaloShard:
         lag = None
         if deviation:
             if self.plan.n_halo == 0 or not self.doubly_stochastic:
+                self._forget_mean()
                 dev = self.deviation()
-                self.mean_prev = None
                 self._mix_all(chunks, G, lr, None)
                 return dev
             if self.mean_prev is None:
@@ -725,22 +762,25 @@ class HaloShard:
         if lag is None:
             # a round that does not publish its column sums leaves mean_prev stale (the local
             # step moved the mean): the next lagged round recomputes it
-            self.mean_prev = None
+            self._forget_mean()
             return None
         if dmax is not None:
             dev_sq, dev_max = parts[0], dmax
         else:
             dev_sq = parts.sum(0)
             dev_max = torch.sqrt(dev_sq.max()).reshape(1)
-        self.transport.all_reduce_(colsum, "sum")
-        self.mean_prev = colsum / float(self.n_total)
+        # the max first (the caller may read it now), then the column sums in the background:
+        # the next round posts its pack and exchange before its mix waits for them (_mean_ready)
         self.transport.all_reduce_(dev_max, "max")
+        mp = torch.empty(self.P, dtype=torch.float32, device=self.device)
+        self._pending_sums = (self.transport.all_reduce_async(colsum, "sum"), colsum, mp)
+        self.mean_prev = mp
         return dev_sq, dev_max
 
     def reset_deviation_lag(self):
         """Forget the lagged mean.  Callers that write ``X`` directly (loading new parameters)
         must call this before the next ``round(deviation=True)``."""
-        self.mean_prev = None
+        self._forget_mean()
 
     def _mix_all(self, chunks, G, lr, lag):
         def post(j):
@@ -749,6 +789,7 @@ class HaloShard:
             return self.transport.exchange(send, recv), halo
 
         pend = post(0)
+        self._mean_ready()
         for j, (c0, c1) in enumerate(chunks):
             nxt = post(j + 1) if j + 1 < len(chunks) else None
             works, halo = pend
@@ -768,6 +809,7 @@ class HaloShard:
         ni, nd, n = pl.n_interior, pl.n_deep, pl.n_local
         send, halo, recv = self.pack(0, 0, self.P, G, lr)
         works = self.transport.exchange(send, recv)
+        self._mean_ready()
         if ni > 0:
             self._mix(self.W_int, self.X, self._rows(self.Y, 0, ni), G, lr, None, lag)
         for w in works:

@@ -1578,13 +1578,26 @@ def main():
     del X
     plan = eng.plan(deviation=True)
 
+    # N > 1: every round's ||x_a - mean||^2 partials all-reduced over the column stripes (the
+    # global deviation: the column mean is stripe-local).  The all-reduce of a round's copy is
+    # posted asynchronously: the next round's launch does not wait for the collective (as at
+    # N = 1, where the deviation stays on the device); all of them are waited for before the
+    # timed region closes
+    pending = []
+
+    def reduce_dev():
+        if world > 1:
+            buf = eng.dev_sq.clone()     # the next round rewrites dev_sq
+            pending.append((dist.all_reduce(buf, async_op=True), buf))
+
     def step():
         eng.round(G=G, lr=lr, deviation=True)
-        if world > 1:
-            dist.all_reduce(eng.dev_sq)   # global ||x_a - mean||^2 over all column stripes
+        reduce_dev()
 
     for _ in range(args.warmup):
         step()
+    for w, _ in pending:
+        w.wait()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -1593,19 +1606,22 @@ def main():
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(args.steps)]
     t0 = time.perf_counter()
+    pending.clear()
     for i in range(args.steps):
         evs[i][0].record(stream)
         eng.round(G=G, lr=lr, deviation=True)
         evs[i][1].record(stream)
-        if world > 1:
-            dist.all_reduce(eng.dev_sq)
+        reduce_dev()
+    for w, _ in pending:
+        w.wait()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     launch_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
-    dev_max = float(torch.sqrt(eng.dev_sq.max()).item())
+    dev_sq_global = pending[-1][1] if pending else eng.dev_sq
+    dev_max = float(torch.sqrt(dev_sq_global.max()).item())
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -773,7 +773,13 @@ class HaloShard:
         # the next round posts its pack and exchange before its mix waits for them (_mean_ready)
         self.transport.all_reduce_(dev_max, "max")
         mp = torch.empty(self.P, dtype=torch.float32, device=self.device)
-        self._pending_sums = (self.transport.all_reduce_async(colsum, "sum"), colsum, mp)
+        post = getattr(self.transport, "all_reduce_async", None)   # (a transport may have none)
+        if post is None:
+            self.transport.all_reduce_(colsum, "sum")
+            work = _Done()
+        else:
+            work = post(colsum, "sum")
+        self._pending_sums = (work, colsum, mp)
         self.mean_prev = mp
         return dev_sq, dev_max
 

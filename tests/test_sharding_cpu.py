@@ -324,3 +324,61 @@ def test_lagged_mean_cleared_by_unlagged_rounds():
         ref_sq, got_sq, ref_max, got_max = out[r]
         np.testing.assert_allclose(got_sq, ref_sq, rtol=1e-5)
         assert abs(got_max - ref_max) <= 1e-5 * ref_max
+
+
+class _SyncOnly:
+    """A transport with only the synchronous API (exchange, all_reduce_): HaloShard falls back
+    to a blocking all-reduce of the column sums."""
+
+    def __init__(self, ep):
+        self.ep = ep
+
+    @property
+    def rank(self):
+        return self.ep.rank
+
+    def exchange(self, sends, recvs):
+        return self.ep.exchange(sends, recvs)
+
+    def all_reduce_(self, t, op="sum"):
+        return self.ep.all_reduce_(t, op)
+
+
+@pytest.mark.parametrize("sync_only", [False, True])
+def test_lagged_deviation_over_several_rounds(sync_only):
+    """Four lagged rounds on 2 virtual ranks: each round's deviation (of the iterate it started
+    from, against the previous round's all-reduced column sums -- posted in the background when
+    the transport can, waited for by the next round's mix) equals the exact one, and the
+    iterates equal single-process rounds, with or without the asynchronous all-reduce."""
+    import threading
+    from shard_oracle_ops import OracleOps
+    csr = torus_csr(4, 4)
+    plans = sharding.split_halo_plans(csr, sharding.torus_block_partition(4, 4, 2))
+    rng = np.random.default_rng(8)
+    P = 8
+    X = rng.standard_normal((16, P), dtype=np.float32)
+    G = rng.standard_normal((16, P), dtype=np.float32)
+    want, devs = X.copy(), []
+    for _ in range(4):
+        mean = want.mean(axis=0, dtype=np.float64)
+        devs.append(np.sqrt(((want - mean) ** 2).sum(axis=1)).max())
+        want = M.mix_once(M.sgd_step(want, G, 0.05), csr.rowptr, csr.col, csr.w)
+    tr = sharding.LocalTransport(2)
+    out = {}
+
+    def run(r):
+        ep = tr.endpoint(r)
+        sh = sharding.HaloShard(plans[r], P, "cpu", _SyncOnly(ep) if sync_only else ep,
+                                n_agents_total=16, ops=OracleOps())
+        sh.load_rows(torch.from_numpy(X[plans[r].local].copy()))
+        Gl = sh.layout_like(torch.from_numpy(G[plans[r].local].copy()))
+        got = [float(sh.round(G=Gl, lr=0.05, deviation=True)[1]) for _ in range(4)]
+        out[r] = (sh.rows().numpy().copy(), got)
+
+    ts = [threading.Thread(target=run, args=(r,)) for r in range(2)]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    for r in range(2):
+        rows, got = out[r]
+        np.testing.assert_array_equal(rows, want[plans[r].local])
+        np.testing.assert_allclose(got, devs, rtol=1e-5)

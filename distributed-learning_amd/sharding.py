@@ -200,6 +200,37 @@ class RankPlan:
         return interior, boundary
 
 
+def _boundary_from_send(plan, peers):
+    """The boundary launch of a split round with the boundary rows' stepped values read from
+    this rank's send blocks (which the pack just wrote: x - lr g rounded as the mix kernel's own
+    local step) instead of re-stepping x and g: sources [the interior window rows [n_deep,
+    n_interior), stepped from x and g | the send blocks of ``peers`` in order | the halo],
+    the entry order of every row kept.  None when some boundary row is in no send block."""
+    c, n, nd, ni = plan.csr, plan.n_local, plan.n_deep, plan.n_interior
+    where, off = {}, 0
+    for q in peers:
+        for i, r in enumerate(plan.send_to[q]):
+            where.setdefault(int(r), off + i)
+        off += len(plan.send_to[q])
+    n_adj, n_send = ni - nd, off
+    e_i = int(c.rowptr[ni])
+    src = np.asarray(c.col[e_i:], np.int64)
+    out = np.empty_like(src)
+    for k, v in enumerate(src.tolist()):
+        if v >= n:                       # halo row
+            out[k] = n_adj + n_send + (v - n)
+        elif v >= ni:                    # a boundary row: its stepped value in a send block
+            if v not in where:
+                return None
+            out[k] = n_adj + where[v]
+        elif v >= nd:                    # an interior row of the window
+            out[k] = v - nd
+        else:
+            raise ValueError("a boundary row reads a row before the window (n_deep)")
+    return Csr(np.asarray(c.rowptr[ni:]) - e_i, out, c.w[e_i:],
+               n_src=n_adj + n_send + (c.n_src - n), n_local=n_adj)
+
+
 def halo_plans(csr: Csr, parts):
     """Per-rank local CSR + halo lists for a partition of the agents of ``csr``.
 
@@ -583,6 +614,7 @@ class HaloShard:
                                  f"x {self.P} params (tile width {T})")
         self.layout = "tiled" if self.T else "rows"
         self.W = self.ops.csr(plan.csr)
+        self.W_bnd_packed, self.bnd_blocks = None, None
         if overlap == "split":
             ci, cb = plan.row_sets()
             self.W_int = self.ops.csr(ci) if plan.n_interior > 0 else None
@@ -607,11 +639,22 @@ class HaloShard:
         # per-peer halo blocks in halo_offset order (dl_mix_args.n_halo_blocks)
         self.halo_blocks = [len(plan.halo_from[q]) for q in
                             sorted(plan.halo_from, key=lambda q: plan.halo_offset[q])]
+        # column-tiled split rounds: the boundary launch reads the boundary rows' stepped values
+        # from the send blocks, which sit right before the halo blocks in one buffer
+        # (_buffers), as further halo blocks -- x and g of those rows are not read again
+        if (overlap == "split" and self.T and plan.n_deep < plan.n_interior < plan.n_local and
+                len(self.send_peers) + len(self.halo_blocks) <= 16):
+            cbp = _boundary_from_send(plan, self.send_peers)
+            if cbp is not None:
+                self.W_bnd_packed = self.ops.csr(cbp)
+                self.bnd_blocks = [len(plan.send_to[q]) for q in self.send_peers] + \
+                    self.halo_blocks
         # X, Y (and the caller's G) stream together: staggered so they do not alias in HBM
         from .engine import staggered_zeros
         self.X = staggered_zeros(self._shape(plan.n_local), 0, self.device)
         self.Y = staggered_zeros(self._shape(plan.n_local), 1, self.device)
         self._bufs = {}
+        self._both = {}   # (slot, width) -> the tiled [send blocks | halo] buffer
         self.mean_prev = None      # global column mean of X (lagged deviation), once known
         # (all-reduce handle, column sums): the previous round's sums still being all-reduced;
         # the next round's pack and exchange are posted before the mix waits for them
@@ -681,15 +724,23 @@ class HaloShard:
         key = (slot, width)
         if key not in self._bufs:
             pl = self.plan
-            send = {q: torch.empty(self._shape(len(r), width), device=self.device)
-                    for q, r in pl.send_to.items()}
             if self.T:
                 nt = width // self.T
-                halo = torch.empty(pl.n_halo * width, device=self.device)
+                # [send blocks in send_peers order | halo blocks]: one buffer, so a split
+                # round's boundary launch reads both as one table of tiled blocks
+                n_send = self.send_row0[-1]
+                both = torch.empty((n_send + pl.n_halo) * width, device=self.device)
+                send = {q: both[self.send_row0[b] * width:self.send_row0[b + 1] * width].view(
+                    nt, self.send_row0[b + 1] - self.send_row0[b], self.T)
+                    for b, q in enumerate(self.send_peers)}
+                halo = both[n_send * width:]
                 recv = {q: halo[pl.halo_offset[q] * width:
                                 (pl.halo_offset[q] + len(ids)) * width].view(nt, len(ids), self.T)
                         for q, ids in pl.halo_from.items()}
+                self._both[key] = both
             else:
+                send = {q: torch.empty(self._shape(len(r), width), device=self.device)
+                        for q, r in pl.send_to.items()}
                 halo = torch.empty(pl.n_halo, width, device=self.device)
                 recv = {q: halo[pl.halo_offset[q]:pl.halo_offset[q] + len(ids)]
                         for q, ids in pl.halo_from.items()}
@@ -709,9 +760,10 @@ class HaloShard:
             self.ops.step_rows(Xc, rows, send[q], G=Gc, lr=lr)
         return send, halo, recv
 
-    def _mix(self, W, X, Y, G, lr, halo, lag):
+    def _mix(self, W, X, Y, G, lr, halo, lag, blocks=None):
         self.ops.mix(W, X, Y, G=G, lr=lr, halo=halo, lag=lag,
-                     halo_blocks=self.halo_blocks if (self.T and halo is not None) else None)
+                     halo_blocks=(blocks or self.halo_blocks) if (self.T and halo is not None)
+                     else None)
 
     def mix_chunk(self, c0, c1, halo, G=None, lr=0.0, lag=None):
         Gc = self._cols(G, c0, c1) if G is not None else None
@@ -820,7 +872,13 @@ class HaloShard:
             self._mix(self.W_int, self.X, self._rows(self.Y, 0, ni), G, lr, None, lag)
         for w in works:
             w.wait()
-        if ni < n:
+        if ni < n and self.W_bnd_packed is not None and ni > 0:
+            # the window's interior rows stepped from x and g, the boundary rows' stepped values
+            # from the send blocks, then the halo (one buffer, bnd_blocks)
+            self._mix(self.W_bnd_packed, self._rows(self.X, nd, ni), self._rows(self.Y, ni),
+                      None if G is None else self._rows(G, nd, ni), lr,
+                      self._both[(0, self.P)], None, blocks=self.bnd_blocks)
+        elif ni < n:
             self._mix(self.W_bnd, self._rows(self.X, nd), self._rows(self.Y, ni),
                       None if G is None else self._rows(G, nd), lr, halo,
                       None if ni > 0 else lag)

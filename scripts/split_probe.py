@@ -1,7 +1,9 @@
 """Probe: a split halo round's boundary launch reading the boundary rows' stepped values from
 the send blocks (HaloShard.W_bnd_packed, the default in the column-tiled layout) against
-re-stepping them from x and g (the plain row_sets launch), one rank of the 8-, 4- and 2-way c4
+re-stepping them from x and g (the plain row_sets launch); one rank of the 8-, 4- and 2-way c4
 partition alone on one GPU (sharding.ResidentHaloTransport), alternating in one process.
+(profiles/r11/split_probe_side_stream.log has a third mode, from a since-removed build: the pack
+posted from a side stream, 435 against 420 us at one rank of 8.)
 
     python scripts/split_probe.py
 """
@@ -34,8 +36,8 @@ def main():
         packed = shard.W_bnd_packed
         res = {"packed": [], "restep": []}
         for rep in range(3):
-            for mode in ("packed", "restep"):
-                shard.W_bnd_packed = packed if mode == "packed" else None
+            for mode in res:
+                shard.W_bnd_packed = packed if mode != "restep" else None
                 for _ in range(5):
                     shard.round(G=G, lr=lr, deviation=True)
                 torch.cuda.synchronize()
@@ -48,8 +50,8 @@ def main():
                 torch.cuda.synchronize()
                 res[mode].append(float(np.median([a.elapsed_time(b) for a, b in ev])) * 1e3)
         out[world] = {k: [round(v, 1) for v in vs] for k, vs in res.items()}
-        print(f"one rank of {world}: split round us, packed {out[world]['packed']} re-stepped "
-              f"{out[world]['restep']}", flush=True)
+        print(f"one rank of {world}: split round us, " +
+              "; ".join(f"{k} {v}" for k, v in out[world].items()), flush=True)
         del shard, G
         torch.cuda.empty_cache()
     print(json.dumps(out))

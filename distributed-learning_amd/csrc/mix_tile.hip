@@ -186,7 +186,7 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
         const int st = min(max(e0 - RD * hr, 0), ntail);
         hdesc = (uint32_t)st | ((uint32_t)min(max(e1 - e0 - RD, 0), ntail - st) << 16);
     }
-    float hacc = 0.f;      // hub lane: its column's squared deviations over the tiles
+    float hacc = 0.f;      // hub lane: its row's squared deviation over the tiles (hub_dev)
     if (RD > 0) {
 #pragma unroll
         for (int i = 0; i < (NRC + 1) / 2; ++i) ri[i] = 0u;
@@ -535,6 +535,13 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
     auto pick = [](const float4 &v, int i) {
         return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w;
     };
+    // hub lanes: a tile's (dx^2 + dy^2) + (dz^2 + dw^2) over the row's four column lanes, the
+    // owner's dev_add order, so dev_sq does not depend on n_hub_rows (all four lanes get it)
+    auto hub_dev = [&](float d) {
+        float v = d * d;
+        v = v + __shfl_xor(v, 1);
+        return v + __shfl_xor(v, 2);
+    };
 
     // column mean of the tile over all agents from per-thread partial sums: thread -> wave
     // (lanes with the same c) -> LDS scratch -> every thread sums the 16 wave partials in order
@@ -631,8 +638,7 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
                                            4u * (uint32_t)hc) = hy;
                 if (DEV) {
                     if (mfi) {
-                        const float d = hy - pick(mean_t, hc);
-                        hacc += d * d;
+                        hacc += hub_dev(hy - pick(mean_t, hc));
                     } else {
                         cs.x += hc == 0 ? hy : 0.f;
                         cs.y += hc == 1 ? hy : 0.f;
@@ -675,10 +681,7 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
                     if (ag < Nr && !(RAG && ag < NH))
                         dev_add(k, RD > 0 ? mix_row_reg(k) : mix_row(ag), mean);
                 }
-                if (RAG && hub_lane) {
-                    const float d = hy - pick(mean, hc);
-                    hacc += d * d;
-                }
+                if (RAG && hub_lane) hacc += hub_dev(hy - pick(mean, hc));
             }
         } else {
             float4 cur[KV];
@@ -716,11 +719,8 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
             if (k < KV && ag < Nr && !(RAG && ag < NH))
                 a.dev_partial[(int64_t)blockIdx.x * Nr + ag] = dacc[j];
         }
-        if (RAG && NH > 0) {   // hub rows: the four column lanes' sums (lanes 4h..4h+3, one wave)
-            float v = hacc;
-            v += __shfl_xor(v, 1);
-            v += __shfl_xor(v, 2);
-            if (hub_lane && hc == 0) a.dev_partial[(int64_t)blockIdx.x * Nr + hr] = v;
+        if (RAG && NH > 0) {   // hub rows: every lane of the row holds the same sum (hub_dev)
+            if (hub_lane && hc == 0) a.dev_partial[(int64_t)blockIdx.x * Nr + hr] = hacc;
         }
         if (a.dev_max_zero != nullptr && blockIdx.x == 0 && tid == 0) *a.dev_max_zero = 0u;
     }

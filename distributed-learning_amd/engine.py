@@ -422,6 +422,8 @@ def step_rows_tiled_peers(X, rows, row0, outs, G=None, lr=0.0):
         raise ValueError("row0 must be [0, ..., rows.numel()] with one entry per peer + 1")
     xl = _tiled_ld(X, "X", X.shape[1], tiles * T, T, X.device)
     gl = _tiled_ld(G, "G", G.shape[1], tiles * T, T, X.device) if G is not None else 0
+    if G is not None and G.shape[1] < X.shape[1]:   # the kernel reads G at X's row ids
+        raise ValueError("G has fewer rows than X")
     for b, o in enumerate(outs):
         _check_tiled(o, f"outs[{b}]", (tiles, row0[b + 1] - row0[b], T), X.device)
     r0 = (ctypes.c_int32 * (n + 1))(*row0)

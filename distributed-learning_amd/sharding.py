@@ -25,6 +25,10 @@ import torch
 
 from .graph import Csr
 
+# the column-tiled pack (dl_step_rows_tiled_peers) and halo mix (dl_mix_args.n_halo_blocks) take
+# at most this many peers' blocks per launch (kMaxPackPeers / kMaxHaloBlocks, dlamd.h)
+MAX_TILED_PEERS = 16
+
 
 # ------------------------------------------------------------------ partitioning (host)
 def contiguous_partition(n, world):
@@ -612,7 +616,14 @@ class HaloShard:
             from .engine import plan_shape
             T = int(tile_cols) if tile_cols else \
                 plan_shape(plan.csr, self.P, deviation=True, tile_cols=-1)["tile_cols"]
-            if T >= 4 and self.P % T == 0:
+            # the tiled pack and the tiled halo mix take at most MAX_TILED_PEERS peers each
+            # (kMaxPackPeers / kMaxHaloBlocks in csrc); the row-major path has no such limit
+            many = max(len(plan.send_to), len(plan.halo_from)) > MAX_TILED_PEERS
+            if layout == "tiled" and many:
+                raise ValueError(f"layout='tiled' takes at most {MAX_TILED_PEERS} peers per rank "
+                                 f"(this rank sends to {len(plan.send_to)} and receives from "
+                                 f"{len(plan.halo_from)}); use layout='rows'")
+            if T >= 4 and self.P % T == 0 and not many:
                 self.T = T
             elif layout == "tiled":
                 raise ValueError(f"no column-tiled plan for {plan.n_local} + {plan.n_halo} rows "
@@ -648,7 +659,7 @@ class HaloShard:
         # from the send blocks, which sit right before the halo blocks in one buffer
         # (_buffers), as further halo blocks -- x and g of those rows are not read again
         if (overlap == "split" and self.T and plan.n_deep < plan.n_interior < plan.n_local and
-                len(self.send_peers) + len(self.halo_blocks) <= 16):
+                len(self.send_peers) + len(self.halo_blocks) <= MAX_TILED_PEERS):
             cbp = _boundary_from_send(plan, self.send_peers)
             if cbp is not None:
                 self.W_bnd_packed = self.ops.csr(cbp)
@@ -660,7 +671,7 @@ class HaloShard:
         self.Y = staggered_zeros(self._shape(plan.n_local), 1, self.device)
         self._bufs = {}
         self._both = {}   # (slot, width) -> the tiled [send blocks | halo] buffer
-        self.mean_prev = None      # global column mean of X (lagged deviation), once known
+        self._mean = None          # global column mean of X (lagged deviation), once known
         # (all-reduce handle, column sums): the previous round's sums still being all-reduced;
         # the next round's pack and exchange are posted before the mix waits for them
         self._pending_sums = None
@@ -702,7 +713,15 @@ class HaloShard:
         if self._pending_sums is not None:   # an all-reduce in flight: finish it, drop it
             self._pending_sums[0].wait()
             self._pending_sums = None
-        self.mean_prev = None
+        self._mean = None
+
+    @property
+    def mean_prev(self):
+        """The global column mean of X that the next lagged round measures against, or None.
+        Reading it finishes the previous round's column-sum all-reduce first, so it is never a
+        buffer still waiting to be filled."""
+        self._mean_ready()
+        return self._mean
 
     def _mean_ready(self):
         """Turn the previous round's all-reduced column sums into mean_prev (the current stream
@@ -802,8 +821,8 @@ class HaloShard:
                 dev = self.deviation()
                 self._mix_all(chunks, G, lr, None)
                 return dev
-            if self.mean_prev is None:
-                self.mean_prev = self._global_mean(self.X)
+            if self._mean is None:
+                self._mean = self._global_mean(self.X)
             colsum = torch.empty(self.P, dtype=torch.float32, device=self.device)
             parts = torch.empty(len(chunks), self.plan.n_local, dtype=torch.float32,
                                 device=self.device)
@@ -811,7 +830,7 @@ class HaloShard:
             # its reduce also gives the max, no torch kernels of its own
             one = split or len(chunks) == 1
             dmax = torch.empty(1, dtype=torch.float32, device=self.device) if one else None
-            lag = (self.mean_prev, colsum, parts, dmax)
+            lag = (self._mean, colsum, parts, dmax)
         if split:
             self._split_round(G, lr, None if lag is None else (lag[0], lag[1], lag[2][0], lag[3]))
         else:
@@ -837,7 +856,7 @@ class HaloShard:
         else:
             work = post(colsum, "sum")
         self._pending_sums = (work, colsum, mp)
-        self.mean_prev = mp
+        self._mean = mp       # filled by _mean_ready (next round, or the mean_prev property)
         return dev_sq, dev_max
 
     def reset_deviation_lag(self):

@@ -155,8 +155,12 @@ typedef struct dl_mix_args {
      * (<= 256; the longest ones first, as in a descending row-length order) are each folded by
      * four lanes, one column each, instead of by one lane.  A Barabasi-Albert hub's CSR row is
      * a serial fp32 fold (the reference's order); split by column it is four shorter scalar
-     * chains.  Any value gives the same bits (each column keeps its left fold); the kernel uses
-     * fewer rows when their register heads do not fit LDS. */
+     * chains.  Any value gives the same y bits (each column keeps its left fold), and with a
+     * doubly stochastic W the same dev_sq / dev_max / mean bits (the hub lanes add a tile's
+     * squared deviations in the owner's order).  With a general W (two-pass deviation) the
+     * column mean gathers the hub rows in another lane order, so dev_sq and mean may differ in
+     * the last bits across n_hub_rows values.  The kernel uses fewer rows when their register
+     * heads do not fit LDS. */
     int32_t n_hub_rows;
 } dl_mix_args;
 
@@ -221,17 +225,26 @@ int dl_mix_rounds(const dl_mix_args *args, int32_t rounds, void *workspace, size
                   dl_stream_t stream);
 
 /* `rounds` mixing rounds in one HBM pass, y = W^rounds x, with the per-round disagreement
- * trace[r] = max_a ||x_a^(r+1) - mean(x)||_2 (device float[rounds]) for r < rounds -- what
+ * trace[r] = max_a ||x_a^(r+1) - mean(x^(r+1))||_2 (device float[rounds]) for r < rounds -- what
  * Mixer.mix(times, eps) (mixer.py:18-41) evaluates after every round (_get_max_deviation,
  * :51-55, 57-66).  The caller finds the first round whose value is below eps (and >= times); if
- * it lies inside the pass it re-runs that many rounds from x with dl_mix_rounds (x is not
- * modified).  Rounds are the dl_mix_round fold (bit-identical).  The mean is the column mean of
- * x: W must be doubly stochastic (mean(W x) = mean(x)).  One agent per thread: 2 <= n_rows <=
- * 1024; no halo rows; g must be NULL; n_params % 4 == 0; 16-byte aligned operands, row-major
- * or column-tiled (tile_cols).  dl_mix_trace_plan gives the most rounds one pass can trace (32,
- * or 24 for > 512 agents of a register-cached regular graph: the per-round deviations live in
- * registers) or DL_ERR_UNSUPPORTED (two
- * column images of all agents must fit LDS).
+ * it lies inside the pass it re-runs that many rounds from x with dl_mix_rounds / dl_mix_round
+ * (x is not modified).  Rounds are the dl_mix_round fold (bit-identical).
+ *   W: any CSR.  A doubly stochastic W (W.doubly_stochastic = 1) takes the column mean of x
+ *     once (mean(W x) = mean(x)); any other W -- row-stochastic or general -- gets every round's
+ *     column mean reduced from that round's own outputs before its deviations (the one-image
+ *     kernel, "GM").  Irregular graphs above 2048 agents also take the one-image kernel.
+ *   Sizes: 2 <= n_rows <= 4096; no halo rows (n_halo == 0, n_local_src 0 or n_rows); g must be
+ *     NULL; n_params % 4 == 0; 16-byte aligned operands, row-major or column-tiled (tile_cols, a
+ *     multiple of 4 on the one-image kernel).  Rounds per pass (dl_mix_trace_plan): two-image
+ *     kernels 32, or 24 above 512 agents of a register-cached regular graph (degree 4, shared
+ *     weights), 16 / 8 above 1024 / 2048 agents; the one-image kernel 24 / 12 / 4 at <= 1024 /
+ *     <= 2048 / <= 4096 agents.
+ *   LDS: two column images of all agents beside the CSR, or else one image [n_rows] float4 plus
+ *     the CSR past each row's register head (min(min_row_nnz, 5) entries) as 8-byte pairs; when
+ *     that does not fit, a narrow image [n_rows] float2 with 6-byte tail entries.  Limits: at
+ *     most 65535 CSR entries past the register heads, and image + tail + 256 B <= 160 KiB.
+ *     Otherwise DL_ERR_UNSUPPORTED (the caller loops dl_mix_round).
  * Workspace: dl_mix_trace_workspace_bytes(n_rows, rounds). */
 int dl_mix_trace_plan(const dl_mix_args *args, int32_t *max_rounds);
 size_t dl_mix_trace_workspace_bytes(int32_t n_rows, int32_t rounds);

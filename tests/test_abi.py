@@ -261,3 +261,54 @@ def test_tiled_halo_arguments_validate_without_a_gpu():
     assert lib.dl_step_rows_tiled(1 << 20, 4, None, 0, 0.0, 1 << 22, 2, 64, 16,
                                   (1 << 20) + 16, None) == _lib.DL_ERR_INVALID   # out overlaps x
     assert b"overlaps" in lib.dl_last_error()
+
+
+@pytest.mark.parametrize("n,nnz,uni,ds,shared,minr,want", [
+    (100, 350, 0, 0, 0, 3, 24),        # row-stochastic W: one-image kernel, every round's mean
+    (1500, 5250, 0, 0, 0, 3, 12),      # ... 2 agents per thread
+    (4096, 5 * 4096, 5, 0, 0, 5, 4),   # ... 4 agents per thread, up to 4096 agents
+    (3000, 9000, 0, 1, 0, 3, 4),       # irregular doubly stochastic above 2048 agents
+    (512, 5 * 512, 5, 1, 1, 5, 32),    # two-image kernels
+    (1024, 5 * 1024, 5, 1, 1, 5, 24),  # register-cached regular graph above 512 agents
+    (2048, 5 * 2048, 5, 1, 1, 5, 16),  # wide kernel
+    (4096, 5 * 4096, 5, 1, 1, 5, 8),
+])
+def test_trace_plan_matches_the_header(n, nnz, uni, ds, shared, minr, want):
+    """dlamd.h's dl_mix_rounds_trace contract, checked on the host (no device call): any W --
+    row-stochastic ones included -- up to 4096 agents, and the rounds per pass it documents."""
+    from distributed_learning_amd import _lib
+    lib = _lib.load()
+    a = _lib.DlMixArgs()
+    a.x, a.y, a.n_params = 1 << 20, 1 << 36, 4096
+    a.ldx = a.ldy = 4096
+    a.W = _lib.DlCsr(1 << 40, 1 << 41, 1 << 42, n, nnz, uni, ds, shared, minr)
+    k = ctypes.c_int32(0)
+    _lib.check(lib.dl_mix_trace_plan(ctypes.byref(a), ctypes.byref(k)), "trace plan")
+    assert k.value == want
+
+
+def test_trace_plan_refusals_match_the_header():
+    """What the header says dl_mix_rounds_trace does not take comes back DL_ERR_UNSUPPORTED with
+    a message: more than 4096 agents, a local step (g), n_params not a multiple of 4, halo rows."""
+    from distributed_learning_amd import _lib
+    lib = _lib.load()
+
+    def plan(n=100, **kw):
+        a = _lib.DlMixArgs()
+        a.x, a.y, a.n_params = 1 << 20, 1 << 36, 4096
+        a.ldx = a.ldy = a.ldg = 4096
+        a.W = _lib.DlCsr(1 << 40, 1 << 41, 1 << 42, n, 3 * n, 0, 0, 0, 3)
+        for key, v in kw.items():
+            setattr(a, key, v)
+        k = ctypes.c_int32(0)
+        return lib.dl_mix_trace_plan(ctypes.byref(a), ctypes.byref(k)), lib.dl_last_error()
+
+    assert plan()[0] == _lib.DL_OK
+    rc, msg = plan(n=5000)
+    assert rc == _lib.DL_ERR_UNSUPPORTED and b"5000" in msg
+    rc, msg = plan(g=1 << 38)
+    assert rc == _lib.DL_ERR_UNSUPPORTED and b"g must be NULL" in msg
+    rc, msg = plan(n_params=4094, ldx=4096, ldy=4096)
+    assert rc == _lib.DL_ERR_UNSUPPORTED and b"multiple of 4" in msg
+    rc, msg = plan(n_halo=4, halo=1 << 39, ldh=4096)
+    assert rc == _lib.DL_ERR_UNSUPPORTED and b"halo" in msg

@@ -418,3 +418,74 @@ def test_split_boundary_reads_send_blocks(world):
     [t.join() for t in ts]
     for r in range(world):
         np.testing.assert_array_equal(out[r], want[plans[r].local])
+
+
+def test_many_peers_fall_back_to_rows():
+    """A rank with more peers than the column-tiled pack and halo mix take (MAX_TILED_PEERS):
+    layout='auto' keeps the row-major path, whose rounds stay bit-identical to single-process
+    rounds, and an explicit layout='tiled' is refused with a clear error."""
+    import threading
+    from shard_oracle_ops import OracleOps
+    n, world, P = 40, 20, 8                     # complete graph: every rank has 19 peers
+    edges = [(u, v) for u in range(n) for v in range(u + 1, n)]
+    csr = from_edge_weights(edges, [1.0 / n] * len(edges), list(range(n)))
+    plans = sharding.halo_plans(csr, sharding.contiguous_partition(n, world))
+    assert len(plans[0].send_to) > sharding.MAX_TILED_PEERS
+    with pytest.raises(ValueError, match="at most"):
+        sharding.HaloShard(plans[0], P, "cpu", sharding.LocalTransport(world).endpoint(0),
+                           n_agents_total=n, ops=OracleOps(), layout="tiled", tile_cols=4)
+    rng = np.random.default_rng(3)
+    X = rng.standard_normal((n, P), dtype=np.float32)
+    G = rng.standard_normal((n, P), dtype=np.float32)
+    want = X.copy()
+    for _ in range(2):
+        want = M.mix_once(M.sgd_step(want, G, 0.1), csr.rowptr, csr.col, csr.w)
+    tr = sharding.LocalTransport(world)
+    out = {}
+
+    def run(r):
+        sh = sharding.HaloShard(plans[r], P, "cpu", tr.endpoint(r), n_agents_total=n,
+                                ops=OracleOps(), layout="auto", tile_cols=4)
+        assert sh.layout == "rows"
+        sh.load_rows(torch.from_numpy(X[plans[r].local].copy()))
+        Gl = sh.layout_like(torch.from_numpy(G[plans[r].local].copy()))
+        for _ in range(2):
+            sh.round(G=Gl, lr=0.1)
+        out[r] = sh.rows().numpy().copy()
+
+    ts = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    for r in range(world):
+        np.testing.assert_array_equal(out[r], want[plans[r].local])
+
+
+def test_mean_prev_is_never_a_pending_buffer():
+    """Between lagged rounds ``mean_prev`` reads as the finished global mean of the current
+    iterate (the property completes the pending column-sum all-reduce first)."""
+    import threading
+    from shard_oracle_ops import OracleOps
+    csr = torus_csr(4, 4)
+    plans = sharding.halo_plans(csr, sharding.torus_block_partition(4, 4, 2))
+    rng = np.random.default_rng(9)
+    P = 8
+    X = rng.standard_normal((16, P), dtype=np.float32)
+    G = rng.standard_normal((16, P), dtype=np.float32)
+    want = M.mix_once(M.sgd_step(X, G, 0.1), csr.rowptr, csr.col, csr.w)
+    tr = sharding.LocalTransport(2)
+    out = {}
+
+    def run(r):
+        sh = sharding.HaloShard(plans[r], P, "cpu", tr.endpoint(r), n_agents_total=16,
+                                ops=OracleOps())
+        sh.load_rows(torch.from_numpy(X[plans[r].local].copy()))
+        Gl = sh.layout_like(torch.from_numpy(G[plans[r].local].copy()))
+        sh.round(G=Gl, lr=0.1, deviation=True)
+        out[r] = sh.mean_prev.numpy().copy()
+
+    ts = [threading.Thread(target=run, args=(r,)) for r in range(2)]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    for r in range(2):
+        np.testing.assert_allclose(out[r], want.mean(axis=0, dtype=np.float64), rtol=1e-5,
+                                   atol=1e-6)

@@ -262,24 +262,67 @@ def traffic_from_profile(kname, path=PROFILE_C2, bytes_hint=None):
     return None, None
 
 
-def cpu_baseline(csr, n, P, cols, sgd, lr):
+def host_cpu():
+    """The GPU box's host CPU: its model name (/proc/cpuinfo) and core counts, for every
+    cpu_baseline record (the numpy restatement itself runs on one of them)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    usable = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None
+    return {"host_cpu": model or platform.processor() or platform.machine(),
+            "host_cores": os.cpu_count(), "host_cores_usable": usable}
+
+
+def cpu_baseline(csr, n, P, cols, sgd, lr, n_halo=0, lagged=False):
     """Bounded sample of the same round on the host: the reference algorithm restated in numpy
-    (Mixer._mix_params_once + _get_deviation_dict, single thread) on all agents x `cols`
-    columns, scaled to the full P (columns are independent).  Also the C restatement."""
+    (Mixer._mix_params_once + _get_deviation_dict, mixer.py:43-66, single thread) on all rows x
+    `cols` columns, scaled to the full P (columns are independent).  Also the C restatement.
+
+    n_halo > 0 (one rank of an agent partition): the CSR's n output rows read n local rows and
+    n_halo halo rows (already stepped, as the exchange delivers them); lagged: the deviation is
+    the halo round's -- ||x_a - mean_prev|| of the local input rows plus their column sums --
+    instead of the exact one of the output."""
     from oracle import cref
     from oracle import mixer_ref as M
     rng = np.random.default_rng(0)
     X = rng.standard_normal((n, cols), dtype=np.float32)
     G = rng.standard_normal((n, cols), dtype=np.float32) if sgd else None
+    H = rng.standard_normal((n_halo, cols), dtype=np.float32) if n_halo else None
+    mp = rng.standard_normal(cols, dtype=np.float32) if lagged else None
+
+    def dev(T, Y):
+        if lagged:
+            np.linalg.norm(X - mp, axis=1)
+            M.column_mean(T[:n])
+        else:
+            M.deviation(Y)
 
     def np_round():
         T = M.sgd_step(X, G, lr) if sgd else X
-        Y = M.mix_once(T, csr.rowptr, csr.col, csr.w)
-        M.deviation(Y)
+        if n_halo:
+            T = np.vstack([T, H])
+        Y = M.mix_once(T, csr.rowptr, csr.col, csr.w)[:n]
+        dev(T, Y)
+
+    # the C restatement folds every source row's CSR row: halo rows get empty rows (output 0)
+    rp = csr.rowptr if not n_halo else np.concatenate(
+        [np.asarray(csr.rowptr), np.full(n_halo, csr.rowptr[-1])])
+    Xc = X if not n_halo else np.vstack([X, H])
+    Gc = G if not (n_halo and sgd) else np.vstack([G, np.zeros_like(H)])
 
     def c_round():
-        Y = cref.mix_round(X, csr.rowptr, csr.col, csr.w, G=G, lr=lr)
-        cref.deviation_sq(Y)
+        Y = cref.mix_round(Xc, rp, csr.col, csr.w, G=Gc, lr=lr)[:n]
+        if lagged:
+            cref.deviation_sq(X, mp)
+            cref.column_mean(Xc[:n])
+        else:
+            cref.deviation_sq(Y)
 
     out = {}
     for name, fn, reps in (("numpy", np_round, 3), ("c", c_round, 3)):
@@ -290,6 +333,26 @@ def cpu_baseline(csr, n, P, cols, sgd, lr):
         dt = (time.perf_counter() - t0) / reps
         out[name] = (cols / P) / dt   # full-size rounds per second
     return out
+
+
+def sample_cols(args, rows):
+    """Columns of a CPU-baseline sample with half as many elements as the c2 line's (1024 agents
+    x --cpu-cols): 10-20 s of host work whatever the row count (the restatement's per-row cost
+    grows with the rows)."""
+    return max(4, args.cpu_cols * 512 // rows // 4 * 4)
+
+
+def cpu_record(csr, n, P, cols, lr, what, n_halo=0, lagged=False):
+    """The cpu_baseline object of a mix-round line (N = 1): the numpy restatement's full-size
+    rounds/s on one host core, the C restatement beside it, the sample and the host CPU."""
+    cols = min(cols, P)
+    cb = cpu_baseline(csr, n, P, cols, True, lr, n_halo=n_halo, lagged=lagged)
+    rows = f"{n} agents" + (f" + {n_halo} halo rows" if n_halo else "")
+    return {"value": cb["numpy"], "unit": "rounds/s", "cores": 1, "kind": "port",
+            "sample": f"{rows} x {cols} of {P} columns, same graph; numpy restatement of "
+                      f"Mixer._mix_params_once + {what} after x-lr*g (mixer.py:43-66), 3 rounds "
+                      f"after one warm-up, scaled to the full column count",
+            "c_port_value": cb["c"], **host_cpu()}
 
 
 def max_over_ranks(v, world, dev):
@@ -507,7 +570,7 @@ def run_c3(args, dev, rank, world):
                "sample": f"torch CPU autograd step of ANNModel on 16 of {n} agents (B={B}), "
                          f"scaled to {n}: {tg:.3f} s; numpy restatement of the mix + deviation "
                          f"on all {n} x {P}: {tm:.3f} s",
-               "host_cores": os.cpu_count()}
+               **host_cpu()}
     rec = {
         "metric": "c3 MLP consensus SGD steps/sec (256 agents x ANNModel 164,560 params)",
         "value": world * args.steps / elapsed,
@@ -586,7 +649,9 @@ def run_gather(args, dev, rank, world):
                  "local step + mix + deviation")
         kdesc = "mix_tile_kernel register-CSR (+dev_reduce), HIP-event time"
         metric = "consensus rounds/sec, 4096 agents x 2^18 fp32 params, per-edge weights"
-        prof_dir = os.path.join(ROOT, "profiles", "r07", "peredge")
+        # the path-4 instance of this graph, profiled at the round-5 head (traffic null until
+        # that summary exists: the r07 per-edge profile was of an older kernel)
+        prof_dir = os.path.join(ROOT, "profiles", "r12", "c4gather")
     P, lr = 1 << 18, 1e-3
     gen = torch.Generator(device=dev).manual_seed(1000 + rank)
     stream = torch.cuda.current_stream(dev)
@@ -632,6 +697,9 @@ def run_gather(args, dev, rank, world):
     g_traffic, g_src = traffic_from_profile("mix_gather_kernel", prof) if prof else (None, None)
     achieved = bytes_per_round / (launch_ms / 1e3) / 1e9
     g_achieved = bytes_per_round / (g_mix[1] / 1e3) / 1e9
+    cpu = None
+    if rank == 0 and not args.no_cpu and world == 1:   # the CPU baseline is an N=1 figure
+        cpu = cpu_record(csr, n, P, sample_cols(args, n), lr, "_get_deviation_dict")
     if rank == 0:
         print(json.dumps({
             "metric": metric,
@@ -655,6 +723,7 @@ def run_gather(args, dev, rank, world):
                        "traffic": g_traffic, "traffic_source": g_src,
                        "read_amplification": (g_traffic / bytes_per_round) if g_traffic else None,
                        "grid_order": os.environ.get("DLAMD_GATHER_ORDER", "agents")},
+            "cpu_baseline": cpu,
         }), flush=True)
 
 
@@ -789,6 +858,9 @@ def run_c4(args, dev, rank, world):
                                                        "summary.json"))
         if world == 1 else (None, None))
     xgmi = _halo_xgmi(schemes, plan["overlap"], P, launch_ms) if world > 1 else None
+    cpu = None
+    if not args.no_cpu and world == 1:   # the CPU baseline is an N=1 figure
+        cpu = cpu_record(csr, n, P, sample_cols(args, n), lr, "_get_deviation_dict")
     rec = {
         "metric": "c4 torus consensus rounds/sec (4096 agents x 2^18 fp32 params)",
         "value": args.steps / elapsed,
@@ -819,7 +891,7 @@ def run_c4(args, dev, rank, world):
         "xgmi": xgmi,
         "dist": getattr(args, "dist_info", None),
         "overlap_schemes": schemes or None,
-        "cpu_baseline": None,
+        "cpu_baseline": cpu,
     }
     print(json.dumps(rec), flush=True)
 
@@ -924,6 +996,12 @@ def run_c4rank(args, dev, rank, world):
     achieved = kern["mix_bytes"] / (kern["mix_ms"] / 1e3) / 1e9
     traffic, src = traffic_from_profile(kern["kernel_instance"], os.path.join(
         ROOT, "profiles", "r11", "c4rank", "summary.json"), bytes_hint=kern["mix_bytes"])
+    cpu = None
+    if not args.no_cpu and world == 1:   # this rank's round on one host core
+        rp = sharding.split_halo_plans(csr, parts)[0]
+        cpu = cpu_record(rp.csr, rp.n_local, P, sample_cols(args, rp.n_local + rp.n_halo), lr,
+                         "the lagged deviation (||x_a - mean_prev||, column sums)",
+                         n_halo=rp.n_halo, lagged=True)
     rec = {
         "metric": f"c4 per-rank halo round, one rank of {args.rank_of} alone (64x64 torus, "
                   f"4096 agents x 2^18 fp32 params)",
@@ -950,7 +1028,7 @@ def run_c4rank(args, dev, rank, world):
                  "frac": kern["pack_bytes"] / (kern["pack_ms"] / 1e3) / 1e9 / HBM_PEAK_GBS},
         "plan": kern["plan"],
         "schemes": schemes,
-        "cpu_baseline": None,
+        "cpu_baseline": cpu,
     }
     print(json.dumps(rec), flush=True)
 
@@ -1008,6 +1086,9 @@ def run_c2halo(args, dev, rank, world):
     if rank != 0:
         return
     achieved = bytes_per_round / (launch_ms / 1e3) / 1e9
+    cpu = None
+    if not args.no_cpu and world == 1:   # the CPU baseline is an N=1 figure
+        cpu = cpu_record(csr, n, P, sample_cols(args, n), lr, "_get_deviation_dict")
     rec = {
         "metric": "c2 graph agent-partitioned consensus rounds/sec (1024 agents x 2^20 fp32 "
                   "params, random 4-regular, halo exchange)",
@@ -1038,7 +1119,7 @@ def run_c2halo(args, dev, rank, world):
         "xgmi": _halo_xgmi(schemes, plan["overlap"], P, launch_ms) if world > 1 else None,
         "dist": getattr(args, "dist_info", None),
         "overlap_schemes": schemes or None,
-        "cpu_baseline": None,
+        "cpu_baseline": cpu,
     }
     print(json.dumps(rec), flush=True)
 
@@ -1140,7 +1221,7 @@ def run_c5(args, dev, rank, world):
                "sample": f"torch CPU forward/backward + optim.SGD step of Wide_ResNet(16, 4) on 2 "
                          f"of {n} agents (B={B}), scaled to {n}: {tg:.2f} s; numpy restatement "
                          f"of the mix + deviation on all {n} x {wl.P}: {tm:.3f} s",
-               "host_cores": os.cpu_count()}
+               **host_cpu()}
     rec = {
         "metric": "c5 WRN-16-4 consensus SGD steps/sec (64 agents x 2,751,146 params)",
         "value": world * args.steps / elapsed,
@@ -1266,7 +1347,7 @@ def run_c1(args, dev, rank, world):
         cpu = {"value": c1_cpu_baseline(Xtr, ytr, topo, args.steps), "unit": "steps/s",
                "cores": 1, "kind": "port",
                "sample": f"the same {args.steps} GD iterations, synchronous numpy restatement of "
-                         "the asyncio rounds (oracle/mixer_ref.jacobi_round)"}
+                         "the asyncio rounds (oracle/mixer_ref.jacobi_round)", **host_cpu()}
     rec = {
         "metric": "c1 Titanic consensus GD iterations/sec (8 agents, ring)",
         "value": world * args.steps / elapsed,
@@ -1376,7 +1457,8 @@ def run_gossip(args, dev, rank, world):
         dt = (time.perf_counter() - t0) / 3
         cpu = {"value": (cols / P) / dt, "unit": "rounds/s", "cores": 1, "kind": "port",
                "sample": f"{n} agents x {cols} of {P} columns, 3 rounds of the numpy "
-                         "restatement of Mixer._mix_params_once, scaled to the full column count"}
+                         "restatement of Mixer._mix_params_once, scaled to the full column count",
+               **host_cpu()}
     nel = n * P
     hbm_bytes = 8 * nel                      # read X, write X' once per K rounds
     lds_bytes = K * nel * 4 * (5 + 1)        # per round: d + 1 = 5 neighbour reads + 1 write
@@ -1653,9 +1735,7 @@ def main():
                              f"numpy restatement of Mixer._mix_params_once + "
                              f"_get_deviation_dict{' after x-lr*g' if sgd else ''}, 3 rounds, "
                              f"scaled to the full column count",
-                   "c_port_value": cb["c"],
-                   "host_cpu": platform.processor() or platform.machine(),
-                   "host_cores": os.cpu_count()}
+                   "c_port_value": cb["c"], **host_cpu()}
         rec = {
             "metric": "consensus rounds/sec + achieved HBM GB/s, 1024 agents x 1M fp32 params",
             "value": value,

@@ -131,3 +131,30 @@ def test_c3_c4_round_kernels_have_committed_traffic(bench, workload, plan, n, al
         os.path.join(ROOT, "profiles", "r11", workload, "summary.json"))
     assert traffic is not None and src.startswith("profiles/r11/")
     assert abs(traffic / alg - 1) < 0.01
+
+
+def test_every_line_carries_a_cpu_baseline(bench):
+    """every BASELINE-config line reports the reference's CPU path beside it (N = 1),
+    with the host CPU named -- no runner hard-codes a null cpu_baseline."""
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    assert '"cpu_baseline": None' not in src
+    info = bench.host_cpu()
+    assert info["host_cpu"] and info["host_cores"] >= 1
+
+
+def test_cpu_record_of_a_halo_rank(bench):
+    """The c4-rank CPU baseline: one rank's local rows + halo rows through the numpy and C
+    restatements (mixer.py:43-66), the lagged deviation, scaled to the full column count."""
+    from distributed_learning_amd import sharding
+    from distributed_learning_amd.graph import best_constant_weight, from_edge_weights, torus_edges
+    edges = torus_edges(8, 8)
+    csr = from_edge_weights(edges, [best_constant_weight(edges, list(range(64)))] * len(edges),
+                            list(range(64)))
+    rp = sharding.split_halo_plans(csr, sharding.torus_block_partition(8, 8, 4))[0]
+    rec = bench.cpu_record(rp.csr, rp.n_local, 256, 64, 1e-3, "the lagged deviation",
+                           n_halo=rp.n_halo, lagged=True)
+    assert rec["value"] > 0 and rec["c_port_value"] > 0 and rec["cores"] == 1
+    assert f"{rp.n_halo} halo rows" in rec["sample"] and rec["host_cpu"]
+    whole = bench.cpu_record(csr, 64, 256, 64, 1e-3, "_get_deviation_dict")
+    assert whole["value"] > 0 and "halo" not in whole["sample"]
+    assert bench.sample_cols(type("A", (), {"cpu_cols": 1 << 18})(), 4096) == 1 << 15

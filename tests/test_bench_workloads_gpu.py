@@ -40,6 +40,8 @@ def test_c4_rank_line(cuda, bench, monkeypatch, capsys, rank_of):
     r = d["roofline"]
     assert r["bound"] == "hbm" and 0.2 < r["frac"] < 1.0, r
     assert 0.2 < d["pack"]["frac"] < 1.0, d["pack"]
+    cpu = d["cpu_baseline"]        # this rank's round on one host core, the CPU named
+    assert cpu["value"] > 0 and cpu["cores"] == 1 and cpu["host_cpu"], cpu
 
 
 def test_c4_ba_line(cuda, bench, monkeypatch, capsys):

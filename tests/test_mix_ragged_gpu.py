@@ -371,3 +371,35 @@ def test_mixer_row_stochastic_4096_wide_models_take_the_round_loop(cuda, monkeyp
     got = np.stack([torch.cat([p.data.reshape(-1) for p in models[i].parameters()]).cpu().numpy()
                     for i in range(n)])
     assert np.array_equal(bits(got), bits(want))
+
+
+@pytest.mark.parametrize("case", ["ba2_4096", "ba1_4096"])
+def test_hub_rows_keep_deviation_bits(cuda, monkeypatch, case):
+    """dlamd.h n_hub_rows: with a doubly stochastic W the fused deviation's bits (dev_sq, the
+    max and the column mean) do not depend on how many leading rows the hub lanes fold -- they
+    add a tile's squared deviations in the owner's (dx^2 + dy^2) + (dz^2 + dw^2) order."""
+    E = eng_mod()
+    csr = CASES[case][0]()
+    n, P = csr.n_rows, 2048
+    rng = np.random.default_rng(17)
+    X = rng.standard_normal((n, P), dtype=np.float32)
+    G = rng.standard_normal((n, P), dtype=np.float32)
+    out = {}
+    for hubs in ("0", "64", None):
+        if hubs is None:
+            monkeypatch.delenv("DLAMD_HUB_ROWS", raising=False)
+        else:
+            monkeypatch.setenv("DLAMD_HUB_ROWS", hubs)
+        eng = E.GossipEngine(csr, P, device=cuda, X=torch.from_numpy(X).to(cuda))
+        assert eng.plan()["path"] == 5 and eng.W.doubly_stochastic
+        mean = torch.empty(P, device=cuda)
+        eng.round(G=eng.layout_like(torch.from_numpy(G).to(cuda)), lr=0.02, deviation=True,
+                  mean=mean)
+        torch.cuda.synchronize()
+        out[hubs] = (eng.W.hub_rows, bits(eng.rows().cpu().numpy()),
+                     bits(eng.agent_dev_sq().cpu().numpy()), bits(eng.dev_max.cpu().numpy()),
+                     bits(mean.cpu().numpy()))
+    assert out["0"][0] == 0 and out[None][0] > 0
+    for hubs in ("64", None):
+        for k in range(1, 5):
+            assert np.array_equal(out[hubs][k], out["0"][k]), (hubs, k)

@@ -61,6 +61,9 @@ def parse():
                             "c4-gather", "c4-ba", "c5"])
     p.add_argument("--rank-of", type=int, default=8,
                    help="c4-rank: the GPU count of the partition whose rank 0 is measured alone")
+    p.add_argument("--halo-chunks", default="8",
+                   help="c4 / c4-rank: column chunks of the 'chunks' overlap scheme; a comma list "
+                        "(c4-rank) times each count as its own scheme")
     p.add_argument("--halo-tile-cols", type=int, default=0,
                    help="c4-rank: column-tiled width of the rank's operands (0 = the planner's)")
     p.add_argument("--irregular", default="ba2", choices=["ba2", "ba1", "deg"],
@@ -748,7 +751,8 @@ def _halo_schemes(args, dev, rank, world, csr, parts, P, lr, gen):
         # boundary-last row order for every scheme (the pack reads one contiguous run of rows)
         rp = sharding.split_halo_plans(csr, parts)[rank]
         shard = sharding.HaloShard(rp, P, dev, sharding.dist_transport(),
-                                   chunk_cols=P // 8 if name == "chunks" else None,
+                                   chunk_cols=P // int(str(args.halo_chunks).split(",")[0])
+                                   if name == "chunks" else None,
                                    n_agents_total=n, overlap="split" if name == "split" else
                                    "chunks")
         shard.X.normal_(generator=gen)
@@ -926,7 +930,11 @@ def run_c4rank(args, dev, rank, world):
     gen = torch.Generator(device=dev).manual_seed(1000 + rank)
     stream = torch.cuda.current_stream(dev)
     schemes = {}
-    names = {"whole": ("chunks", None), "chunks": ("chunks", P // 8), "split": ("split", None)}
+    counts = [int(k) for k in str(args.halo_chunks).split(",")]
+    names = {"whole": ("chunks", None)}
+    for k in counts:
+        names["chunks" if len(counts) == 1 else f"chunks{k}"] = ("chunks", P // k)
+    names["split"] = ("split", None)
     G = kern = None
     for name, (overlap, chunk) in names.items():
         # boundary-last row order for every scheme: the rows the peers read are then one

@@ -176,7 +176,7 @@ struct ParMat {
 };
 
 // one gradient value into G (plain store: non-temporal G stores, so that X' and the batch could
-// stay in the MALL, measured 3722 vs 3722 steps/s)
+// stay in the MALL, measured 3722 vs 3722 steps/s, profiles/HISTORY.md section 5)
 __device__ __forceinline__ void gstore(float *p, float v) {
     *p = v;
 }

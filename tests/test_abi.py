@@ -107,7 +107,7 @@ def test_shared_row_weights_flag_and_plan():
 @pytest.mark.parametrize("n,T", [(1024, 16), (512, 32), (256, 64), (2048, 8), (4096, 4),
                                  (64, 128), (7, 128)])
 def test_tiled_width_choice(n, T):
-    """dl_mix_plan_shape(tile_cols=-1) picks the widest tile of <= 64 KiB for
+    """dl_mix_plan_shape(tile_cols=-1) picks the widest tile of <= 64 KiB (profiles/HISTORY.md §5) for
     degree-4 graphs with one shared weight sequence."""
     from distributed_learning_amd import _lib
     lib = _lib.load()

@@ -1340,13 +1340,32 @@ def run_c1(args, dev, rank, world):
                                                          d["y"][:nt])}
     facade = None
     if rank == 0:
+        # the drop-in API (the notebook's learning_instance: host LogRegTitanic gradients, await
+        # run_round per iteration) under both facade schedules.  At convergence_eps 10 every
+        # round is one Jacobi step in lockstep, so the two return the same bits
+        # (tests/test_asyncio_gpu.py); "synchronous" is one dl_perron_round per round.
         fs = min(args.steps, 500)
-        asyncio.run(workloads.consensus_gd(topo, Xtr, ytr, 5, convergence_eps=10, device=dev))
-        t1 = time.perf_counter()
-        asyncio.run(workloads.consensus_gd(topo, Xtr, ytr, fs, convergence_eps=10, device=dev))
-        facade = {"value": fs / (time.perf_counter() - t1), "unit": "steps/s", "steps": fs,
-                  "path": "utils.consensus_asyncio facade: host gradients + dl_perron_round per "
-                          "round"}
+        facade, outs = {}, {}
+        for sched in ("synchronous", "reference"):
+            asyncio.run(workloads.consensus_gd(topo, Xtr, ytr, 5, convergence_eps=10,
+                                               device=dev, consensus=sched))
+            t1 = time.perf_counter()
+            outs[sched] = asyncio.run(workloads.consensus_gd(topo, Xtr, ytr, fs,
+                                                             convergence_eps=10, device=dev,
+                                                             consensus=sched))
+            facade[sched] = fs / (time.perf_counter() - t1)
+        facade = {"value": facade["synchronous"], "unit": "steps/s", "steps": fs,
+                  "schedule": "synchronous",
+                  "path": "utils.consensus_asyncio facade, schedule='synchronous': host "
+                          "gradients + one dl_perron_round per round (pinned staging, one "
+                          "synchronisation)",
+                  "reference_schedule_value": facade["reference"],
+                  "reference_schedule_path": "schedule='reference': the reference's asyncio "
+                                             "message protocol replayed, every agent step on the "
+                                             "device",
+                  "schedules_bit_identical": all(
+                      np.array_equal(outs["synchronous"][t], outs["reference"][t])
+                      for t in outs["reference"])}
     if rank != 0:
         return
     acc = workloads.accuracy(w[0], d["X"][:nt], d["y"][:nt])

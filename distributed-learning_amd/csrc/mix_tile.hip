@@ -246,11 +246,6 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
             }
             __syncthreads();
         }
-    } else if (MIX) {
-        for (int i = tid; i < a.n_w; i += NT) lw[i] = a.w[i];
-        for (int i = tid; i < nnz; i += NT) lcol[i] = (uint16_t)a.col[i];
-        if (!a.regular)
-            for (int i = tid; i <= Nr; i += NT) lrp[i] = (uint16_t)a.rowptr[i];
     }
     const int reg = a.regular;
 
@@ -316,6 +311,14 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
     float dacc[ND];
 #pragma unroll
     for (int k = 0; k < ND; ++k) dacc[k] = 0.f;
+    // LD (C > 1, KV <= 4): each lane instead keeps its own chunk's partial of every pass's row,
+    // and the row group's C lanes are summed ONCE, after the last tile -- no cross-lane
+    // reduction per pass and tile (log2 C ds_bpermutes per pass: at c3's 256 x 164,608 round
+    // they were 20-30 us of a 117-us launch, scripts/c3_scale_probe.py)
+    constexpr bool LD = DEV && C > 1 && KV <= 4;
+    float ldev[LD ? KV : 1];
+#pragma unroll
+    for (int k = 0; k < (LD ? KV : 1); ++k) ldev[k] = 0.f;
 
     auto prefetch = [&](int tile_id) {
         const int64_t col0 = a.col_base + (int64_t)tile_id * T;
@@ -566,6 +569,11 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
         const float dx = y.x - mean.x, dy = y.y - mean.y;
         const float dz = y.z - mean.z, dw = y.w - mean.w;
         float v = (dx * dx + dy * dy) + (dz * dz + dw * dw);
+        if constexpr (LD) {   // (k is a runtime pass index: a select per register)
+#pragma unroll
+            for (int j = 0; j < KV; ++j) ldev[j] += j == k ? v : 0.f;
+            return;
+        }
 #pragma unroll
         for (int m = 1; m < C; m <<= 1) v += __shfl_xor(v, m);  // sum over the row group
         const bool mine = (k % C) == c;
@@ -575,6 +583,15 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
 
     int tile_id = blockIdx.x;
     if (tile_id < a.n_tiles) prefetch(tile_id);
+    // the LDS CSR is staged after the first tile's loads are issued: its loads (an L2 hit for
+    // every workgroup but the first) then wait behind the tile's instead of delaying them, and
+    // the first staging barrier below publishes it
+    if (RD == 0 && MIX) {
+        for (int i = tid; i < a.n_w; i += NT) lw[i] = a.w[i];
+        for (int i = tid; i < nnz; i += NT) lcol[i] = (uint16_t)a.col[i];
+        if (!a.regular)
+            for (int i = tid; i <= Nr; i += NT) lrp[i] = (uint16_t)a.rowptr[i];
+    }
     for (; tile_id < a.n_tiles; tile_id += gridDim.x) {
         // opaque per tile: keeps LICM from hoisting one offset register per pass
         asm volatile("" : "+v"(ox), "+v"(og), "+v"(oy));
@@ -711,7 +728,17 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
         }
         if (a.dev_max_zero != nullptr && blockIdx.x == 0 && tid == 0) *a.dev_max_zero = 0u;
     }
-    if (DEV) {
+    if (LD) {
+#pragma unroll
+        for (int k = 0; k < (LD ? KV : 1); ++k) {
+            float v = ldev[k];
+#pragma unroll
+            for (int m = 1; m < C; m <<= 1) v += __shfl_xor(v, m);   // over the row group
+            const int ag = s + k * SLOTS;
+            if (c == 0 && ag < Nr) a.dev_partial[(int64_t)blockIdx.x * Nr + ag] = v;
+        }
+        if (a.dev_max_zero != nullptr && blockIdx.x == 0 && tid == 0) *a.dev_max_zero = 0u;
+    } else if (DEV) {
 #pragma unroll
         for (int j = 0; j < ND; ++j) {
             const int k = j * C + c;  // the pass this lane's slot j holds

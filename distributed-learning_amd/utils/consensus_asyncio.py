@@ -85,6 +85,7 @@ class ConsensusNetwork:
         self._pending = {}
         self._shutdown = False
         self._adj = None
+        self._rounds = {}       # (agents, values per agent, dtype) -> engine.PerronRounds
         self.last_round_iterations = 0
 
     def _debug(self, *args, **kwargs):
@@ -199,14 +200,16 @@ class ConsensusNetwork:
                 task.cancel()
             if not self.running_round and all(self.agent_new_round.values()):
                 await self._open_round()
-            self._debug(f"checking DONE: {sum(map(int, self.agent_converged.values()))}"
-                        f"/{len(self.tokens)} converged")
+            if self.debug:
+                self._debug(f"checking DONE: {sum(map(int, self.agent_converged.values()))}"
+                            f"/{len(self.tokens)} converged")
             if self.running_round and all(self.agent_converged.values()):
                 await self._close_round()
 
     def _on_agent_message(self, token, msg):
         if isinstance(msg, tuple) and msg[0] == NEW_ROUND:
-            self._debug(f'got NEW_ROUND from "{token}" with weight {msg[1]}')
+            if self.debug:
+                self._debug(f'got NEW_ROUND from "{token}" with weight {msg[1]}')
             if self.running_round:
                 self._debug(f'got NEW_ROUND from "{token}" but round is already running')
             self.agent_new_round[token] = True
@@ -273,7 +276,8 @@ class ConsensusNetwork:
             raise RuntimeError(f'agent {agent.token!r} is already in a round')
         fut = asyncio.get_running_loop().create_future()
         self._pending[agent.token] = (value, weight, fut)
-        self._debug(f'got NEW_ROUND from "{agent.token}" with weight {weight}')
+        if self.debug:
+            self._debug(f'got NEW_ROUND from "{agent.token}" with weight {weight}')
         if len(self._pending) == len(self.tokens):
             self._run_synchronous_round()
         return await fut
@@ -286,19 +290,20 @@ class ConsensusNetwork:
         shape = vals[0].shape
         dtype = np.result_type(*[v.dtype for v in vals], np.float32)
         tdt = torch.float32 if dtype == np.float32 else torch.float64
-        Y = torch.as_tensor(np.stack([v.reshape(-1) for v in vals]).astype(
-            np.float32 if tdt == torch.float32 else np.float64), device=self._dev())
-        weights = np.asarray([float(pending[t][1]) for t in self.tokens], np.float64)
+        weights = [float(pending[t][1]) for t in self.tokens]
         mean_w = sum(pending[t][1] for t in self.tokens) / len(self.tokens)
-        conv = np.asarray([self.agents[t].convergence_eps for t in self.tokens], np.float64)
-        k = _engine.perron_round(
-            Y, self._adj[0], self._adj[1], self._calc_eps(), float(conv[0]),
-            weight=torch.as_tensor(weights, device=self._dev()), mean_weight=float(mean_w),
-            max_iter=MAX_MIX_ITERATIONS,
-            conv_eps_rows=None if np.all(conv == conv[0]) else torch.as_tensor(conv,
-                                                                            device=self._dev()))
+        conv = [self.agents[t].convergence_eps for t in self.tokens]
+        # one context per value shape and dtype: pinned staging + device buffers made once, a
+        # round is one H2D copy, one launch, one D2H copy and one synchronisation
+        key = (len(vals), int(vals[0].size), tdt)
+        ctx = self._rounds.get(key)
+        if ctx is None:
+            ctx = self._rounds[key] = _engine.PerronRounds(self._adj[0], self._adj[1], key[0],
+                                                           key[1], tdt, self._dev())
+        out, k = ctx.run(vals, weights, float(mean_w), self._calc_eps(), float(conv[0]),
+                         MAX_MIX_ITERATIONS,
+                         conv_eps_rows=None if all(c == conv[0] for c in conv) else conv)
         self.last_round_iterations = k
-        out = Y.cpu().numpy()
         self._debug('===== ALL NODES CONVERGED! DONE =====')
         self.running_round = False
         for i, t in enumerate(self.tokens):
@@ -348,7 +353,8 @@ class ConsensusAgent:
         if isinstance(self.master_sockets, ConsensusNetwork):
             return await self._run_round_synchronous(value, weight)
         self.round_counter += 1
-        self._debug(f'running new round with v={value}, w={weight}')
+        if self.debug:   # (formatting numpy values costs ~10 us a call)
+            self._debug(f'running new round with v={value}, w={weight}')
         inbox, outbox = self.master_sockets
         if not self.network_ready:                                   # :212-218
             self._debug('initialized. Waiting for NETWORK_READY')
@@ -388,7 +394,8 @@ class ConsensusAgent:
                 await outbox.put(CONVERGED if c else NOT_CONVERGED)
                 flagged = c
         out = store.result(y)
-        self._debug(f'final result: {out}')
+        if self.debug:
+            self._debug(f'final result: {out}')
         return out
 
     def _master_says(self, msg):
@@ -437,10 +444,12 @@ class ConsensusAgent:
     async def _run_round_synchronous(self, value, weight):
         net = self.master_sockets
         self.round_counter += 1
-        self._debug(f'running new round with v={value}, w={weight}')
+        if self.debug:   # (formatting numpy values costs ~10 us a call)
+            self._debug(f'running new round with v={value}, w={weight}')
         if not self.network_ready:
             await net._ready.wait()
             self.network_ready = True
         res = await net._submit(self, value, weight)
-        self._debug(f'final result: {res}')
+        if self.debug:
+            self._debug(f'final result: {res}')
         return res

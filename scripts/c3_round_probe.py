@@ -29,13 +29,19 @@ def time_it(fn, reps=20, rounds=5):
 
 
 def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cases", default="", help="comma list of case-name prefixes (all if empty)")
+    ap.add_argument("--no-ceiling", action="store_true")
+    args = ap.parse_args()
     dev = torch.device("cuda", 0)
     n, P, lr = 256, 164560, 0.05
     csr, _ = bench.build_graph(n)
     alg = 12 * n * P
-    copy, triad, var = bench.copy_ceiling(dev, nbytes=256 * 164608 * 4, reps=20)
-    print(json.dumps({"case": "ceiling", "copy_GBs": copy, "triad_GBs": triad,
-                      "variants": var}), flush=True)
+    if not args.no_ceiling:
+        copy, triad, var = bench.copy_ceiling(dev, nbytes=256 * 164608 * 4, reps=20)
+        print(json.dumps({"case": "ceiling", "copy_GBs": copy, "triad_GBs": triad,
+                          "variants": var}), flush=True)
     gen = torch.Generator(device=dev).manual_seed(0)
     X0 = torch.randn(n, P, device=dev, generator=gen)
     G0 = torch.randn(n, P, device=dev, generator=gen)
@@ -54,7 +60,10 @@ def main():
         ("tiled T128", "tiled", 128, P, {}),
         ("tiled T16", "tiled", 16, P, {}),
     ]
+    want = [c for c in args.cases.split(",") if c]
     for name, layout, T, Pp, env in cases:
+        if want and not any(name.startswith(w) for w in want):
+            continue
         for k, v in env.items():
             os.environ[k] = v
         try:
@@ -64,7 +73,9 @@ def main():
             Gl = eng.layout_like(G)
             plan = eng.plan(deviation=True)
             med, lo, hi = time_it(lambda: eng.round(G=Gl, lr=lr, deviation=True))
+            nodev = time_it(lambda: eng.round(G=Gl, lr=lr, deviation=False))[0]
             print(json.dumps({"case": name, "plan": plan, "us": med * 1e3,
+                              "us_no_deviation": nodev * 1e3,
                               "spread_us": [lo * 1e3, hi * 1e3],
                               "GBs": alg / (med / 1e3) / 1e9,
                               "frac": alg / (med / 1e3) / 1e9 / 8000.0}), flush=True)

@@ -185,3 +185,25 @@ def test_titanic_grid5_10k_exact_consensus_equals_notebook(golden, cuda):
     for wt in list(w.values()) + list(w1.values()):
         np.testing.assert_allclose(wt, nb["titanic_grid5_10k_w"], atol=6e-8)
         assert workloads.accuracy(wt, d["X"][:nt], d["y"][:nt]) == nb["titanic_grid5_10k_score"]
+
+
+def test_titanic_ring8_synchronous_schedule_matches_reference(golden, cuda):
+    """BASELINE config c1 through the synchronous facade schedule (one dl_perron_round per
+    round, pinned staging, engine.PerronRounds): at convergence_eps 10 every reference round is
+    one lockstep Jacobi step, so the 4000-step reference run is reproduced as by the default
+    schedule, and 300 steps of both schedules are bit-identical."""
+    from distributed_learning_amd import workloads
+    d = golden("titanic.npz")
+    nt = int(d["n_test"])
+    topo = [(i, (i + 1) % 8) for i in range(8)]
+    X, y = d["X"][nt:], d["y"][nt:]
+    w = asyncio.run(workloads.consensus_gd(topo, X, y, int(d["ring8_steps"]), convergence_eps=10,
+                                           consensus="synchronous"))
+    got = np.stack([w[t] for t in d["ring8_tokens"].tolist()])
+    np.testing.assert_allclose(got, d["ring8_eps10_final_w"], rtol=0, atol=1e-12)
+    a = asyncio.run(workloads.consensus_gd(topo, X, y, 300, convergence_eps=10,
+                                           consensus="synchronous"))
+    b = asyncio.run(workloads.consensus_gd(topo, X, y, 300, convergence_eps=10,
+                                           consensus="reference"))
+    for t in b:
+        assert np.array_equal(a[t], b[t]), t

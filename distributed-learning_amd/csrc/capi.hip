@@ -63,6 +63,16 @@ int grid_mult() {
     return k < 1 ? 1 : (k > 8 ? 8 : k);
 }
 
+// ... for a launch of n_tiles tiles over `slots` resident workgroups: the 2x grid pays on long
+// persistent launches (c2 / c4: 128 tile passes per slot); on short ones (c3 column-tiled: 2572
+// tiles of 64 columns on 512 slots, 5 passes) the second wave of workgroups only adds its ramp:
+// 105.3 vs 110.1 us with one slot's grid (scripts/c3_round_probe.py, profiles/r12/c3_round).
+// An explicit DLAMD_GRID_MULT still applies everywhere.
+int grid_mult_for(int64_t n_tiles, int64_t slots) {
+    if (!getenv("DLAMD_GRID_MULT") && n_tiles < 16 * slots) return 1;
+    return grid_mult();
+}
+
 // Upper bound of per-workgroup partial rows any path writes.
 // MI355X Infinity Cache (MALL), shared by all XCDs
 constexpr size_t kMallBytes = (size_t)256 << 20;
@@ -216,7 +226,8 @@ bool plan_reg(const dl_mix_args *a, int c, bool want_dev, Plan *pl) {
     pl->pub.path = head > 0 ? 5 : 4;
     pl->pub.tile_cols = (int32_t)T;
     pl->pub.grid = (int32_t)balanced_grid(
-        n_tiles, (int64_t)device_cus() * bpc * (a->tile_cols > 0 ? grid_mult() : 1));
+        n_tiles, (int64_t)device_cus() * bpc *
+                     (a->tile_cols > 0 ? grid_mult_for(n_tiles, (int64_t)device_cus() * bpc) : 1));
     pl->pub.lds_bytes = (int32_t)lds;
     pl->pub.n_tiles = (int32_t)n_tiles;
     pl->pub.regular = head > 0 ? 0 : 1;
@@ -275,7 +286,9 @@ int plan_mix(const dl_mix_args *a, Plan *pl) {
         if (bpc > wg_per_cu_cap()) bpc = wg_per_cu_cap();
         if (c == 4) bpc = 1;
         const int64_t grid =
-            balanced_grid(n_tiles, (int64_t)device_cus() * (bpc < 1 ? 1 : bpc) * grid_mult());
+            balanced_grid(n_tiles, (int64_t)device_cus() * (bpc < 1 ? 1 : bpc) *
+                                   grid_mult_for(n_tiles, (int64_t)device_cus() *
+                                                              (bpc < 1 ? 1 : bpc)));
         pl->pub.path = 1;
         pl->pub.tile_cols = a->tile_cols;
         pl->pub.grid = (int32_t)grid;
@@ -1337,6 +1350,16 @@ int dl_column_sum(const float *x, int64_t ldx, int32_t n_rows, int64_t n_params,
     hipError_t e = dl::launch_column_sum(x, ldx, n_rows, n_params, colsum, 0.f,
                                          static_cast<hipStream_t>(stream));
     return e == hipSuccess ? DL_OK : hip_fail(e, "column_sum launch");
+}
+
+int dl_row_sums(const float *parts, int32_t n_parts, int32_t n_rows, float *sums, float *max_sqrt,
+                dl_stream_t stream) {
+    g_err.clear();
+    if (!parts || n_parts <= 0 || n_rows <= 0 || (!sums && !max_sqrt))
+        return fail(DL_ERR_INVALID, "dl_row_sums: bad arguments");
+    hipError_t e = dl::launch_dev_reduce(parts, n_parts, n_rows, sums, max_sqrt,
+                                         static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? DL_OK : hip_fail(e, "dev_reduce launch");
 }
 
 int dl_max_column_std(const float *x, int64_t ldx, int32_t n_rows, int64_t n_params, float *out,

@@ -316,6 +316,7 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
     // reduction per pass and tile (log2 C ds_bpermutes per pass: at c3's 256 x 164,608 round
     // they were 20-30 us of a 117-us launch, scripts/c3_scale_probe.py)
     constexpr bool LD = DEV && C > 1 && KV <= 4;
+
     float ldev[LD ? KV : 1];
 #pragma unroll
     for (int k = 0; k < (LD ? KV : 1); ++k) ldev[k] = 0.f;
@@ -388,7 +389,27 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
     // y_a = sum_e w_e * t_{col_e} for agent ag, chunk c: left fold in CSR order from +0.0
     // (mixer.py:47); reads only LDS.
     const bool wshared = a.n_w != nnz;  // weight of entry e is lw[e - e0]
+    // regular rows of 5 entries sharing one weight sequence (a degree-4 graph with uniform
+    // weights: c2, c3, c4): the 5 weights in scalar registers from row 0's CSR, the row's 5
+    // column ids and then its 5 tile values read back to back -- 6 LDS round trips a row
+    // become 2 (the same products and sums in the same order: the same bits)
+    const bool reg5 = MIX && RD == 0 && KV <= 4 && reg == 5 && wshared;
+    float w5[5];
+#pragma unroll
+    for (int e = 0; e < 5; ++e) w5[e] = reg5 ? a.w[e] : 0.f;
     auto mix_row = [&](int ag) {
+        if (reg5) {
+            uint32_t ci[5];
+#pragma unroll
+            for (int e = 0; e < 5; ++e) ci[e] = lcol[ag * 5 + e];
+            float4 v[5];
+#pragma unroll
+            for (int e = 0; e < 5; ++e) v[e] = tile[ci[e] * C + c];
+            float4 acc = zero4();
+#pragma unroll
+            for (int e = 0; e < 5; ++e) axpy4(acc, w5[e], v[e]);
+            return acc;
+        }
         int e0, e1;
         if (reg) {
             e0 = ag * reg;
@@ -546,17 +567,36 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
         return v + __shfl_xor(v, 2);
     };
 
+    // the sum of the 16 per-wave column partials scratch[wave][c], read once per wave instead
+    // of once per thread: the 64 / C lanes of a wave that share chunk c read a share of the 16
+    // partials each and add them with shuffles over the slot bits.  (Every thread reading all
+    // 16 took 16 x 16 B x 1024 = 256 KiB of LDS reads per tile, 4-16x the tile: the fused
+    // deviation cost 17-50 us of c3's ~100-us round on it, profiles/r12/c3_dev.)
+    auto wave_partials = [&]() {
+        constexpr int SW = 64 / C;                      // lanes of a wave with the same c
+        constexpr int NW = NT / 64;                     // waves (partials per chunk)
+        constexpr int PER = NW > SW ? NW / SW : 1;      // partials per lane
+        const int j = (tid & 63) / C;                   // this lane's slot in its wave
+        float4 sum = zero4();
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            const int wv = j + q * SW;
+            if (wv < NW) add4(sum, scratch[wv * C + c]);
+        }
+#pragma unroll
+        for (int m = C; m < 64; m <<= 1) sum = shfl_xor4(sum, m);
+        return sum;
+    };
+
     // column mean of the tile over all agents from per-thread partial sums: thread -> wave
-    // (lanes with the same c) -> LDS scratch -> every thread sums the 16 wave partials in order
+    // (lanes with the same c) -> LDS scratch -> the 16 wave partials (wave_partials)
     auto tile_mean = [&](float4 cs) {
 #pragma unroll
         for (int m = C; m < 64; m <<= 1) cs = shfl_xor4(cs, m);
         const int wave = tid >> 6, lane = tid & 63;
         if (lane < C) scratch[wave * C + lane] = cs;
         __syncthreads();
-        float4 mean = zero4();
-#pragma unroll
-        for (int wv = 0; wv < NT / 64; ++wv) add4(mean, scratch[wv * C + c]);
+        float4 mean = wave_partials();
         const float n = (float)Nr;
         mean.x = mean.x / n;
         mean.y = mean.y / n;
@@ -629,10 +669,17 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
                 if ((tid & 63) < C) scratch[(tid >> 6) * C + (tid & 63)] = cst;
             }
             __syncthreads();
+            // the next tile's loads go out first: they land while we mix from LDS.  Issued after
+            // the staging barrier: issuing it before (right after the staging writes) measured
+            // 10 % slower (scripts/grid_sweep.py, profiles/r05/grid_sweep_early_prefetch.log; the
+            // register-head + LDS-tail kernel, one workgroup per CU, 10 % slower too: c4-ba 327
+            // vs 361 rounds/s).  And before the tile mean's 16 scratch reads: behind them it left
+            // HBM idle for part of every tile (the fused deviation cost 17-50 us of c3's ~100-us
+            // round, profiles/r12/c3_dev)
+            if (nxt < a.n_tiles) prefetch(nxt);
             float4 mean_t = zero4();
             if (mfi || lsum) {
-#pragma unroll
-                for (int wv = 0; wv < NT / 64; ++wv) add4(mean_t, scratch[wv * C + c]);
+                mean_t = wave_partials();
                 if (lsum && s == 0) st4(a.colsum_out, col0 + 4 * c, P, FAST, mean_t);
                 const float n = (float)Nr;
                 mean_t.x = mean_t.x / n;
@@ -640,11 +687,6 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
                 mean_t.z = mean_t.z / n;
                 mean_t.w = mean_t.w / n;
             }
-            // lands while we mix from LDS.  Issued after the staging barrier: issuing it before
-            // (right after the staging writes) measured 10 % slower (scripts/grid_sweep.py,
-            // profiles/r05/grid_sweep_early_prefetch.log; the register-head + LDS-tail kernel,
-            // one workgroup per CU, 10 % slower too: c4-ba 327 vs 361 rounds/s)
-            if (nxt < a.n_tiles) prefetch(nxt);
             float *yt = const_cast<float *>(
                 reinterpret_cast<const float *>(tile_base(a.y, a.yts, tile_id)));
             float4 cs = zero4();
@@ -664,21 +706,25 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
                     }
                 }
             }
+            auto store_y = [&](int k, int ag, const float4 &acc) {
+                if (FAST) {
+                    if (a.nt_store)
+                        nt_store4(acc, at(yt, oy + (uint32_t)k * sy));
+                    else
+                        *at(yt, oy + (uint32_t)k * sy) = acc;
+                } else {
+                    st4(a.y + (int64_t)ag * a.ldy, col0 + 4 * c, P, false, acc);
+                }
+            };
             // passes stay rolled: interleaving them would hold KV accumulators at once on top
-            // of the 2*KV prefetch registers
+            // of the 2*KV prefetch registers (and mixing every pass before reducing the tile
+            // mean behind a second barrier measured 4-9 % slower on c2 / c4, profiles/r12)
 #pragma unroll 1
             for (int k = 0; k < KV; ++k) {
                 const int ag = s + k * SLOTS;
                 if (ag < Nr && !(RAG && ag < NH)) {   // (hub rows: folded by their lanes above)
                     const float4 acc = RD > 0 ? mix_row_reg(k) : mix_row(ag);
-                    if (FAST) {
-                        if (a.nt_store)
-                            nt_store4(acc, at(yt, oy + (uint32_t)k * sy));
-                        else
-                            *at(yt, oy + (uint32_t)k * sy) = acc;
-                    }
-                    else
-                        st4(a.y + (int64_t)ag * a.ldy, col0 + 4 * c, P, false, acc);
+                    store_y(k, ag, acc);
                     if (DEV) {
                         if (mfi)
                             dev_add(k, acc, mean_t);

@@ -558,6 +558,12 @@ class HipOps:
                          mean_prev=mean_prev, colsum_out=colsum, workspace=self.ws, tiled=tiled,
                          halo_blocks=halo_blocks)
 
+    def row_sums(self, parts):
+        """(sum over the rows of parts, max sqrt of it): a chunked round's deviation."""
+        sums = torch.empty(parts.shape[1], dtype=torch.float32, device=parts.device)
+        mx = torch.empty(1, dtype=torch.float32, device=parts.device)
+        return self.E.row_sums(parts, sums, mx)
+
     def column_sum(self, X):
         return self.E.column_sum(X)
 
@@ -842,6 +848,8 @@ class HaloShard:
             return None
         if dmax is not None:
             dev_sq, dev_max = parts[0], dmax
+        elif hasattr(self.ops, "row_sums"):   # chunks: one launch for the sum and the max
+            dev_sq, dev_max = self.ops.row_sums(parts)
         else:
             dev_sq = parts.sum(0)
             dev_max = torch.sqrt(dev_sq.max()).reshape(1)

@@ -339,6 +339,13 @@ int dl_from_tiled(const float *src, int32_t n_rows, int64_t n_params, int32_t ti
 int dl_column_sum(const float *x, int64_t ldx, int32_t n_rows, int64_t n_params, float *colsum,
                   dl_stream_t stream);
 
+/* sums[a] = sum_b parts[b][a] over n_parts rows of n_rows floats (fixed order, fp64), max_sqrt[0]
+ * = max_a sqrt(sums[a]); either output nullable.  The per-agent ||x_a - mean||^2 of a round run
+ * as several column chunks (each chunk's dev_sq is one row of parts), and their max -- the
+ * _get_max_deviation of mixer.py:51-55 over the whole round -- in one launch. */
+int dl_row_sums(const float *parts, int32_t n_parts, int32_t n_rows, float *sums, float *max_sqrt,
+                dl_stream_t stream);
+
 /* out[0] = max_p std_a(x[a, p]) (population std, the intent of mixer.py:82-84). */
 int dl_max_column_std(const float *x, int64_t ldx, int32_t n_rows, int64_t n_params, float *out,
                       dl_stream_t stream);

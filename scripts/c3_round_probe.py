@@ -59,6 +59,12 @@ def main():
         ("tiled T32", "tiled", 32, P, {}),
         ("tiled T128", "tiled", 128, P, {}),
         ("tiled T16", "tiled", 16, P, {}),
+        # plan path 4: the CSR in registers (DLAMD_FORCE_REG, a test knob): no LDS CSR reads
+        ("reg rows T64", "rows", None, 164608, {"DLAMD_FORCE_REG": "1",
+                                                "DLAMD_MAX_TILE_CHUNKS": "16"}),
+        ("reg tiled T64", "tiled", 64, P, {"DLAMD_FORCE_REG": "1"}),
+        ("reg tiled T64 mult1", "tiled", 64, P, {"DLAMD_FORCE_REG": "1", "DLAMD_GRID_MULT": "1"}),
+        ("reg tiled T32", "tiled", 32, P, {"DLAMD_FORCE_REG": "1"}),
     ]
     want = [c for c in args.cases.split(",") if c]
     for name, layout, T, Pp, env in cases:

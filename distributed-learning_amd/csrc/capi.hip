@@ -303,6 +303,24 @@ int plan_mix(const dl_mix_args *a, Plan *pl) {
     if ((force_reg || (prefer_reg_tail(a->W, R, 1) && !force_gather)) && R <= 65535 &&
         a->n_params % 4 == 0 && plan_reg(a, 1, want_dev, pl))
         return DL_OK;
+    // with the fused deviation, prefer the widest tile at <= 4 row passes per thread: the
+    // kernel then keeps each lane's deviation partials in registers and reduces them once per
+    // launch (mix_tile.hip LD); c3's 256 agents: 64-column tiles, 116 -> 105 us a round
+    // (scripts/c3_round_probe.py, profiles/r12/c3_round)
+    int cdev = 0;
+    if (want_dev)
+        for (int c = cmax; c >= 2; c >>= 1)
+            if ((int64_t)R * c <= 4 * (int64_t)dl::kTileThreads) {
+                cdev = c;
+                break;
+            }
+    // ... and one workgroup per CU there: c3 3704-3729 against 3589-3610 steps/s with two
+    // (same box, profiles/r12/c3_round/c3_rows_wg*.log)
+    bool one_per_cu = false;
+    if (cdev > 0 && cdev < cmax && a->n_params % (4 * cdev) == 0) {
+        cmax = cdev;
+        one_per_cu = true;
+    }
     if (csr > 0 && R <= 65535 && !force_gather) {
         for (int c = cmax; c >= 1; c >>= 1) {
             if ((int64_t)R * c > (int64_t)dl::kRowsPerThread * dl::kTileThreads) continue;
@@ -315,6 +333,7 @@ int plan_mix(const dl_mix_args *a, Plan *pl) {
             if (n_tiles > 0x7fffffff) continue;
             int bpc = (int)(dl::kLdsBytes / lds);
             if (bpc > wg_per_cu_cap()) bpc = wg_per_cu_cap();  // 1024 threads: <= 2 per CU
+            if (one_per_cu && c == cmax) bpc = 1;
             const int64_t grid =
                 balanced_grid(n_tiles, (int64_t)device_cus() * bpc);
             pl->pub.path = 1;

@@ -567,36 +567,19 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
         return v + __shfl_xor(v, 2);
     };
 
-    // the sum of the 16 per-wave column partials scratch[wave][c], read once per wave instead
-    // of once per thread: the 64 / C lanes of a wave that share chunk c read a share of the 16
-    // partials each and add them with shuffles over the slot bits.  (Every thread reading all
-    // 16 took 16 x 16 B x 1024 = 256 KiB of LDS reads per tile, 4-16x the tile: the fused
-    // deviation cost 17-50 us of c3's ~100-us round on it, profiles/r12/c3_dev.)
-    auto wave_partials = [&]() {
-        constexpr int SW = 64 / C;                      // lanes of a wave with the same c
-        constexpr int NW = NT / 64;                     // waves (partials per chunk)
-        constexpr int PER = NW > SW ? NW / SW : 1;      // partials per lane
-        const int j = (tid & 63) / C;                   // this lane's slot in its wave
-        float4 sum = zero4();
-#pragma unroll
-        for (int q = 0; q < PER; ++q) {
-            const int wv = j + q * SW;
-            if (wv < NW) add4(sum, scratch[wv * C + c]);
-        }
-#pragma unroll
-        for (int m = C; m < 64; m <<= 1) sum = shfl_xor4(sum, m);
-        return sum;
-    };
-
     // column mean of the tile over all agents from per-thread partial sums: thread -> wave
-    // (lanes with the same c) -> LDS scratch -> the 16 wave partials (wave_partials)
+    // (lanes with the same c) -> LDS scratch -> every thread sums the 16 wave partials in order
+    // (reading them once per wave and adding across the wave's slot lanes with shuffles instead
+    // measured no faster, profiles/r12)
     auto tile_mean = [&](float4 cs) {
 #pragma unroll
         for (int m = C; m < 64; m <<= 1) cs = shfl_xor4(cs, m);
         const int wave = tid >> 6, lane = tid & 63;
         if (lane < C) scratch[wave * C + lane] = cs;
         __syncthreads();
-        float4 mean = wave_partials();
+        float4 mean = zero4();
+#pragma unroll
+        for (int wv = 0; wv < NT / 64; ++wv) add4(mean, scratch[wv * C + c]);
         const float n = (float)Nr;
         mean.x = mean.x / n;
         mean.y = mean.y / n;
@@ -673,13 +656,13 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
             // the staging barrier: issuing it before (right after the staging writes) measured
             // 10 % slower (scripts/grid_sweep.py, profiles/r05/grid_sweep_early_prefetch.log; the
             // register-head + LDS-tail kernel, one workgroup per CU, 10 % slower too: c4-ba 327
-            // vs 361 rounds/s).  And before the tile mean's 16 scratch reads: behind them it left
-            // HBM idle for part of every tile (the fused deviation cost 17-50 us of c3's ~100-us
-            // round, profiles/r12/c3_dev)
+            // vs 361 rounds/s).  And ahead of the tile mean's scratch reads (-1 to -5 us on c3's
+            // 100-us round, profiles/r12)
             if (nxt < a.n_tiles) prefetch(nxt);
             float4 mean_t = zero4();
             if (mfi || lsum) {
-                mean_t = wave_partials();
+#pragma unroll
+                for (int wv = 0; wv < NT / 64; ++wv) add4(mean_t, scratch[wv * C + c]);
                 if (lsum && s == 0) st4(a.colsum_out, col0 + 4 * c, P, FAST, mean_t);
                 const float n = (float)Nr;
                 mean_t.x = mean_t.x / n;

@@ -241,7 +241,7 @@ def kernel_name(plan, sgd, dev, n_src, halo=0, lag=False):
             f"{rag}>(dl::TileArgs)")
 
 
-PROFILE_C2 = os.path.join(ROOT, "profiles", "r11", "c2", "summary.json")
+PROFILE_C2 = os.path.join(ROOT, "profiles", "r12", "c2", "summary.json")
 
 
 def traffic_from_profile(kname, path=PROFILE_C2, bytes_hint=None):
@@ -522,7 +522,7 @@ def run_c3(args, dev, rank, world):
     # HBM bytes per launch from the committed PMC passes of this workload (profiles/r11/c3: the
     # round-4 build; the local-step emission's from r10), and the kernel's rocprofv3 average over
     # the same command's timed graph steps
-    c3_path = (os.path.join(ROOT, "profiles", "r11", "c3", "summary.json") if sgd.emit == "grad"
+    c3_path = (os.path.join(ROOT, "profiles", "r12", "c3", "summary.json") if sgd.emit == "grad"
                else os.path.join(ROOT, "profiles", "r10", "c3_step", "summary.json"))
     if not os.path.exists(c3_path) and sgd.emit == "grad":
         c3_path = os.path.join(ROOT, "profiles", "r10", "c3", "summary.json")
@@ -645,7 +645,7 @@ def run_gather(args, dev, rank, world):
         kdesc = "mix_tile_kernel register head + LDS tail (+dev_reduce), HIP-event time"
         metric = "consensus rounds/sec, 4096 agents x 2^18 fp32 params, irregular graph"
         # the committed profile is of the Barabasi-Albert m = 2 graph only
-        prof_dir = os.path.join(ROOT, "profiles", "r11", "c4ba") if args.irregular == "ba2" else None
+        prof_dir = os.path.join(ROOT, "profiles", "r12", "c4ba") if args.irregular == "ba2" else None
     else:
         csr, n = per_edge_torus(64, 64)
         gname = ("c4-gather: 64x64 torus, per-edge weights (best constant x U[0.9, 1.1]), fused "
@@ -858,7 +858,7 @@ def run_c4(args, dev, rank, world):
     # single GPU: HBM bytes per launch from the committed PMC passes of this kernel instance
     # (profiles/r11/c4)
     c4_traffic, c4_src = (traffic_from_profile(
-        kernel_name(plan, True, True, n), os.path.join(ROOT, "profiles", "r11", "c4",
+        kernel_name(plan, True, True, n), os.path.join(ROOT, "profiles", "r12", "c4",
                                                        "summary.json"))
         if world == 1 else (None, None))
     xgmi = _halo_xgmi(schemes, plan["overlap"], P, launch_ms) if world > 1 else None
@@ -1003,7 +1003,7 @@ def run_c4rank(args, dev, rank, world):
         v["round_hbm_frac"] = v["round_hbm_bytes"] / (v["round_ms"] / 1e3) / 1e9 / HBM_PEAK_GBS
     achieved = kern["mix_bytes"] / (kern["mix_ms"] / 1e3) / 1e9
     traffic, src = traffic_from_profile(kern["kernel_instance"], os.path.join(
-        ROOT, "profiles", "r11", "c4rank", "summary.json"), bytes_hint=kern["mix_bytes"])
+        ROOT, "profiles", "r12", "c4rank", "summary.json"), bytes_hint=kern["mix_bytes"])
     cpu = None
     if not args.no_cpu and world == 1:   # this rank's round on one host core
         rp = sharding.split_halo_plans(csr, parts)[0]

@@ -87,11 +87,34 @@ __device__ __forceinline__ void add4(float4 &a, float4 b) {
     a.w = a.w + b.w;
 }
 
+// v + v[lane ^ m] across the wave (m a power of two, a compile-time constant after unrolling),
+// without the LDS unit where gfx950 has a register path: xor 1 / 2 are DPP quad permutes, xor
+// 16 / 32 the v_permlane16/32_swap pair (their two results are {v, partner} per lane, in some
+// order: the sum is the same IEEE add); xor 4 / 8 stay ds_bpermute.  Bit-identical to
+// v + __shfl_xor(v, m) (a + b == b + a).
+__device__ __forceinline__ float xor_add(float v, int m) {
+    if (m == 1)
+        return v + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true));
+    if (m == 2)
+        return v + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, true));
+    if (m == 16) {
+        const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v),
+                                                        false, false);
+        return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    }
+    if (m == 32) {
+        const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v),
+                                                        false, false);
+        return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    }
+    return v + __shfl_xor(v, m);
+}
+
 __device__ __forceinline__ float4 shfl_xor4(float4 v, int m) {
-    v.x += __shfl_xor(v.x, m);
-    v.y += __shfl_xor(v.y, m);
-    v.z += __shfl_xor(v.z, m);
-    v.w += __shfl_xor(v.w, m);
+    v.x = xor_add(v.x, m);
+    v.y = xor_add(v.y, m);
+    v.z = xor_add(v.z, m);
+    v.w = xor_add(v.w, m);
     return v;
 }
 
@@ -563,8 +586,8 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
     // owner's dev_add order, so dev_sq does not depend on n_hub_rows (all four lanes get it)
     auto hub_dev = [&](float d) {
         float v = d * d;
-        v = v + __shfl_xor(v, 1);
-        return v + __shfl_xor(v, 2);
+        v = xor_add(v, 1);
+        return xor_add(v, 2);
     };
 
     // column mean of the tile over all agents from per-thread partial sums: thread -> wave
@@ -598,7 +621,7 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
             return;
         }
 #pragma unroll
-        for (int m = 1; m < C; m <<= 1) v += __shfl_xor(v, m);  // sum over the row group
+        for (int m = 1; m < C; m <<= 1) v = xor_add(v, m);  // sum over the row group
         const bool mine = (k % C) == c;
 #pragma unroll
         for (int j = 0; j < ND; ++j) dacc[j] += (mine && j == k / C) ? v : 0.f;
@@ -751,7 +774,7 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
         for (int k = 0; k < (LAG ? KV : 1); ++k) {
             float v = lacc[k];
 #pragma unroll
-            for (int m = 1; m < C; m <<= 1) v += __shfl_xor(v, m);   // over the row group
+            for (int m = 1; m < C; m <<= 1) v = xor_add(v, m);   // over the row group
             const int ag = s + k * SLOTS;   // a local source row
             if (c == 0 && ag < NL) a.dev_partial[(int64_t)blockIdx.x * NL + ag] = v;
         }
@@ -762,7 +785,7 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
         for (int k = 0; k < (LD ? KV : 1); ++k) {
             float v = ldev[k];
 #pragma unroll
-            for (int m = 1; m < C; m <<= 1) v += __shfl_xor(v, m);   // over the row group
+            for (int m = 1; m < C; m <<= 1) v = xor_add(v, m);   // over the row group
             const int ag = s + k * SLOTS;
             if (c == 0 && ag < Nr) a.dev_partial[(int64_t)blockIdx.x * Nr + ag] = v;
         }

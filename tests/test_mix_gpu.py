@@ -504,3 +504,68 @@ def test_tcp_run_once_round(cuda, edges, w):
     want = M.tcp_run_once(edges, w, {k: X[i] for i, k in enumerate(csr.keys)})
     np.testing.assert_allclose(got, np.stack([want[k] for k in csr.keys]), rtol=1e-5, atol=1e-6)
 
+
+
+def shared_weight_graph(n, seed, doubly=True):
+    """A random 4-regular graph whose every row carries the same weight sequence (CSR
+    shared_row_weights: the tile kernel's unrolled degree-5 rows with the weights in scalar
+    registers).  doubly: the best-constant weights (W doubly stochastic, the tile mean taken
+    from the staged inputs); else one asymmetric sequence whose columns do not sum to 1 (the
+    two-pass tile mean)."""
+    from distributed_learning_amd.graph import Csr, random_regular_edges
+    edges = random_regular_edges(4, n, seed=seed)
+    nbrs = [[] for _ in range(n)]
+    for u, v in edges:
+        nbrs[u].append(v)
+        nbrs[v].append(u)
+    seq = [0.2] * 5 if doubly else [0.4, 0.3, 0.1, 0.15, 0.05]
+    rp, cl, w = [0], [], []
+    for a in range(n):
+        cl += [a] + nbrs[a]
+        w += seq
+        rp.append(len(cl))
+    csr = Csr(rp, cl, w, keys=list(range(n)))
+    assert csr.shared_row_weights and csr.uniform_row_nnz == 5
+    assert bool(csr.doubly_stochastic) == doubly
+    return csr
+
+
+@pytest.mark.parametrize("T", [4, 8, 16, 32, 64, 128])
+@pytest.mark.parametrize("doubly", [True, False])
+def test_tiled_widths_shared_weights(cuda, T, doubly):
+    """Every column-tiled width (C = 1 .. 32 float4 chunks per row: the cross-lane sums on DPP,
+    v_permlane16/32_swap and ds_bpermute, the per-lane deviation partials at <= 4 passes per
+    thread) with the fused step and deviation on a shared-weight degree-4 graph: bit-exact
+    rounds, deviation and mean within tolerance, both tile-mean paths."""
+    E = eng_mod()
+    n, P = 256, 128 * 24 + 64
+    csr = shared_weight_graph(n, seed=T, doubly=doubly)
+    rng = np.random.default_rng(T + 7 * doubly)
+    X = rng.standard_normal((n, P), dtype=np.float32)
+    G = rng.standard_normal((n, P), dtype=np.float32)
+    eng = E.GossipEngine(csr, P, device=cuda, X=torch.from_numpy(X).to(cuda), layout="tiled",
+                         tile_cols=T)
+    plan = eng.plan()
+    assert plan["path"] == 1 and plan["tile_cols"] == T, plan
+    mean = torch.empty(P, device=cuda)
+    eng.round(G=eng.layout_like(torch.from_numpy(G).to(cuda)), lr=0.03, deviation=True,
+              mean=mean)
+    torch.cuda.synchronize()
+    want = cref.mix_round(X, csr.rowptr, csr.col, csr.w, G=G, lr=0.03)
+    assert np.array_equal(bits(eng.rows().cpu().numpy()), bits(want))
+    check_dev(want, eng.dev_sq.cpu().numpy(), float(eng.dev_max.item()), mean.cpu().numpy())
+
+
+def test_row_sums(cuda):
+    """dl_row_sums (a chunked halo round's deviation and its max in one launch): column sums of
+    the partial rows in a fixed order, max of their square roots."""
+    E = eng_mod()
+    rng = np.random.default_rng(5)
+    parts = torch.from_numpy(rng.random((3, 1000), dtype=np.float32)).to(cuda)
+    sums = torch.empty(1000, device=cuda)
+    mx = torch.empty(1, device=cuda)
+    E.row_sums(parts, sums, mx)
+    torch.cuda.synchronize()
+    want = parts.cpu().double().sum(0).float().numpy()
+    np.testing.assert_allclose(sums.cpu().numpy(), want, rtol=1e-6)
+    assert float(mx.item()) == pytest.approx(float(np.sqrt(want).max()), rel=1e-6)

@@ -119,15 +119,19 @@ __global__ void __launch_bounds__(256) step_rows_tiled_kernel(
     const float4 *xp = x + r * tcq + cc;
     const float4 *gp = g ? g + r * tcq + cc : nullptr;
     float4 *op = ob + (int64_t)(i - r0) * tcq + cc;
+    // each workgroup walks ONE contiguous run of tiles, U consecutive tiles' loads in flight:
+    // its reads and writes stay inside a few MB instead of striding the whole matrix (a lane's
+    // loads were gridDim.y tiles = 38 MB apart at c4's rank of 8)
     constexpr int U = 4;
-    int64_t t = blockIdx.y;
-    const int64_t gy = gridDim.y;
-    for (; t + (U - 1) * gy < n_tiles; t += U * gy) {
+    const int64_t per = (n_tiles + gridDim.y - 1) / gridDim.y;
+    int64_t t = (int64_t)blockIdx.y * per;
+    const int64_t t_end = t + per < n_tiles ? t + per : n_tiles;
+    for (; t + (U - 1) < t_end; t += U) {
         float4 v[U], w[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            v[u] = xp[(t + u * gy) * xs];
-            if (gp) w[u] = gp[(t + u * gy) * gs];
+            v[u] = xp[(t + u) * xs];
+            if (gp) w[u] = gp[(t + u) * gs];
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -141,10 +145,10 @@ __global__ void __launch_bounds__(256) step_rows_tiled_kernel(
             // alone 52.9 -> 47.9 us at the c4 rank-of-8 shape, scripts/pack_probe.hip)
             typedef float f4 __attribute__((ext_vector_type(4)));
             __builtin_nontemporal_store(f4{v[u].x, v[u].y, v[u].z, v[u].w},
-                                        reinterpret_cast<f4 *>(op + (t + u * gy) * os));
+                                        reinterpret_cast<f4 *>(op + (t + u) * os));
         }
     }
-    for (; t < n_tiles; t += gy) {
+    for (; t < t_end; ++t) {
         float4 v = xp[t * xs];
         if (gp) {
             const float4 w = gp[t * gs];

@@ -6,6 +6,8 @@
 //   Perron / asyncio Jacobi round (consensus_asyncio.py:231-310), fp32 and fp64
 #include "dl_internal.h"
 
+#include <cstdlib>
+
 namespace dl {
 namespace {
 
@@ -88,19 +90,21 @@ __global__ void __launch_bounds__(256) step_rows_kernel(const float *__restrict_
     }
 }
 
-// Column-tiled form, every peer of a halo exchange in one launch: thread (i, cc) of the x
-// dimension owns float4 chunk cc of selected row i (rows of all peers concatenated, peer b's in
-// [row0[b], row0[b+1])) in every tile t = blockIdx.y, blockIdx.y + gridDim.y, ... (peer, row
-// and offsets computed once; no division in the loop), four tiles' loads in flight before
-// their stores.  x / g tiles are [x_rows][T] / [g_rows][T] blocks; peer b's output is its own
-// contiguous block [n_tiles][n_b][T] (one RCCL send buffer).  The reads are T*4-byte row
-// segments.
+// Column-tiled form, every peer of a halo exchange in one launch.  The selected rows of all peers
+// are concatenated (peer b's in [row0[b], row0[b+1])); one tile's work is L = n_sel * T/4 float4
+// lanes (row i, chunk cc).  A workgroup holds `sub` lane groups of lp >= L threads (lp = L
+// rounded up to a wave when L < 256, so a 96-row exchange keeps 3 of 4 lanes busy instead of
+// 3 of 8), group s walking tiles t0 + s, t0 + s + sub, ... of the workgroup's ONE contiguous run
+// of tiles, four tiles' loads in flight before their stores (peer, row and offsets computed
+// once; no division in the loop).  x / g tiles are [x_rows][T] / [g_rows][T] blocks; peer b's
+// output is its own contiguous block [n_tiles][n_b][T] (one RCCL send buffer).
 __global__ void __launch_bounds__(256) step_rows_tiled_kernel(
     const float4 *__restrict__ x, int x_rows, const float4 *__restrict__ g, int g_rows, float lr,
-    const int32_t *__restrict__ rows, PackPeers pp, int64_t n_tiles, int tcq) {
-    const int q = blockIdx.x * 256 + threadIdx.x;
+    const int32_t *__restrict__ rows, PackPeers pp, int64_t n_tiles, int tcq, int lp, int sub) {
+    const int s = threadIdx.x / lp;
+    const int q = blockIdx.x * lp + (threadIdx.x - s * lp);
     const int n_sel = pp.row0[pp.n];
-    if (q >= n_sel * tcq) return;
+    if (s >= sub || q >= n_sel * tcq) return;
     const int i = q / tcq, cc = q - (q / tcq) * tcq;
     // this row's peer: an unrolled select over the <= kMaxPackPeers table (kernel arguments
     // are not indexed dynamically)
@@ -119,19 +123,20 @@ __global__ void __launch_bounds__(256) step_rows_tiled_kernel(
     const float4 *xp = x + r * tcq + cc;
     const float4 *gp = g ? g + r * tcq + cc : nullptr;
     float4 *op = ob + (int64_t)(i - r0) * tcq + cc;
-    // each workgroup walks ONE contiguous run of tiles, U consecutive tiles' loads in flight:
-    // its reads and writes stay inside a few MB instead of striding the whole matrix (a lane's
-    // loads were gridDim.y tiles = 38 MB apart at c4's rank of 8)
+    // one contiguous run of tiles per workgroup: its reads and writes stay inside a few MB
+    // instead of striding the whole matrix (pack 104 -> 96 us at c4's rank of 8)
     constexpr int U = 4;
     const int64_t per = (n_tiles + gridDim.y - 1) / gridDim.y;
-    int64_t t = (int64_t)blockIdx.y * per;
-    const int64_t t_end = t + per < n_tiles ? t + per : n_tiles;
-    for (; t + (U - 1) < t_end; t += U) {
+    const int64_t t0 = (int64_t)blockIdx.y * per;
+    const int64_t t_end = t0 + per < n_tiles ? t0 + per : n_tiles;
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    int64_t t = t0 + s;
+    for (; t + (U - 1) * sub < t_end; t += U * sub) {
         float4 v[U], w[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            v[u] = xp[(t + u) * xs];
-            if (gp) w[u] = gp[(t + u) * gs];
+            v[u] = xp[(t + u * sub) * xs];
+            if (gp) w[u] = gp[(t + u * sub) * gs];
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -143,12 +148,11 @@ __global__ void __launch_bounds__(256) step_rows_tiled_kernel(
             }
             // non-temporal: the send blocks are read once, by the peers' RCCL receives (the pack
             // alone 52.9 -> 47.9 us at the c4 rank-of-8 shape, scripts/pack_probe.hip)
-            typedef float f4 __attribute__((ext_vector_type(4)));
             __builtin_nontemporal_store(f4{v[u].x, v[u].y, v[u].z, v[u].w},
-                                        reinterpret_cast<f4 *>(op + (t + u) * os));
+                                        reinterpret_cast<f4 *>(op + (t + u * sub) * os));
         }
     }
-    for (; t < t_end; ++t) {
+    for (; t < t_end; t += sub) {
         float4 v = xp[t * xs];
         if (gp) {
             const float4 w = gp[t * gs];
@@ -157,7 +161,6 @@ __global__ void __launch_bounds__(256) step_rows_tiled_kernel(
             v.z = v.z - lr * w.z;
             v.w = v.w - lr * w.w;
         }
-        typedef float f4 __attribute__((ext_vector_type(4)));
         __builtin_nontemporal_store(f4{v.x, v.y, v.z, v.w}, reinterpret_cast<f4 *>(op + t * os));
     }
 }
@@ -416,15 +419,23 @@ hipError_t launch_step_rows_tiled(const float *x, int x_rows, const float *g, in
     const int64_t lanes = (int64_t)pp.row0[pp.n] * tcq;
     const int64_t bx = (lanes + 255) / 256;
     if (bx > 65535 || pp.n < 1 || pp.n > kMaxPackPeers) return hipErrorInvalidValue;
-    // about 2048 resident threads per CU over 256 CUs; each thread walks >= 4 tiles
+    // lane groups: one tile's lanes rounded up to a wave, as many groups as fit 256 threads
+    const int lp = lanes >= 256 ? 256 : (int)((lanes + 63) / 64 * 64);
+    const int sub = 256 / lp;
+    // about 2048 resident threads per CU over 256 CUs; each lane group walks >= 4 tiles
     int64_t gy = (256 * 2048) / (bx * 256);
-    const int64_t gmax = (n_tiles + 3) / 4;
+    // DLAMD_PACK_RUN=n (a measurement knob): runs of n tiles per workgroup instead
+    if (const char *pr = getenv("DLAMD_PACK_RUN")) {
+        const int64_t run = atoi(pr);
+        if (run > 0) gy = (n_tiles + run - 1) / run;
+    }
+    const int64_t gmax = (n_tiles + 4 * sub - 1) / (4 * sub);
     if (gy > gmax) gy = gmax;
     if (gy > 65535) gy = 65535;
     if (gy < 1) gy = 1;
     hipLaunchKernelGGL(step_rows_tiled_kernel, dim3((unsigned)bx, (unsigned)gy), dim3(256), 0, s,
                        reinterpret_cast<const float4 *>(x), x_rows,
-                       reinterpret_cast<const float4 *>(g), g_rows, lr, rows, pp, n_tiles, tcq);
+                       reinterpret_cast<const float4 *>(g), g_rows, lr, rows, pp, n_tiles, tcq, lp, sub);
     return hipGetLastError();
 }
 

@@ -504,7 +504,7 @@ dl::TileArgs tile_args(const dl_mix_args *a) {
         const size_t y_bytes = (size_t)a->W.n_rows * (size_t)a->n_params * 4;
         t.nt_store = nt ? (nt[0] == '0' ? 0 : 1) : (y_bytes > kMallBytes ? 1 : 0);
         const char *ntl = getenv("DLAMD_NT_LOAD");
-        t.nt_load = (ntl && ntl[0] == '0') ? 0 : 1;
+        t.nt_load = !ntl ? 3 : ntl[0] == '0' ? 0 : ntl[0] == 'x' ? 1 : ntl[0] == 'g' ? 2 : 3;
     }
     t.n_params = a->n_params;
     t.lr = a->lr;

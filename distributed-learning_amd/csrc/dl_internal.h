@@ -33,7 +33,7 @@ struct TileArgs {
     int32_t n_w;      // weights staged in LDS: nnz, or `regular` when every row shares row 0's
     int32_t mean_from_inputs;  // 1: W doubly stochastic -> tile mean taken from the staged t
     int32_t nt_store;          // 1: non-temporal stores of y (FAST path)
-    int32_t nt_load;           // 1: non-temporal loads of x, g (FAST path)
+    int32_t nt_load;           // non-temporal loads (FAST path): bit 0 x / halo, bit 1 g
     int64_t n_params;
     int32_t n_tiles;
     int64_t col_base; // first column of tile 0

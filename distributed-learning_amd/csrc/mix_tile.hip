@@ -16,6 +16,7 @@
 // which reproduces the reference's left fold bit for bit.
 #include <mutex>
 #include <set>
+#include <type_traits>
 #include <utility>
 
 #include "dl_internal.h"
@@ -368,32 +369,36 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
                 const char *bx = loc || !ok ? xt : ht;
                 const uint32_t o1 = loc ? ox + k * sx : ok ? oh : 16u * c;
                 const float4 *p1 = reinterpret_cast<const float4 *>(bx + o1);
-                px[k] = a.nt_load ? nt_load4(p1) : *p1;
+                px[k] = (a.nt_load & 1) ? nt_load4(p1) : *p1;
                 if (SGD) {
                     const float4 *p2 =
                         reinterpret_cast<const float4 *>(gt + (loc ? og + k * sg : 16u * c));
-                    pg[k] = a.nt_load ? nt_load4(p2) : *p2;
+                    pg[k] = (a.nt_load & 2) ? nt_load4(p2) : *p2;
                 }
             }
         } else if (FAST) {
             const float *xt = reinterpret_cast<const float *>(tile_base(a.x, a.xts, tile_id));
             const float *gt =
                 SGD ? reinterpret_cast<const float *>(tile_base(a.g, a.gts, tile_id)) : nullptr;
-            if (a.nt_load) {
+            // one straight-line loop per load policy (bit 0: x non-temporal, bit 1: g)
+            auto loads = [&](auto ntx, auto ntg) {
 #pragma unroll
                 for (int k = 0; k < KV; ++k) {
                     const bool ok = s + k * SLOTS < R;
-                    px[k] = nt_load4(at(xt, ok ? ox + k * sx : 16u * c));
-                    if (SGD) pg[k] = nt_load4(at(gt, ok ? og + k * sg : 16u * c));
+                    const float4 *p1 = at(xt, ok ? ox + k * sx : 16u * c);
+                    px[k] = decltype(ntx)::value ? nt_load4(p1) : *p1;
+                    if (SGD) {
+                        const float4 *p2 = at(gt, ok ? og + k * sg : 16u * c);
+                        pg[k] = decltype(ntg)::value ? nt_load4(p2) : *p2;
+                    }
                 }
-            } else {
-#pragma unroll
-                for (int k = 0; k < KV; ++k) {
-                    const bool ok = s + k * SLOTS < R;
-                    px[k] = *at(xt, ok ? ox + k * sx : 16u * c);
-                    if (SGD) pg[k] = *at(gt, ok ? og + k * sg : 16u * c);
-                }
-            }
+            };
+            using T1 = std::true_type;
+            using F0 = std::false_type;
+            if (a.nt_load == 3) loads(T1{}, T1{});
+            else if (a.nt_load == 1) loads(T1{}, F0{});
+            else if (a.nt_load == 2) loads(F0{}, T1{});
+            else loads(F0{}, F0{});
         } else {
             const int64_t cc = col0 + 4 * c;
 #pragma unroll

@@ -33,6 +33,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--cases", default="", help="comma list of case-name prefixes (all if empty)")
     ap.add_argument("--no-ceiling", action="store_true")
+    ap.add_argument("--pad-cols", default="", help="comma list of padded row widths: the "
+                    "default row-major plan at each (tile-count quantisation)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     n, P, lr = 256, 164560, 0.05
@@ -66,6 +68,8 @@ def main():
         ("reg tiled T64 mult1", "tiled", 64, P, {"DLAMD_FORCE_REG": "1", "DLAMD_GRID_MULT": "1"}),
         ("reg tiled T32", "tiled", 32, P, {"DLAMD_FORCE_REG": "1"}),
     ]
+    for w in [int(v) for v in args.pad_cols.split(",") if v]:
+        cases.append((f"rows pad{w}", "rows", None, w, {}))
     want = [c for c in args.cases.split(",") if c]
     for name, layout, T, Pp, env in cases:
         if want and not any(name.startswith(w) for w in want):
@@ -73,8 +77,8 @@ def main():
         for k, v in env.items():
             os.environ[k] = v
         try:
-            X = torch.nn.functional.pad(X0, (0, Pp - P)) if layout == "rows" else X0
-            G = torch.nn.functional.pad(G0, (0, Pp - P)) if layout == "rows" else G0
+            X = torch.nn.functional.pad(X0, (0, Pp - P))[:, :Pp].contiguous() if layout == "rows" else X0
+            G = torch.nn.functional.pad(G0, (0, Pp - P))[:, :Pp].contiguous() if layout == "rows" else G0
             eng = engine.GossipEngine(csr, Pp, device=dev, X=X, layout=layout, tile_cols=T)
             Gl = eng.layout_like(G)
             plan = eng.plan(deviation=True)
@@ -83,8 +87,8 @@ def main():
             print(json.dumps({"case": name, "plan": plan, "us": med * 1e3,
                               "us_no_deviation": nodev * 1e3,
                               "spread_us": [lo * 1e3, hi * 1e3],
-                              "GBs": alg / (med / 1e3) / 1e9,
-                              "frac": alg / (med / 1e3) / 1e9 / 8000.0}), flush=True)
+                              "GBs": 12 * n * Pp / (med / 1e3) / 1e9,
+                              "frac": 12 * n * Pp / (med / 1e3) / 1e9 / 8000.0}), flush=True)
             del eng, Gl, X, G
             torch.cuda.empty_cache()
         finally:

@@ -1060,16 +1060,19 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
         constexpr int XITEMS = (MB / 4) * (CW / 4);    // 384 items per chunk
         f32x4 xva[4], xvb[4];                          // two chunks in flight
         const bool xt = tid < XITEMS;
-        const int xb0 = 4 * (tid / (CW / 4)), xc = 4 * (tid % (CW / 4));
+        // lanes past the items load an item's address too (their registers are never used)
+        const int xi = xt ? tid : tid - XITEMS;
+        const int xb0 = 4 * (xi / (CW / 4)), xc = 4 * (xi % (CW / 4));
+        // Every lane issues its four loads unconditionally from a clamped address, and the
+        // columns from din on (the ones column din, db1, then zeros) are substituted at the
+        // registers' single use (chunk, below): a load the compiler may branch around made the
+        // wait before that use a vmcnt(0), which also drained every G store of the tiles just
+        // issued (all nine chunk waits of this phase, in the ISA).
         auto load = [&](f32x4 (&xv)[4], int c0) {
-            if (!xt) return;
+            const int c = c0 + xc < din ? c0 + xc : din - 4;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int c = c0 + xc;
-                // column din is the ones column (db1); din % 4 == 0 puts it at a float4 start
-                xv[i] = c < din ? *reinterpret_cast<const f32x4 *>(x + (int64_t)(xb0 + i) * din + c)
-                        : c == din ? f32x4{1.f, 0.f, 0.f, 0.f} : f32x4{0.f, 0.f, 0.f, 0.f};
-            }
+            for (int i = 0; i < 4; ++i)
+                xv[i] = *reinterpret_cast<const f32x4 *>(x + (int64_t)(xb0 + i) * din + c);
         };
         load(xva, 0);
         load(xvb, CW);
@@ -1089,10 +1092,20 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
         const PM gw1 = mat(Gr, o_w1, din), gb1 = mat(Gr, o_b1, 0);
         const int r = lane & 31, hh = lane >> 5;
         auto chunk = [&](int ci, f32x4 (&xv)[4]) {
-            if (xt) split_store(xv, xb0, xc, xplanes, XP);
+            if (xt) {
+                // column din is the ones column (db1); din % 4 == 0 puts it at a float4 start
+                const int c = ci * CW + xc;
+                f32x4 v[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    v[i] = c < din ? xv[i]
+                           : c == din ? f32x4{1.f, 0.f, 0.f, 0.f} : f32x4{0.f, 0.f, 0.f, 0.f};
+                split_store(v, xb0, xc, xplanes, XP);
+            }
             __syncthreads();
             const int c0 = ci * CW;
-            if (ci + 2 < nc) load(xv, c0 + 2 * CW);
+            // (unconditional: past the last chunk it re-reads the last one, never used)
+            load(xv, ci + 2 < nc ? c0 + 2 * CW : (nc - 1) * CW);
             const int ntc = min(CW / 32, (din + 1 - c0 + 31) / 32);
             for (int it = wave; it < 5 * ntc; it += 8) {
                 const int nt = it % ntc, t = it / ntc;
@@ -1117,9 +1130,11 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
             }
             __syncthreads();
         };
+        // chunks in pairs, the second of the last pair run even past nc (no tiles then: ntc <= 0),
+        // so the loads and waits are the same straight-line code every pair
         for (int ci = 0; ci < nc; ci += 2) {
             chunk(ci, xva);
-            if (ci + 1 < nc) chunk(ci + 1, xvb);
+            chunk(ci + 1, xvb);
         }
     } else {
     // fp32: dW1 by 256-column chunks of x, staged in the H2/H3 space (free now: dZ2 and dZ3

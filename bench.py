@@ -61,7 +61,9 @@ def parse():
                             "c4-gather", "c4-ba", "c5"])
     p.add_argument("--rank-of", type=int, default=8,
                    help="c4-rank: the GPU count of the partition whose rank 0 is measured alone")
-    p.add_argument("--halo-chunks", default="8",
+    # 2: the cheapest chunk count on one GPU at rank-of 8 / 4 / 2 (433 / 746 / 1340 us a round
+    # against 459 / 789 / 1346 at 4 and 494 / 833 / 1418 at 8, profiles/r12/c4rank_rankof)
+    p.add_argument("--halo-chunks", default="2",
                    help="c4 / c4-rank: column chunks of the 'chunks' overlap scheme; a comma list "
                         "(c4-rank) times each count as its own scheme")
     p.add_argument("--halo-tile-cols", type=int, default=0,
@@ -743,9 +745,9 @@ def _halo_schemes(args, dev, rank, world, csr, parts, P, lr, gen):
     n = csr.n_rows
     G = None
     schemes = {}
-    # "whole": one exchange, then one launch (no overlap, no per-chunk launches); "chunks": 8
-    # column chunks, the exchange of one overlapping the mix of the previous; "split": the
-    # interior rows mix while the one exchange is in flight
+    # "whole": one exchange, then one launch (no overlap, no per-chunk launches); "chunks":
+    # --halo-chunks column chunks, the exchange of one overlapping the mix of the previous;
+    # "split": the interior rows mix while the one exchange is in flight
     names = ["whole", "chunks", "split"] if args.halo_overlap == "both" else [args.halo_overlap]
     for name in names:
         # boundary-last row order for every scheme (the pack reads one contiguous run of rows)

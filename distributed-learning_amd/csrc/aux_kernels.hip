@@ -425,10 +425,11 @@ hipError_t launch_step_rows_tiled(const float *x, int x_rows, const float *g, in
     // about 2048 resident threads per CU over 256 CUs; each lane group walks >= 4 tiles
     int64_t gy = (256 * 2048) / (bx * 256);
     // DLAMD_PACK_RUN=n (a measurement knob): runs of n tiles per workgroup instead
-    if (const char *pr = getenv("DLAMD_PACK_RUN")) {
-        const int64_t run = atoi(pr);
-        if (run > 0) gy = (n_tiles + run - 1) / run;
-    }
+    static const int64_t pack_run = [] {
+        const char *pr = getenv("DLAMD_PACK_RUN");
+        return pr ? (int64_t)atoi(pr) : (int64_t)0;
+    }();
+    if (pack_run > 0) gy = (n_tiles + pack_run - 1) / pack_run;
     const int64_t gmax = (n_tiles + 4 * sub - 1) / (4 * sub);
     if (gy > gmax) gy = gmax;
     if (gy > 65535) gy = 65535;

@@ -443,10 +443,14 @@ int check_mix_args(const dl_mix_args *a) {
         return fail(DL_ERR_INVALID, "dl_mix_round: the column mean of a halo round is global: "
                                     "use colsum_out and an all-reduce");
     if ((a->dev_sq || a->dev_max || a->mean_prev || a->colsum_out) && halo_round &&
-        !(a->mean_prev && a->colsum_out && a->dev_sq))
+        !(a->mean_prev && a->colsum_out && (a->dev_sq || !a->dev_max)))
         return fail(DL_ERR_INVALID,
                     "dl_mix_round: a halo round's deviation is the lagged one: mean_prev, "
-                    "colsum_out and dev_sq together (or dl_column_sum + dl_deviation after it)");
+                    "colsum_out and dev_sq together, or both without dev_sq / dev_max (partial "
+                    "rows left in the workspace), or dl_column_sum + dl_deviation after it");
+    if (halo_round && a->mean_prev && !a->dev_sq && !a->dev_max && a->tile_cols <= 0)
+        return fail(DL_ERR_INVALID, "dl_mix_round: partial rows without dev_sq need the "
+                                    "column-tiled layout (one launch, plan grid rows)");
     // extents: a tiled operand of `rows` used rows inside blocks of `ld` rows spans (tiles - 1)
     // block strides plus its used rows of the last tile
     const int64_t Tc = a->tile_cols;
@@ -1197,6 +1201,9 @@ int dl_mix_round(const dl_mix_args *args, void *workspace, size_t ws_bytes, dl_s
         }
         if (parts) {
             if (Nr <= 1 && !lag) return zero_deviation(Nr, args->dev_sq, args->dev_max, s);
+            // a lagged round asked for neither output leaves its grid_full partial rows to the
+            // caller (column chunks reduced once, dl_row_sums)
+            if (lag && !args->dev_sq && !args->dev_max) return DL_OK;
             hipError_t e = dl::launch_dev_reduce(partial, grid_full + grid_tail, Np, args->dev_sq,
                                                  args->dev_max, s, true);
             if (e != hipSuccess) return hip_fail(e, "dev_reduce launch");

@@ -202,7 +202,9 @@ def mix_round(W: DeviceCsr, X, Y, G=None, lr=0.0, halo=None, dev_sq=None, dev_ma
     buffer of per-peer tiled blocks of ``halo_blocks`` rows, see ``mix_args_tiled``).
     Halo rounds (``halo`` rows): ``mean_prev`` (the global column mean of X), ``colsum_out`` and
     ``dev_sq`` together give the lagged deviation -- dev_sq = ||x_a - mean_prev||^2 of the
-    INPUT rows, colsum_out = this rank's column sums of X - lr G (include/dlamd.h)."""
+    INPUT rows, colsum_out = this rank's column sums of X - lr G (include/dlamd.h).  Without
+    dev_sq / dev_max (column-tiled only) the round leaves its [plan grid, n_local] partial rows
+    in ``workspace`` -- then a float32 tensor slice the caller reduces (``row_sums``)."""
     lib = _lib.load()
     if tiled is not None:
         P = tiled[0]
@@ -217,9 +219,14 @@ def mix_round(W: DeviceCsr, X, Y, G=None, lr=0.0, halo=None, dev_sq=None, dev_ma
                     t.dim() != 1 or t.stride(0) != 1:
                 raise ValueError(f"{name} must be a contiguous float32 [n_params] device tensor")
             setattr(args, name, _lib.ptr(t))
-    workspace = workspace or Workspace(W.device)
-    wp, wn = workspace.ptr_size(lib.dl_mix_workspace_bytes(max(W.n_rows, W.n_local),
-                                                           W.n_src - W.n_local, P))
+    if isinstance(workspace, torch.Tensor):   # a caller-placed slice (partial rows it reduces)
+        if workspace.device != W.device or not workspace.is_contiguous():
+            raise ValueError("a tensor workspace must be a contiguous tensor on W's device")
+        wp, wn = _lib.ptr(workspace), workspace.numel() * workspace.element_size()
+    else:
+        workspace = workspace or Workspace(W.device)
+        wp, wn = workspace.ptr_size(lib.dl_mix_workspace_bytes(max(W.n_rows, W.n_local),
+                                                               W.n_src - W.n_local, P))
     _lib.check(lib.dl_mix_round(ctypes.byref(args), wp, wn, _lib.stream_handle(W.device)),
                "dl_mix_round")
 

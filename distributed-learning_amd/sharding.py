@@ -18,6 +18,7 @@ Two decompositions of the agent matrix X[N, P]:
 The transport is pluggable: ``DistTransport`` (torch.distributed, RCCL on GPU / gloo on CPU) and
 ``LocalTransport`` (in-process virtual ranks, used to test the halo logic on one device).
 """
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -558,6 +559,19 @@ class HipOps:
                          mean_prev=mean_prev, colsum_out=colsum, workspace=self.ws, tiled=tiled,
                          halo_blocks=halo_blocks)
 
+    def mix_partials(self, W, X, Y, G, lr, halo, mean_prev, colsum, parts, halo_blocks):
+        """A column-tiled lagged halo round that leaves its [plan grid, n_local] deviation
+        partial rows in ``parts`` (a float32 slice) instead of reducing them: the column chunks
+        of a round then share one ``row_sums`` over all their rows (one reduce launch a round,
+        not one per chunk)."""
+        tiled = (X.shape[0] * X.shape[2], X.shape[2])
+        self.E.mix_round(W, X, Y, G=G, lr=lr, halo=halo, mean_prev=mean_prev, colsum_out=colsum,
+                         workspace=parts, tiled=tiled, halo_blocks=halo_blocks)
+
+    def partial_rows(self, W, width, tile_cols):
+        """Partial rows a column-tiled lagged round of ``width`` columns writes (its plan grid)."""
+        return int(self.E.plan_shape(W, width, deviation=True, tile_cols=tile_cols)["grid"])
+
     def row_sums(self, parts):
         """(sum over the rows of parts, max sqrt of it): a chunked round's deviation."""
         sums = torch.empty(parts.shape[1], dtype=torch.float32, device=parts.device)
@@ -830,13 +844,24 @@ class HaloShard:
             if self._mean is None:
                 self._mean = self._global_mean(self.X)
             colsum = torch.empty(self.P, dtype=torch.float32, device=self.device)
-            parts = torch.empty(len(chunks), self.plan.n_local, dtype=torch.float32,
-                                device=self.device)
             # one launch measures every local row (one chunk, or the split's interior launch):
             # its reduce also gives the max, no torch kernels of its own
             one = split or len(chunks) == 1
             dmax = torch.empty(1, dtype=torch.float32, device=self.device) if one else None
-            lag = (self._mean, colsum, parts, dmax)
+            prow = None if one else self._partial_rows(chunks)
+            if prow is not None:
+                # column-tiled chunks: every chunk's kernel leaves its partial rows in its own
+                # slice of one buffer, and one row_sums reduces them all (no reduce per chunk)
+                # (flat, with slack: each chunk's slice runs to the end of the buffer, which
+                # covers the ABI's aligned size of its grid rows)
+                nl = self.plan.n_local
+                flat = torch.empty(prow[-1] * nl + 64, dtype=torch.float32, device=self.device)
+                parts = flat[:prow[-1] * nl].view(prow[-1], nl)
+                prow = (prow, flat)
+            else:
+                parts = torch.empty(len(chunks), self.plan.n_local, dtype=torch.float32,
+                                    device=self.device)
+            lag = (self._mean, colsum, parts, dmax, prow)
         if split:
             self._split_round(G, lr, None if lag is None else (lag[0], lag[1], lag[2][0], lag[3]))
         else:
@@ -872,6 +897,26 @@ class HaloShard:
         must call this before the next ``round(deviation=True)``."""
         self._forget_mean()
 
+    def _partial_rows(self, chunks):
+        """Row offsets of each column chunk's partial rows in one buffer ([0, g0, g0 + g1, ...]),
+        or None where chunks reduce one by one (row-major layout, ops without mix_partials,
+        rounds without halo rows)."""
+        # (n_local % 4: every chunk's slice starts 16-byte aligned; DLAMD_CHUNK_PARTIALS=0, a
+        # measurement knob, keeps one reduce per chunk)
+        if not (self.T and self.plan.n_halo and self.plan.n_local % 4 == 0 and
+                hasattr(self.ops, "mix_partials") and
+                os.environ.get("DLAMD_CHUNK_PARTIALS", "1") != "0"):
+            return None
+        widths = sorted({c1 - c0 for c0, c1 in chunks})
+        key = (tuple(widths), self.T)
+        if getattr(self, "_prow_key", None) != key:
+            self._prow_grid = {w: self.ops.partial_rows(self.W, w, self.T) for w in widths}
+            self._prow_key = key
+        off = [0]
+        for c0, c1 in chunks:
+            off.append(off[-1] + self._prow_grid[c1 - c0])
+        return off
+
     def _mix_all(self, chunks, G, lr, lag):
         def post(j):
             c0, c1 = chunks[j]
@@ -885,8 +930,17 @@ class HaloShard:
             works, halo = pend
             for w in works:
                 w.wait()
-            cl = None if lag is None else (lag[0][c0:c1], lag[1][c0:c1], lag[2][j], lag[3])
-            self.mix_chunk(c0, c1, halo, G, lr, cl)
+            if lag is not None and lag[4] is not None:   # partial rows, reduced after the loop
+                pr, flat = lag[4]
+                Gc = self._cols(G, c0, c1) if G is not None else None
+                self.ops.mix_partials(self.W, self._cols(self.X, c0, c1),
+                                      self._cols(self.Y, c0, c1), Gc, lr,
+                                      halo if self.plan.n_halo else None, lag[0][c0:c1],
+                                      lag[1][c0:c1], flat[pr[j] * self.plan.n_local:],
+                                      self.halo_blocks)
+            else:
+                cl = None if lag is None else (lag[0][c0:c1], lag[1][c0:c1], lag[2][j], lag[3])
+                self.mix_chunk(c0, c1, halo, G, lr, cl)
             pend = nxt
         self.X, self.Y = self.Y, self.X
 

@@ -127,7 +127,11 @@ typedef struct dl_mix_args {
                                colsum_out and dev_sq):
                                the global column mean of x (the previous round's all-reduced
                                colsum_out / N): dev_sq[a] = ||x_a - mean_prev||^2, dev_max =
-                               max sqrt (nullable). */
+                               max sqrt (nullable).  With dev_sq and dev_max both NULL the
+                               round leaves its partial sums in the workspace instead -- rows
+                               [0, plan grid) of n_local_src floats, column-tiled layout only --
+                               for the caller to reduce (one dl_row_sums over several column
+                               chunks' partial rows placed back to back). */
     float *colsum_out;      /* nullable [n_params] (as mean_prev): sum over the local source rows of
                                the stepped inputs t = x - lr*g, in a fixed order.  Summed over all
                                ranks it is the column sum of the round's output when the global W

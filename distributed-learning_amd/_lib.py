@@ -131,7 +131,7 @@ SIGNATURES = {
     "dl_from_tiled": (_i32, [_vp, _i32, _i64, _i32, _vp, _i64, _vp]),
     "dl_column_sum": (_i32, [_vp, _i64, _i32, _i64, _vp, _vp]),
     "dl_max_column_std": (_i32, [_vp, _i64, _i32, _i64, _vp, _vp]),
-    "dl_row_sums": (_i32, [_vp, _i32, _i32, _vp, _vp, _vp]),
+    "dl_row_sums": (_i32, [_vp, _i32, _i32, _vp, _vp, _i32, _vp]),
     "dl_step_rows": (_i32, [_vp, _i64, _vp, _i64, _f32, _vp, _i32, _i64, _vp, _i64, _vp]),
     "dl_step_rows_tiled": (_i32, [_vp, _i32, _vp, _i32, _f32, _vp, _i32, _i64, _i32, _vp, _vp]),
     "dl_step_rows_tiled_peers": (_i32, [_vp, _i32, _vp, _i32, _f32, _vp, _i32, _vp, _vp, _i64,

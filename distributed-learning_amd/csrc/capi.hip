@@ -443,12 +443,12 @@ int check_mix_args(const dl_mix_args *a) {
         return fail(DL_ERR_INVALID, "dl_mix_round: the column mean of a halo round is global: "
                                     "use colsum_out and an all-reduce");
     if ((a->dev_sq || a->dev_max || a->mean_prev || a->colsum_out) && halo_round &&
-        !(a->mean_prev && a->colsum_out && (a->dev_sq || !a->dev_max)))
+        !(a->mean_prev && a->colsum_out))
         return fail(DL_ERR_INVALID,
                     "dl_mix_round: a halo round's deviation is the lagged one: mean_prev, "
-                    "colsum_out and dev_sq together, or both without dev_sq / dev_max (partial "
-                    "rows left in the workspace), or dl_column_sum + dl_deviation after it");
-    if (halo_round && a->mean_prev && !a->dev_sq && !a->dev_max && a->tile_cols <= 0)
+                    "colsum_out and dev_sq together, or both without dev_sq (partial rows left "
+                    "in the workspace), or dl_column_sum + dl_deviation after it");
+    if (halo_round && a->mean_prev && !a->dev_sq && a->tile_cols <= 0)
         return fail(DL_ERR_INVALID, "dl_mix_round: partial rows without dev_sq need the "
                                     "column-tiled layout (one launch, plan grid rows)");
     // extents: a tiled operand of `rows` used rows inside blocks of `ld` rows spans (tiles - 1)
@@ -1201,9 +1201,9 @@ int dl_mix_round(const dl_mix_args *args, void *workspace, size_t ws_bytes, dl_s
         }
         if (parts) {
             if (Nr <= 1 && !lag) return zero_deviation(Nr, args->dev_sq, args->dev_max, s);
-            // a lagged round asked for neither output leaves its grid_full partial rows to the
-            // caller (column chunks reduced once, dl_row_sums)
-            if (lag && !args->dev_sq && !args->dev_max) return DL_OK;
+            // a lagged round without dev_sq leaves its grid_full partial rows to the caller
+            // (column chunks reduced once, dl_row_sums); its dev_max, if any, the kernel zeroed
+            if (lag && !args->dev_sq) return DL_OK;
             hipError_t e = dl::launch_dev_reduce(partial, grid_full + grid_tail, Np, args->dev_sq,
                                                  args->dev_max, s, true);
             if (e != hipSuccess) return hip_fail(e, "dev_reduce launch");
@@ -1379,12 +1379,12 @@ int dl_column_sum(const float *x, int64_t ldx, int32_t n_rows, int64_t n_params,
 }
 
 int dl_row_sums(const float *parts, int32_t n_parts, int32_t n_rows, float *sums, float *max_sqrt,
-                dl_stream_t stream) {
+                int32_t max_zeroed, dl_stream_t stream) {
     g_err.clear();
     if (!parts || n_parts <= 0 || n_rows <= 0 || (!sums && !max_sqrt))
         return fail(DL_ERR_INVALID, "dl_row_sums: bad arguments");
     hipError_t e = dl::launch_dev_reduce(parts, n_parts, n_rows, sums, max_sqrt,
-                                         static_cast<hipStream_t>(stream));
+                                         static_cast<hipStream_t>(stream), max_zeroed != 0);
     return e == hipSuccess ? DL_OK : hip_fail(e, "dev_reduce launch");
 }
 

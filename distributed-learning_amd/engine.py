@@ -386,15 +386,17 @@ def deviation_tiled(Xt, n_params, dev_sq=None, dev_max=None, mean_out=None,
     return dev_sq, dev_max
 
 
-def row_sums(parts, sums=None, max_sqrt=None):
+def row_sums(parts, sums=None, max_sqrt=None, max_zeroed=False):
     """dl_row_sums: sums[a] = sum_b parts[b][a] (fixed order), max_sqrt[0] = max sqrt(sums) --
-    a chunked round's per-agent deviation and its max in one launch."""
+    a chunked round's per-agent deviation and its max in one launch (max_zeroed: max_sqrt
+    already holds 0, as a partial-rows dl_mix_round given it as dev_max leaves it)."""
     lib = _lib.load()
     if parts.dim() != 2 or not parts.is_contiguous() or parts.dtype != torch.float32:
         raise ValueError("parts must be a contiguous float32 [n_parts, n_rows] tensor")
     nb, n = parts.shape
     _lib.check(lib.dl_row_sums(_lib.ptr(parts), nb, n, _lib.ptr(sums), _lib.ptr(max_sqrt),
-                               _lib.stream_handle(parts.device)), "dl_row_sums")
+                               int(bool(max_zeroed)), _lib.stream_handle(parts.device)),
+               "dl_row_sums")
     return sums, max_sqrt
 
 

@@ -559,22 +559,26 @@ class HipOps:
                          mean_prev=mean_prev, colsum_out=colsum, workspace=self.ws, tiled=tiled,
                          halo_blocks=halo_blocks)
 
-    def mix_partials(self, W, X, Y, G, lr, halo, mean_prev, colsum, parts, halo_blocks):
+    def mix_partials(self, W, X, Y, G, lr, halo, mean_prev, colsum, parts, halo_blocks,
+                     zero_max=None):
         """A column-tiled lagged halo round that leaves its [plan grid, n_local] deviation
         partial rows in ``parts`` (a float32 slice) instead of reducing them: the column chunks
         of a round then share one ``row_sums`` over all their rows (one reduce launch a round,
-        not one per chunk)."""
+        not one per chunk).  ``zero_max``: a [1] buffer the kernel sets to 0 for that reduce."""
         tiled = (X.shape[0] * X.shape[2], X.shape[2])
         self.E.mix_round(W, X, Y, G=G, lr=lr, halo=halo, mean_prev=mean_prev, colsum_out=colsum,
-                         workspace=parts, tiled=tiled, halo_blocks=halo_blocks)
+                         dev_max=zero_max, workspace=parts, tiled=tiled, halo_blocks=halo_blocks)
 
     def partial_rows(self, W, width, tile_cols):
         """Partial rows a column-tiled lagged round of ``width`` columns writes (its plan grid)."""
         return int(self.E.plan_shape(W, width, deviation=True, tile_cols=tile_cols)["grid"])
 
-    def row_sums(self, parts):
-        """(sum over the rows of parts, max sqrt of it): a chunked round's deviation."""
+    def row_sums(self, parts, zeroed_max=None):
+        """(sum over the rows of parts, max sqrt of it): a chunked round's deviation.
+        ``zeroed_max``: a [1] buffer already set to 0 on the stream (mix_partials' zero_max)."""
         sums = torch.empty(parts.shape[1], dtype=torch.float32, device=parts.device)
+        if zeroed_max is not None:
+            return self.E.row_sums(parts, sums, zeroed_max, max_zeroed=True)
         mx = torch.empty(1, dtype=torch.float32, device=parts.device)
         return self.E.row_sums(parts, sums, mx)
 
@@ -857,7 +861,8 @@ class HaloShard:
                 nl = self.plan.n_local
                 flat = torch.empty(prow[-1] * nl + 64, dtype=torch.float32, device=self.device)
                 parts = flat[:prow[-1] * nl].view(prow[-1], nl)
-                prow = (prow, flat)
+                # the max's word, zeroed by the first chunk's kernel: no memset before the reduce
+                prow = (prow, flat, torch.empty(1, dtype=torch.float32, device=self.device))
             else:
                 parts = torch.empty(len(chunks), self.plan.n_local, dtype=torch.float32,
                                     device=self.device)
@@ -873,6 +878,8 @@ class HaloShard:
             return None
         if dmax is not None:
             dev_sq, dev_max = parts[0], dmax
+        elif lag[4] is not None:   # chunk partial rows: one launch, the max already zeroed
+            dev_sq, dev_max = self.ops.row_sums(parts, zeroed_max=lag[4][2])
         elif hasattr(self.ops, "row_sums"):   # chunks: one launch for the sum and the max
             dev_sq, dev_max = self.ops.row_sums(parts)
         else:
@@ -931,13 +938,13 @@ class HaloShard:
             for w in works:
                 w.wait()
             if lag is not None and lag[4] is not None:   # partial rows, reduced after the loop
-                pr, flat = lag[4]
+                pr, flat, zmax = lag[4]
                 Gc = self._cols(G, c0, c1) if G is not None else None
                 self.ops.mix_partials(self.W, self._cols(self.X, c0, c1),
                                       self._cols(self.Y, c0, c1), Gc, lr,
                                       halo if self.plan.n_halo else None, lag[0][c0:c1],
                                       lag[1][c0:c1], flat[pr[j] * self.plan.n_local:],
-                                      self.halo_blocks)
+                                      self.halo_blocks, zero_max=zmax if j == 0 else None)
             else:
                 cl = None if lag is None else (lag[0][c0:c1], lag[1][c0:c1], lag[2][j], lag[3])
                 self.mix_chunk(c0, c1, halo, G, lr, cl)

@@ -127,11 +127,12 @@ typedef struct dl_mix_args {
                                colsum_out and dev_sq):
                                the global column mean of x (the previous round's all-reduced
                                colsum_out / N): dev_sq[a] = ||x_a - mean_prev||^2, dev_max =
-                               max sqrt (nullable).  With dev_sq and dev_max both NULL the
-                               round leaves its partial sums in the workspace instead -- rows
-                               [0, plan grid) of n_local_src floats, column-tiled layout only --
-                               for the caller to reduce (one dl_row_sums over several column
-                               chunks' partial rows placed back to back). */
+                               max sqrt (nullable).  With dev_sq NULL the round leaves its
+                               partial sums in the workspace instead -- rows [0, plan grid) of
+                               n_local_src floats, column-tiled layout only -- for the caller to
+                               reduce (one dl_row_sums over several column chunks' partial rows
+                               placed back to back); a dev_max is then only set to 0, for that
+                               dl_row_sums (max_zeroed = 1). */
     float *colsum_out;      /* nullable [n_params] (as mean_prev): sum over the local source rows of
                                the stepped inputs t = x - lr*g, in a fixed order.  Summed over all
                                ranks it is the column sum of the round's output when the global W
@@ -345,10 +346,12 @@ int dl_column_sum(const float *x, int64_t ldx, int32_t n_rows, int64_t n_params,
 
 /* sums[a] = sum_b parts[b][a] over n_parts rows of n_rows floats (fixed order, fp64), max_sqrt[0]
  * = max_a sqrt(sums[a]); either output nullable.  The per-agent ||x_a - mean||^2 of a round run
- * as several column chunks (each chunk's dev_sq is one row of parts), and their max -- the
- * _get_max_deviation of mixer.py:51-55 over the whole round -- in one launch. */
+ * as several column chunks (their partial rows back to back in parts, see mean_prev), and their
+ * max -- the _get_max_deviation of mixer.py:51-55 over the whole round -- in one launch.
+ * max_zeroed = 1: max_sqrt already holds 0 (a dl_mix_round given it as dev_max without dev_sq
+ * zeroes it), so no memset is queued before the reduce. */
 int dl_row_sums(const float *parts, int32_t n_parts, int32_t n_rows, float *sums, float *max_sqrt,
-                dl_stream_t stream);
+                int32_t max_zeroed, dl_stream_t stream);
 
 /* out[0] = max_p std_a(x[a, p]) (population std, the intent of mixer.py:82-84). */
 int dl_max_column_std(const float *x, int64_t ldx, int32_t n_rows, int64_t n_params, float *out,

@@ -569,3 +569,8 @@ def test_row_sums(cuda):
     want = parts.cpu().double().sum(0).float().numpy()
     np.testing.assert_allclose(sums.cpu().numpy(), want, rtol=1e-6)
     assert float(mx.item()) == pytest.approx(float(np.sqrt(want).max()), rel=1e-6)
+    # max_zeroed: the caller (a partial-rows dl_mix_round's dev_max) already set the word to 0
+    sums2, mx2 = torch.empty(1000, device=cuda), torch.zeros(1, device=cuda)
+    E.row_sums(parts, sums2, mx2, max_zeroed=True)
+    torch.cuda.synchronize()
+    assert torch.equal(sums2, sums) and torch.equal(mx2, mx)

@@ -253,6 +253,19 @@ def test_tiled_halo_arguments_validate_without_a_gpu():
     assert rc == _lib.DL_ERR_INVALID and b"halo" in msg
     rc, msg = err(args(n_hub_rows=-1))
     assert rc == _lib.DL_ERR_INVALID and b"n_hub_rows" in msg
+    # the lagged deviation: mean_prev and colsum_out together; without dev_sq the round leaves
+    # its partial rows in the workspace (column-tiled only), so dev_max alone is accepted there
+    # and the row-major layout refuses it -- all before any device call
+    rc, msg = err(args(mean_prev=1 << 36))
+    assert rc == _lib.DL_ERR_INVALID and b"lagged" in msg
+    rc, msg = err(args(tile_cols=0, ldx=64, ldy=64, ldh=64, mean_prev=1 << 36,
+                       colsum_out=(1 << 36) + 4096, dev_max=(1 << 36) + 8192))
+    assert rc == _lib.DL_ERR_INVALID and b"column-tiled" in msg
+    rc, msg = err(args(mean_prev=1 << 36, colsum_out=(1 << 36) + 4096))
+    assert rc == _lib.DL_ERR_WORKSPACE, msg   # accepted: only the missing workspace is refused
+    # dl_row_sums: outputs and sizes checked on the host
+    assert lib.dl_row_sums(None, 2, 8, 1 << 20, None, 0, None) == _lib.DL_ERR_INVALID
+    assert lib.dl_row_sums(1 << 20, 2, 8, None, None, 1, None) == _lib.DL_ERR_INVALID
     # dl_step_rows_tiled: arguments before any launch
     assert lib.dl_step_rows_tiled(None, 4, None, 0, 0.0, None, 2, 64, 16, None, None) == \
         _lib.DL_ERR_INVALID

@@ -15,6 +15,8 @@
 // registers while the current tile's rounds run.
 #include "dl_internal.h"
 
+#include <type_traits>
+
 namespace dl {
 namespace {
 
@@ -123,23 +125,40 @@ __global__ void __launch_bounds__(kTileThreads) mix_multi_kernel(TileArgs a, int
     // register-cached CSR (RE > 0): byte offset of each neighbour's chunk c inside an image
     uint32_t coff[KV][RE > 0 ? RE : 1];
     float wreg[RE > 0 ? RE : 1];
+    bool self_ok = true;   // every row of this thread lists itself first (the diagonal of W)
     if constexpr (RE > 0) {
 #pragma unroll
         for (int e = 0; e < RE; ++e) wreg[e] = a.w[e];
 #pragma unroll
         for (int k = 0; k < KV; ++k) {
             const int ag = FULL || s + k * SLOTS < Nr ? s + k * SLOTS : 0;
+            self_ok = self_ok && a.col[ag * RE] == ag;
 #pragma unroll
             for (int e = 0; e < RE; ++e)
                 coff[k][e] = ((uint32_t)a.col[ag * RE + e] * C + c) * 16u;
         }
     }
-    auto mix_row_reg = [&](const float4 *src, int k) {
+    // Every row's first entry its own agent (W = I - L(w) with the diagonal first,
+    // graph.from_edge_weights: c2, c4): that operand is the value this very thread produced for
+    // the row in the previous round (or staged), so it is kept in a register (own[k]) and the
+    // round reads 4 neighbours from LDS instead of 5 -- same operand, same fold, same bits.
+    // Decided per wave (a wave vote, no LDS: a uniform branch, so the skipped read is not
+    // issued; __syncthreads_and would add static LDS beside the full dynamic allocation).
+    const bool self0 = RE > 0 && __all(self_ok ? 1 : 0) != 0;
+    float4 own[RE > 0 ? KV : 1];
+#pragma unroll
+    for (int k = 0; k < (RE > 0 ? KV : 1); ++k) own[k] = mm_zero4();
+    auto mix_row_reg = [&](const float4 *src, int k, auto selfc) {
+        constexpr bool SELF = decltype(selfc)::value;
         const char *base = reinterpret_cast<const char *>(src);
         float4 acc = mm_zero4();
 #pragma unroll
         for (int e = 0; e < (RE > 0 ? RE : 1); ++e) {
-            const float4 v = *reinterpret_cast<const float4 *>(base + coff[k][e]);
+            float4 v;
+            if (SELF && e == 0)
+                v = own[k];
+            else
+                v = *reinterpret_cast<const float4 *>(base + coff[k][e]);
             const float w = wreg[e];
             acc.x = acc.x + w * v.x;
             acc.y = acc.y + w * v.y;
@@ -148,8 +167,8 @@ __global__ void __launch_bounds__(kTileThreads) mix_multi_kernel(TileArgs a, int
         }
         return acc;
     };
-    auto out_row = [&](const float4 *src, int k, int ag) {
-        if constexpr (RE > 0) return mix_row_reg(src, k);
+    auto out_row = [&](const float4 *src, int k, int ag, auto selfc) {
+        if constexpr (RE > 0) return mix_row_reg(src, k, selfc);
         return mix_row(src, ag);
     };
 
@@ -176,6 +195,7 @@ __global__ void __launch_bounds__(kTileThreads) mix_multi_kernel(TileArgs a, int
                 t.z = t.z - a.lr * pg[k].z;
                 t.w = t.w - a.lr * pg[k].w;
             }
+            if (RE > 0) own[k] = t;
             if (FULL || r < Nr) {
                 img0[r * C + c] = t;
                 if (DEV) {
@@ -222,6 +242,9 @@ __global__ void __launch_bounds__(kTileThreads) mix_multi_kernel(TileArgs a, int
         stage();
         prefetch(min(tile_id + (int)gridDim.x, last));
     }
+    // the tile loop twice, with and without the own-operand register (self0 is wave-uniform:
+    // one branch here, none inside the rounds)
+    auto tiles = [&](auto selfc) {
     for (; tile_id < a.n_tiles; tile_id += gridDim.x) {
         asm volatile("" : "+v"(ox), "+v"(og), "+v"(oy));
         const int nxt = min(tile_id + (int)gridDim.x, last);
@@ -231,7 +254,11 @@ __global__ void __launch_bounds__(kTileThreads) mix_multi_kernel(TileArgs a, int
 #pragma unroll
             for (int k = 0; k < KV; ++k) {
                 const int ag = s + k * SLOTS;
-                if (FULL || ag < Nr) dst[ag * C + c] = out_row(src, k, ag);
+                if (FULL || ag < Nr) {
+                    const float4 o = out_row(src, k, ag, selfc);
+                    dst[ag * C + c] = o;
+                    if (RE > 0) own[k] = o;
+                }
                 // one output row at a time: keeps the RE neighbour reads of the next row from
                 // being hoisted above this one's (register pressure at 1024 threads)
                 __builtin_amdgcn_sched_barrier(0);
@@ -246,7 +273,7 @@ __global__ void __launch_bounds__(kTileThreads) mix_multi_kernel(TileArgs a, int
         for (int k = 0; k < KV; ++k) {
             const int ag = s + k * SLOTS;
             if (FULL || ag < Nr) {
-                const float4 y = out_row(src, k, ag);
+                const float4 y = out_row(src, k, ag, selfc);
                 float4 *py = const_cast<float4 *>(mm_at(yt, oy + (uint32_t)k * sy));
                 if (MODE == 2 || (MODE == 0 && a.nt_store))
                     mm_nt_store4(y, py);
@@ -272,6 +299,17 @@ __global__ void __launch_bounds__(kTileThreads) mix_multi_kernel(TileArgs a, int
         __syncthreads();   // both images and the scratch are rewritten by the next tile
         stage();   // the next tile (past the end: a re-read of the last one, then unused)
         prefetch(min(nxt + (int)gridDim.x, last));   // lands while the next tile's rounds run
+    }
+    };
+    // (pure gossip only, and not at C = 2 x KV = 4 with the deviation: beside those registers
+    // the second copy spills)
+    if constexpr (RE > 0 && !SGD && !(C == 2 && KV == 4 && DEV)) {
+        if (self0)
+            tiles(std::true_type{});
+        else
+            tiles(std::false_type{});
+    } else {
+        tiles(std::false_type{});
     }
     if (DEV) {
 #pragma unroll

@@ -94,6 +94,7 @@ struct Plan {
     uint32_t csr_off, scratch_off;
     int head;       // path 5: CSR entries per row in registers (the rest in LDS)
     int tail_fmt;   // path 5: LDS tail entries of 8 B (2) or 6 B (1)
+    int grp;        // path 1, column-tiled: data tiles per kernel tile (0 / 1: one)
 };
 
 // Workgroups per CU the tile kernel may use (LDS permitting): 2 unless DLAMD_WG_PER_CU=1
@@ -277,14 +278,38 @@ int plan_mix(const dl_mix_args *a, Plan *pl) {
             return fail(DL_ERR_INVALID, "dl_mix_round: tile_cols %d does not fit this graph "
                                         "(%d rows); query dl_mix_plan_query on row-major args",
                         a->tile_cols, R);
-        const int64_t n_tiles = (a->n_params + a->tile_cols - 1) / a->tile_cols;
+        int64_t n_tiles = (a->n_params + a->tile_cols - 1) / a->tile_cols;
+        // tile groups: a halo round of few source rows (the split scheme's boundary launch,
+        // 276 rows at 16 columns: 18 KB a tile, latency-bound) walks g <= 8 consecutive data tiles
+        // as one kernel tile of 4cg columns, at <= 4 row passes per thread (the halo kernel's
+        // limit); DLAMD_TILE_GROUP=g caps g (1: off, a measurement knob)
+        int g = 1, cg = c;
+        int64_t lds_g = lds;
+        if (a->n_halo > 0) {
+            int gcap = 8;
+            if (const char *v = getenv("DLAMD_TILE_GROUP")) gcap = atoi(v);
+            for (int gg = 8; gg >= 2; gg >>= 1) {
+                if (gg > gcap) continue;
+                const int cc = c * gg;
+                const int64_t l = (int64_t)R * cc * 16 + csr +
+                                  (want_dev ? (int64_t)(dl::kTileThreads / 64) * cc * 16 : 0);
+                if (cc > dl::kMaxChunks || n_tiles % gg ||
+                    (int64_t)R * cc > 4 * (int64_t)dl::kTileThreads || l > dl::kLdsBytes)
+                    continue;
+                g = gg;
+                cg = cc;
+                lds_g = l;
+                break;
+            }
+        }
+        n_tiles /= g;
         // two 1024-thread workgroups per CU when LDS allows, except at C = 4, where the second
         // workgroup's LDS traffic (4 rows of 64 B per 16 lanes: the most bank conflicts of any
         // C) costs more than its extra loads in flight (measured 5.5 vs 5.8 TB/s at N = 1024;
         // the c4 rank of 8's 608-row halo round: 69.1 vs 70.1 % of spec, profiles/r11/session_c)
-        int bpc = (int)(dl::kLdsBytes / lds);
+        int bpc = (int)(dl::kLdsBytes / lds_g);
         if (bpc > wg_per_cu_cap()) bpc = wg_per_cu_cap();
-        if (c == 4) bpc = 1;
+        if (cg == 4) bpc = 1;
         const int64_t grid =
             balanced_grid(n_tiles, (int64_t)device_cus() * (bpc < 1 ? 1 : bpc) *
                                    grid_mult_for(n_tiles, (int64_t)device_cus() *
@@ -292,12 +317,13 @@ int plan_mix(const dl_mix_args *a, Plan *pl) {
         pl->pub.path = 1;
         pl->pub.tile_cols = a->tile_cols;
         pl->pub.grid = (int32_t)grid;
-        pl->pub.lds_bytes = (int32_t)lds;
+        pl->pub.lds_bytes = (int32_t)lds_g;
         pl->pub.n_tiles = (int32_t)n_tiles;
         pl->pub.regular = reg;
-        pl->chunks = c;
-        pl->csr_off = (uint32_t)tile;
-        pl->scratch_off = (uint32_t)(tile + csr);
+        pl->chunks = cg;
+        pl->grp = g;
+        pl->csr_off = (uint32_t)((int64_t)R * cg * 16);
+        pl->scratch_off = (uint32_t)((int64_t)R * cg * 16 + csr);
         return DL_OK;
     }
     if ((force_reg || (prefer_reg_tail(a->W, R, 1) && !force_gather)) && R <= 65535 &&
@@ -1156,6 +1182,10 @@ int dl_mix_round(const dl_mix_args *args, void *workspace, size_t ws_bytes, dl_s
             return fail(DL_ERR_WORKSPACE, "dl_mix_round: workspace %zu < %zu bytes", ws_bytes, need);
         t.csr_off = pl.csr_off;
         t.scratch_off = pl.scratch_off;
+        if (pl.grp > 1) {   // tile groups: chunk c of a kernel row -> data tile c / (T / 4)
+            t.grp = pl.grp;
+            t.cd_sh = __builtin_ctz((unsigned)(T / 4));
+        }
         float *partial = parts ? reinterpret_cast<float *>(ws) : nullptr;
         if (parts) t.dev_max_zero = reinterpret_cast<unsigned int *>(args->dev_max);
         int lds = pl.pub.lds_bytes;

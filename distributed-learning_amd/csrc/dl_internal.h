@@ -66,6 +66,11 @@ struct TileArgs {
     // {weight, row} pairs at LDS byte offset hub_off
     int32_t n_hub;
     uint32_t hub_off;
+    // column-tiled partition rounds (FAST): one kernel tile = `grp` consecutive data tiles of T
+    // columns (chunk c of a kernel row is chunk c & (2^cd_sh - 1) of data tile c >> cd_sh), so a
+    // short launch moves grp times the bytes per pass; grp = 1 (the default) is the plain tile
+    int32_t grp;
+    int32_t cd_sh;
 };
 constexpr int kMaxHaloBlocks = 16;
 

@@ -158,9 +158,19 @@ __device__ __forceinline__ float4 *at(float *base, uint32_t off) {
 //        (one ds_read_b64 per entry, +4 % on c4-ba); RAG = 1: fp32 weights then u16 rows (6 B,
 //        for tails that do not fit LDS at 8 B).  The fold runs the
 //        register head, then the tail, in CSR order: still the reference's left fold.
+// Waves per SIMD the compiler must leave room for: 8 (<= 64 VGPRs, two 1024-thread workgroups
+// per CU) for the grouped halo launch of few rows (C >= 8 at <= 3 passes, the split scheme's
+// boundary launch, latency-bound at one workgroup a CU), else no constraint
+template <int C, int KV, int HALO, bool LAG>
+constexpr int tile_waves_per_eu() {
+    return (HALO == 2 && C >= 8 && KV <= 3 && !LAG) ? 8 : 1;
+}
+
 template <int C, int KV, bool SGD, bool DEV, bool MIX, int HALO, bool FAST, int RD = 0,
           bool LAG = false, int RAG = 0>
-__global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
+__global__ void __attribute__((amdgpu_flat_work_group_size(1, kTileThreads),
+                               amdgpu_waves_per_eu(tile_waves_per_eu<C, KV, HALO, LAG>())))
+mix_tile_kernel(TileArgs a) {
     constexpr bool PACK = RAG == 2;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float4 *tile = reinterpret_cast<float4 *>(smem);
@@ -274,17 +284,25 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
     const int reg = a.regular;
 
     // FAST-path byte offsets: lane row s / chunk c; pass k adds k * step
-    // (row stride = ld*4 in the row-major layout, T*4 in the column-tiled one)
-    uint32_t ox = (uint32_t)s * a.xrs + 16u * c;
+    // (row stride = ld*4 in the row-major layout, T*4 in the column-tiled one).  Tile groups
+    // (a.grp > 1, column-tiled halo rounds): chunk c lies in data tile gt = c >> cd_sh of the group, at
+    // chunk c & (2^cd_sh - 1) of it -- gt data-tile strides further (< 4 GiB: 32-bit, checked
+    // by the host like every FAST offset)
+    const int grp = (HALO == 2 && a.grp > 1) ? a.grp : 1;   // the host groups halo rounds only
+    const int gt = grp > 1 ? c >> a.cd_sh : 0;
+    const uint32_t lc = 16u * (uint32_t)(grp > 1 ? c & ((1 << a.cd_sh) - 1) : c);
+    const uint32_t cx = lc + (uint32_t)gt * (uint32_t)a.xts;   // row 0's chunk c in x
+    const uint32_t cgx = SGD ? lc + (uint32_t)gt * (uint32_t)a.gts : 0u;
+    uint32_t ox = (uint32_t)s * a.xrs + cx;
     const uint32_t sx = (uint32_t)SLOTS * a.xrs;
-    uint32_t og = SGD ? (uint32_t)s * a.grs + 16u * c : 0u;
+    uint32_t og = SGD ? (uint32_t)s * a.grs + cgx : 0u;
     const uint32_t sg = SGD ? (uint32_t)SLOTS * a.grs : 0u;
-    uint32_t oy = (uint32_t)s * a.yrs + 16u * c;
+    uint32_t oy = (uint32_t)s * a.yrs + lc + (uint32_t)gt * (uint32_t)a.yts;
     const uint32_t sy = (uint32_t)SLOTS * a.yrs;
     // byte address of tile t's first element (row 0) in x / g / y
     auto tile_base = [&](const void *p, int64_t ts, int tile_id) {
         return reinterpret_cast<const char *>(p) + (a.tiled ? 0 : a.col_base * 4) +
-               (int64_t)tile_id * ts;
+               (int64_t)tile_id * grp * ts;
     };
     float4 *scratch = reinterpret_cast<float4 *>(smem + a.scratch_off);
 
@@ -294,12 +312,13 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
     // dynamic indexing of the kernel arguments).  Local passes keep 16c / 0 (not read).  Two
     // registers per pass: the host keeps this instantiation at KV <= 4 (no spills).
     constexpr bool HT = HALO == 2;
+    const int Td = T / grp;   // data tile width
     uint32_t hoff[HT ? KV : 1], hstr[HT ? KV : 1];
     if (HT) {
 #pragma unroll
         for (int k = 0; k < KV; ++k) {
             const int h = s + k * SLOTS - NL;
-            uint32_t o = 16u * c, st = 0u;
+            uint32_t o = lc, st = 0u;
             if (h >= 0 && h < R - NL) {
                 {
                     int r0 = 0, r1 = R - NL;
@@ -315,8 +334,9 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
                     for (int b = 1; b <= kMaxHaloBlocks; ++b)
                         if (b <= a.n_hblk && a.hblk_row0[b] > h && a.hblk_row0[b - 1] <= h)
                             r1 = a.hblk_row0[b];
-                    o += bo + (uint32_t)(h - r0) * (uint32_t)(T * 4);
-                    st = (uint32_t)(r1 - r0) * (uint32_t)(T * 4);
+                    o += bo + (uint32_t)(h - r0) * (uint32_t)(Td * 4);
+                    st = (uint32_t)(r1 - r0) * (uint32_t)(Td * 4);
+                    o += (uint32_t)gt * st;   // this chunk's data tile of the group
                 }
             }
             hoff[k] = o;
@@ -357,38 +377,38 @@ __global__ void __launch_bounds__(kTileThreads) mix_tile_kernel(TileArgs a) {
             // ldh; or per-peer tiled blocks, hoff/hstr); the per-lane base select keeps every
             // pass straight-line code
             const char *xt = tile_base(a.x, a.xts, tile_id);
-            const char *gt = SGD ? tile_base(a.g, a.gts, tile_id) : nullptr;
+            const char *gtb = SGD ? tile_base(a.g, a.gts, tile_id) : nullptr;
             const char *ht = reinterpret_cast<const char *>(a.halo) + (HT ? 0 : col0 * 4);
 #pragma unroll
             for (int k = 0; k < KV; ++k) {
                 const int r = s + k * SLOTS;
                 const bool loc = r < NL;
                 const bool ok = r < R;
-                const uint32_t oh = HT ? hoff[k] + (uint32_t)tile_id * hstr[k]
+                const uint32_t oh = HT ? hoff[k] + (uint32_t)(tile_id * grp) * hstr[k]
                                        : (uint32_t)(r - NL) * a.hrs + 16u * c;
                 const char *bx = loc || !ok ? xt : ht;
-                const uint32_t o1 = loc ? ox + k * sx : ok ? oh : 16u * c;
+                const uint32_t o1 = loc ? ox + k * sx : ok ? oh : cx;
                 const float4 *p1 = reinterpret_cast<const float4 *>(bx + o1);
                 px[k] = (a.nt_load & 1) ? nt_load4(p1) : *p1;
                 if (SGD) {
                     const float4 *p2 =
-                        reinterpret_cast<const float4 *>(gt + (loc ? og + k * sg : 16u * c));
+                        reinterpret_cast<const float4 *>(gtb + (loc ? og + k * sg : cgx));
                     pg[k] = (a.nt_load & 2) ? nt_load4(p2) : *p2;
                 }
             }
         } else if (FAST) {
             const float *xt = reinterpret_cast<const float *>(tile_base(a.x, a.xts, tile_id));
-            const float *gt =
+            const float *gtb =
                 SGD ? reinterpret_cast<const float *>(tile_base(a.g, a.gts, tile_id)) : nullptr;
             // one straight-line loop per load policy (bit 0: x non-temporal, bit 1: g)
             auto loads = [&](auto ntx, auto ntg) {
 #pragma unroll
                 for (int k = 0; k < KV; ++k) {
                     const bool ok = s + k * SLOTS < R;
-                    const float4 *p1 = at(xt, ok ? ox + k * sx : 16u * c);
+                    const float4 *p1 = at(xt, ok ? ox + k * sx : cx);
                     px[k] = decltype(ntx)::value ? nt_load4(p1) : *p1;
                     if (SGD) {
-                        const float4 *p2 = at(gt, ok ? og + k * sg : 16u * c);
+                        const float4 *p2 = at(gtb, ok ? og + k * sg : cgx);
                         pg[k] = decltype(ntg)::value ? nt_load4(p2) : *p2;
                     }
                 }

@@ -180,7 +180,9 @@ typedef struct dl_mix_plan {
     int32_t tile_cols;  /* T: columns per tile (path 1) */
     int32_t grid;       /* workgroups launched */
     int32_t lds_bytes;  /* dynamic LDS per workgroup */
-    int32_t n_tiles;
+    int32_t n_tiles;    /* tiles one launch walks; a column-tiled halo round of few source rows
+                           walks groups of 2, 4 or 8 consecutive data tiles as one (n_params /
+                           (tile_cols x group)), tile_cols staying the data layout's width */
     int32_t regular;    /* 1 if every row has the same entry count (CSR row_ptr not staged) */
     int32_t head;       /* (ABI 8) path 5: CSR entries per row kept in registers (2, 3 or 5);
                            path 4: 5; else 0 */

@@ -286,6 +286,11 @@ def test_c4_ranks_full_size_tiled(cuda, overlap, world):
         sh = sharding.HaloShard(pl, P, cuda, tr.endpoint(pl.rank), n_agents_total=n,
                                 overlap=overlap, chunk_cols=P // 8 if overlap == "chunks" else None)
         assert sh.layout == "tiled" and sh.halo_blocks == blocks
+        if overlap == "split" and sh.W_bnd_packed is not None:
+            # the boundary launch (276 / 372 / 384 source rows) walks groups of 2 / 4 / 8 data
+            # tiles as one kernel tile of 32 columns (dl_mix_plan.n_tiles)
+            bp = E.plan_shape(sh.W_bnd_packed, P, tile_cols=sh.T)
+            assert bp["tile_cols"] == sh.T and bp["n_tiles"] == P // 32, bp
         ids = torch.as_tensor(pl.local, device=cuda)
         sh.load_rows(X[ids])
         shards.append((sh, sh.layout_like(G[ids]), ids))

@@ -218,6 +218,7 @@ def test_tiled_halo_arguments_validate_without_a_gpu():
     _lib.check(lib.dl_mix_plan_shape(3000, 100, 1 << 16, 5 * 3000, 5, 1, 1, -1, ctypes.byref(pl)),
                "plan")
     assert (3100 * pl.tile_cols // 4) <= 4 * 1024
+    assert pl.n_tiles * pl.tile_cols == 1 << 16            # no tile groups at 3100 rows
 
     def args(**kw):
         a = _lib.DlMixArgs()
@@ -325,3 +326,31 @@ def test_trace_plan_refusals_match_the_header():
     assert rc == _lib.DL_ERR_UNSUPPORTED and b"multiple of 4" in msg
     rc, msg = plan(n_halo=4, halo=1 << 39, ldh=4096)
     assert rc == _lib.DL_ERR_UNSUPPORTED and b"halo" in msg
+
+
+def test_tile_groups_plan_without_a_gpu(monkeypatch):
+    """A column-tiled halo round of few source rows walks g consecutive data tiles as one kernel
+    tile (the split scheme's boundary launch: 92 output rows over 276 sources at T = 16 -> g = 2;
+    372 at T = 8 -> 4; 384 at T = 4 -> 8): n_tiles counts kernel tiles, tile_cols stays the data
+    width, the kernel keeps <= 4 row passes per thread; DLAMD_TILE_GROUP=1 turns groups off, and
+    the whole round's 608 rows or a round without halo rows never group (runs without a GPU)."""
+    from distributed_learning_amd import _lib
+    lib = _lib.load()
+    P = 1 << 18
+
+    def plan(rows, halo, T):
+        pl = _lib.DlMixPlan()
+        _lib.check(lib.dl_mix_plan_shape(rows, halo, P, 5 * rows, 5, 1, 1, T, ctypes.byref(pl)),
+                   "plan")
+        assert pl.path == 1 and pl.tile_cols == T
+        return pl
+    for rows, halo, T, g in [(92, 184, 16, 2), (124, 248, 8, 4), (128, 256, 4, 8)]:
+        pl = plan(rows, halo, T)
+        assert pl.n_tiles == P // (T * g), (rows, halo, T, pl.n_tiles)
+        assert (rows + halo) * (T * g // 4) <= 4 * 1024
+    assert plan(512, 96, 16).n_tiles == P // 16
+    assert plan(276, 0, 16).n_tiles == P // 16
+    monkeypatch.setenv("DLAMD_TILE_GROUP", "1")
+    assert plan(92, 184, 16).n_tiles == P // 16
+    monkeypatch.setenv("DLAMD_TILE_GROUP", "2")
+    assert plan(124, 248, 8).n_tiles == P // 16

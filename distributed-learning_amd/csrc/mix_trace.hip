@@ -253,27 +253,21 @@ __global__ void __launch_bounds__(kTileThreads) mix_trace_rows_kernel(TileArgs a
     float4 *img0 = reinterpret_cast<float4 *>(smem);
     float4 *img1 = img0 + N * C;
     float4 *scratch = reinterpret_cast<float4 *>(smem + a.scratch_off);   // [16][C]
-    uint32_t coff[KV][RE];
     float wreg[RE];
 #pragma unroll
     for (int e = 0; e < RE; ++e) wreg[e] = a.w[e];
+    // own operand: when every row's first CSR entry is the row itself (W = I - L(w)), the thread
+    // that produced agent ag's chunk in round r folds it from a register in round r + 1 -- four
+    // LDS reads a row instead of five (as in mix_multi_kernel); a wave vote picks the
+    // instantiation.  The LDS offsets (< 64 KiB: N <= 1024 rows of 64 B) are packed two to a
+    // register, which pays for the own values' registers
+    bool self_ok = true;
 #pragma unroll
     for (int k = 0; k < KV; ++k) {
         const int ag = FULL || s + k * SLOTS < N ? s + k * SLOTS : 0;
-#pragma unroll
-        for (int e = 0; e < RE; ++e) coff[k][e] = ((uint32_t)a.col[ag * RE + e] * C + c) * 16u;
+        self_ok = self_ok && a.col[ag * RE] == ag;
     }
-    // the fold as (x, y) / (z, w) pairs (fold2), the five neighbour reads issued first
-    auto mix = [&](const float4 *src, int k, f32x2 &lo, f32x2 &hi) {
-        const char *base = reinterpret_cast<const char *>(src);
-        f32x4 v[RE];
-#pragma unroll
-        for (int e = 0; e < RE; ++e) v[e] = *reinterpret_cast<const f32x4 *>(base + coff[k][e]);
-        lo = f32x2{0.f, 0.f};
-        hi = f32x2{0.f, 0.f};
-#pragma unroll
-        for (int e = 0; e < RE; ++e) fold2(lo, hi, wreg[e], v[e]);
-    };
+    const bool self0 = __all(self_ok);
     const int lsh = __builtin_ctz((unsigned)a.lchunks);
     const int64_t lmask = (int64_t)a.lchunks - 1;
     auto off = [&](int64_t ts, int64_t row, int64_t q) {
@@ -294,6 +288,39 @@ __global__ void __launch_bounds__(kTileThreads) mix_trace_rows_kernel(TileArgs a
             px[k] = tr_load4(xb + off(a.xts, (int64_t)ag * a.xrs, q * C + c));
         }
     };
+    auto tiles = [&](auto selfc) {
+    constexpr bool SELF = decltype(selfc)::value;
+    constexpr int E0 = SELF ? 1 : 0;              // first entry read from LDS
+    constexpr int NO = (RE - E0 + 1) / 2;         // offset registers per pass (two per register)
+    uint32_t coff[KV][NO];
+#pragma unroll
+    for (int k = 0; k < KV; ++k) {
+        const int ag = FULL || s + k * SLOTS < N ? s + k * SLOTS : 0;
+#pragma unroll
+        for (int j = 0; j < NO; ++j) {
+            const int e = E0 + 2 * j;
+            const uint32_t o1 = ((uint32_t)a.col[ag * RE + e] * C + c) * 16u;
+            const uint32_t o2 = e + 1 < RE ? ((uint32_t)a.col[ag * RE + e + 1] * C + c) * 16u : 0u;
+            coff[k][j] = o1 | (o2 << 16);
+        }
+    }
+    float4 selfv[SELF ? KV : 1];   // this thread's agents' chunks of the current round
+    // the fold as (x, y) / (z, w) pairs (fold2), the neighbour reads issued first
+    auto mix = [&](const float4 *src, int k, f32x2 &lo, f32x2 &hi) {
+        const char *base = reinterpret_cast<const char *>(src);
+        f32x4 v[RE];
+        if (SELF) v[0] = f32x4{selfv[k].x, selfv[k].y, selfv[k].z, selfv[k].w};
+#pragma unroll
+        for (int e = E0; e < RE; ++e) {
+            const uint32_t w2 = coff[k][(e - E0) >> 1];
+            const uint32_t o = (e - E0) & 1 ? w2 >> 16 : w2 & 0xffffu;
+            v[e] = *reinterpret_cast<const f32x4 *>(base + o);
+        }
+        lo = f32x2{0.f, 0.f};
+        hi = f32x2{0.f, 0.f};
+#pragma unroll
+        for (int e = 0; e < RE; ++e) fold2(lo, hi, wreg[e], v[e]);
+    };
     int64_t q = blockIdx.x;
     if (q < nsteps) prefetch(q);
     for (; q < nsteps; q += gridDim.x) {
@@ -301,6 +328,7 @@ __global__ void __launch_bounds__(kTileThreads) mix_trace_rows_kernel(TileArgs a
 #pragma unroll
         for (int k = 0; k < KV; ++k) {
             const int ag = s + k * SLOTS;
+            if (SELF) selfv[k] = px[k];
             if (FULL || ag < N) {
                 img0[ag * C + c] = px[k];
                 cs.x += px[k].x;
@@ -345,10 +373,12 @@ __global__ void __launch_bounds__(kTileThreads) mix_trace_rows_kernel(TileArgs a
                     f32x2 lo, hi;
                     mix(src, k, lo, hi);
                     const float4 y = make_float4(lo.x, lo.y, hi.x, hi.y);
-                    if (!last)
+                    if (!last) {
                         dst[ag * C + c] = y;
-                    else
+                        if (SELF) selfv[k] = y;
+                    } else {
                         tr_store4(y, yb + off(a.yts, (int64_t)ag * a.yrs, q * C + c));
+                    }
                     v = dev2(lo, hi, mlo, mhi);
                 }
                 v += quad_xor1(v);   // the agent's 4 chunk lanes (whole wave active)
@@ -366,6 +396,11 @@ __global__ void __launch_bounds__(kTileThreads) mix_trace_rows_kernel(TileArgs a
             if (r + 1 < rounds) round(false, dacc[r]);
         round(true, dlast);
     }
+    };
+    if (self0)
+        tiles(std::true_type{});
+    else
+        tiles(std::false_type{});
     const int mine_ag = s + c * SLOTS;
     if (c < KV && (FULL || mine_ag < N)) {
 #pragma unroll

@@ -310,6 +310,10 @@ int plan_mix(const dl_mix_args *a, Plan *pl) {
         int bpc = (int)(dl::kLdsBytes / lds_g);
         if (bpc > wg_per_cu_cap()) bpc = wg_per_cu_cap();
         if (cg == 4) bpc = 1;
+        // an ungrouped halo round's kernel takes > 64 VGPRs, so a second 1024-thread workgroup
+        // never shares the CU: a grid sized for two only queues them (rank-of 4 / 2 halo mix
+        // 1.5 / 2 % slower, profiles/r12/halo_grid/); the grouped one is held to 64 VGPRs
+        if (a->n_halo > 0 && g == 1) bpc = 1;
         const int64_t grid =
             balanced_grid(n_tiles, (int64_t)device_cus() * (bpc < 1 ? 1 : bpc) *
                                    grid_mult_for(n_tiles, (int64_t)device_cus() *

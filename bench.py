@@ -243,7 +243,37 @@ def kernel_name(plan, sgd, dev, n_src, halo=0, lag=False):
             f"{rag}>(dl::TileArgs)")
 
 
-PROFILE_C2 = os.path.join(ROOT, "profiles", "r12", "c2", "summary.json")
+# the c2 line's committed evidence: rocprofv3 kernel trace + PMC passes of the same bench line,
+# taken in the same gpurun call as the bench run saved beside it (bench.json)
+PROFILE_C2 = os.path.join(ROOT, "profiles", "r13", "c2", "summary.json")
+
+
+def profile_entry(kname, path=PROFILE_C2):
+    """The committed rocprofv3 summary entry of this kernel instance (calls, avg_us, median_us,
+    PMC bytes), or None if it was not profiled."""
+    try:
+        with open(path) as f:
+            kernels = json.load(f)["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None
+    for name, e in kernels.items():
+        if kname in name:
+            return e
+    return None
+
+
+def rocprof_fields(kname, bytes_per_launch, path=PROFILE_C2):
+    """roofline fields from the committed profile itself: its kernel average as a launch time
+    and the fraction of the HBM peak it implies (the same algorithmic bytes), beside the live
+    HIP-event figures, so the line's frac can be checked against the profile it cites."""
+    e = profile_entry(kname, path)
+    if e is None or not e.get("avg_us"):
+        return {}
+    out = {"rocprof_launch_ms": e["avg_us"] / 1e3,
+           "rocprof_frac": bytes_per_launch / (e["avg_us"] / 1e6) / 1e9 / HBM_PEAK_GBS}
+    if e.get("median_us"):
+        out["rocprof_median_ms"] = e["median_us"] / 1e3
+    return out
 
 
 def traffic_from_profile(kname, path=PROFILE_C2, bytes_hint=None):
@@ -1794,7 +1824,8 @@ def main():
                          "measured_copy_ceiling_GBs": ceiling,
                          "measured_triad_ceiling_GBs": triad,
                          "frac_of_measured_triad": achieved / triad,
-                         "stream_variants_GBs": ceiling_variants},
+                         "stream_variants_GBs": ceiling_variants,
+                         **rocprof_fields(kname, bytes_per_round)},
             "cpu_baseline": cpu,
             "final_max_deviation": dev_max,
             "fdla_weights": fdla,

@@ -310,10 +310,17 @@ int plan_mix(const dl_mix_args *a, Plan *pl) {
         int bpc = (int)(dl::kLdsBytes / lds_g);
         if (bpc > wg_per_cu_cap()) bpc = wg_per_cu_cap();
         if (cg == 4) bpc = 1;
-        // an ungrouped halo round's kernel takes > 64 VGPRs, so a second 1024-thread workgroup
-        // never shares the CU: a grid sized for two only queues them (rank-of 4 / 2 halo mix
-        // 1.5 / 2 % slower, profiles/r12/halo_grid/); the grouped one is held to 64 VGPRs
-        if (a->n_halo > 0 && g == 1) bpc = 1;
+        // two 1024-thread workgroups share a CU only at <= 64 VGPRs.  Of the column-tiled halo
+        // instantiations only those mix_tile.hip's tile_waves_per_eu caps are that small (C >= 8
+        // at <= 3 row passes without the lagged deviation: 53-64 VGPRs, no spills); every other
+        // one takes 66-123 (profiles/r13/vgprs.txt), so a grid sized for two would only queue
+        // them (rank-of 4 / 2 halo mix 1.5 / 2 % slower, profiles/r12/halo_grid/)
+        if (a->n_halo > 0) {
+            const int64_t slots = dl::kTileThreads / cg;
+            const bool capped = cg >= 8 && (R + slots - 1) / slots <= 3 && !a->mean_prev &&
+                                !a->colsum_out;
+            if (!capped) bpc = 1;
+        }
         const int64_t grid =
             balanced_grid(n_tiles, (int64_t)device_cus() * (bpc < 1 ? 1 : bpc) *
                                    grid_mult_for(n_tiles, (int64_t)device_cus() *
@@ -481,6 +488,10 @@ int check_mix_args(const dl_mix_args *a) {
     if (halo_round && a->mean_prev && !a->dev_sq && a->tile_cols <= 0)
         return fail(DL_ERR_INVALID, "dl_mix_round: partial rows without dev_sq need the "
                                     "column-tiled layout (one launch, plan grid rows)");
+    if (halo_round && a->mean_prev && !a->dev_sq && !a->partial_rows_out)
+        return fail(DL_ERR_INVALID, "dl_mix_round: a lagged halo round without dev_sq leaves its "
+                                    "deviation as partial rows: pass partial_rows_out (ABI 9) to "
+                                    "receive their count, or dev_sq for the reduced deviation");
     // extents: a tiled operand of `rows` used rows inside blocks of `ld` rows spans (tiles - 1)
     // block strides plus its used rows of the last tile
     const int64_t Tc = a->tile_cols;
@@ -1135,6 +1146,7 @@ int dl_mix_round(const dl_mix_args *args, void *workspace, size_t ws_bytes, dl_s
     g_err.clear();
     int rc = check_mix_args(args);
     if (rc) return rc;
+    if (args->partial_rows_out) *args->partial_rows_out = 0;
     Plan pl;
     rc = plan_mix(args, &pl);
     if (rc) return rc;
@@ -1235,9 +1247,13 @@ int dl_mix_round(const dl_mix_args *args, void *workspace, size_t ws_bytes, dl_s
         }
         if (parts) {
             if (Nr <= 1 && !lag) return zero_deviation(Nr, args->dev_sq, args->dev_max, s);
-            // a lagged round without dev_sq leaves its grid_full partial rows to the caller
-            // (column chunks reduced once, dl_row_sums); its dev_max, if any, the kernel zeroed
-            if (lag && !args->dev_sq) return DL_OK;
+            // a lagged round without dev_sq leaves its partial rows to the caller (column
+            // chunks reduced once, dl_row_sums) and says how many; its dev_max, if any, the
+            // kernel zeroed
+            if (lag && !args->dev_sq) {
+                *args->partial_rows_out = grid_full + grid_tail;
+                return DL_OK;
+            }
             hipError_t e = dl::launch_dev_reduce(partial, grid_full + grid_tail, Np, args->dev_sq,
                                                  args->dev_max, s, true);
             if (e != hipSuccess) return hip_fail(e, "dev_reduce launch");

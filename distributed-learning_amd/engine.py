@@ -203,8 +203,10 @@ def mix_round(W: DeviceCsr, X, Y, G=None, lr=0.0, halo=None, dev_sq=None, dev_ma
     Halo rounds (``halo`` rows): ``mean_prev`` (the global column mean of X), ``colsum_out`` and
     ``dev_sq`` together give the lagged deviation -- dev_sq = ||x_a - mean_prev||^2 of the
     INPUT rows, colsum_out = this rank's column sums of X - lr G (include/dlamd.h).  Without
-    dev_sq / dev_max (column-tiled only) the round leaves its [plan grid, n_local] partial rows
-    in ``workspace`` -- then a float32 tensor slice the caller reduces (``row_sums``)."""
+    dev_sq / dev_max (column-tiled only) the round leaves its [R, n_local] partial rows in
+    ``workspace`` -- then a float32 tensor slice the caller reduces (``row_sums``) -- and returns
+    R, which the ABI reports from the launch itself (dl_mix_args.partial_rows_out, ABI 9).
+    Otherwise returns None."""
     lib = _lib.load()
     if tiled is not None:
         P = tiled[0]
@@ -219,6 +221,16 @@ def mix_round(W: DeviceCsr, X, Y, G=None, lr=0.0, halo=None, dev_sq=None, dev_ma
                     t.dim() != 1 or t.stride(0) != 1:
                 raise ValueError(f"{name} must be a contiguous float32 [n_params] device tensor")
             setattr(args, name, _lib.ptr(t))
+    n_parts = None
+    if mean_prev is not None and dev_sq is None:
+        # the partial-rows mode: only into a caller-placed slice the caller reduces itself (with
+        # the internal workspace the partials would be dropped and the round have no deviation)
+        if not isinstance(workspace, torch.Tensor):
+            raise ValueError("a lagged halo round without dev_sq leaves its deviation partial "
+                             "rows in the workspace: pass dev_sq, or a tensor workspace to "
+                             "reduce with row_sums")
+        n_parts = ctypes.c_int32(-1)
+        args.partial_rows_out = ctypes.pointer(n_parts)
     if isinstance(workspace, torch.Tensor):   # a caller-placed slice (partial rows it reduces)
         if workspace.device != W.device or not workspace.is_contiguous():
             raise ValueError("a tensor workspace must be a contiguous tensor on W's device")
@@ -229,6 +241,7 @@ def mix_round(W: DeviceCsr, X, Y, G=None, lr=0.0, halo=None, dev_sq=None, dev_ma
                                                                W.n_src - W.n_local, P))
     _lib.check(lib.dl_mix_round(ctypes.byref(args), wp, wn, _lib.stream_handle(W.device)),
                "dl_mix_round")
+    return None if n_parts is None else int(n_parts.value)
 
 
 def mix_rounds(W: DeviceCsr, X, Y, rounds, G=None, lr=0.0, dev_sq=None, dev_max=None, mean=None,
@@ -519,7 +532,12 @@ class PerronRounds:
         self.y = torch.empty((n, P), dtype=tdt, device=self.device)
         self.w = torch.empty(n, dtype=torch.float64, device=self.device)
         self.it = torch.zeros(1, dtype=torch.int32, device=self.device)
-        self.conv_rows = None
+        # per-agent convergence eps (agents built with different convergence_eps): pinned
+        # staging + device buffer made once, copied only when the values change
+        self.h_conv = torch.empty(n, dtype=torch.float64, **pin)
+        self.h_conv_np = self.h_conv.numpy()
+        self.conv_rows = torch.empty(n, dtype=torch.float64, device=self.device)
+        self._conv_key = None
         self.rowptr, self.col = rowptr, col
         self.ws = Workspace(self.device)
         wp, wn = self.ws.ptr_size(lib.dl_perron_workspace_bytes(1 if tdt == torch.float64 else 0,
@@ -546,8 +564,13 @@ class PerronRounds:
             if conv_eps_rows is None:
                 a.conv_eps_rows = None
             else:
-                self.conv_rows = torch.as_tensor(np.asarray(conv_eps_rows, np.float64),
-                                                 device=self.device)
+                key = tuple(float(e) for e in conv_eps_rows)
+                if len(key) != self.n:
+                    raise ValueError(f"conv_eps_rows needs {self.n} entries (got {len(key)})")
+                if key != self._conv_key:
+                    self.h_conv_np[:] = key
+                    self.conv_rows.copy_(self.h_conv, non_blocking=True)
+                    self._conv_key = key
                 a.conv_eps_rows = _lib.ptr(self.conv_rows)
             _lib.check(self.lib.dl_perron_round(ctypes.byref(a), self.wp, self.wn,
                                                 _lib.stream_handle(self.device)),

@@ -561,17 +561,23 @@ class HipOps:
 
     def mix_partials(self, W, X, Y, G, lr, halo, mean_prev, colsum, parts, halo_blocks,
                      zero_max=None):
-        """A column-tiled lagged halo round that leaves its [plan grid, n_local] deviation
-        partial rows in ``parts`` (a float32 slice) instead of reducing them: the column chunks
-        of a round then share one ``row_sums`` over all their rows (one reduce launch a round,
-        not one per chunk).  ``zero_max``: a [1] buffer the kernel sets to 0 for that reduce."""
+        """A column-tiled lagged halo round that leaves its [R, n_local] deviation partial rows
+        at the start of ``parts`` (a float32 slice) instead of reducing them, and returns R as
+        the launch reports it (dl_mix_args.partial_rows_out): the column chunks of a round then
+        place their rows back to back and share one ``row_sums`` (one reduce launch a round, not
+        one per chunk).  ``zero_max``: a [1] buffer the kernel sets to 0 for that reduce."""
         tiled = (X.shape[0] * X.shape[2], X.shape[2])
-        self.E.mix_round(W, X, Y, G=G, lr=lr, halo=halo, mean_prev=mean_prev, colsum_out=colsum,
-                         dev_max=zero_max, workspace=parts, tiled=tiled, halo_blocks=halo_blocks)
+        return self.E.mix_round(W, X, Y, G=G, lr=lr, halo=halo, mean_prev=mean_prev,
+                                colsum_out=colsum, dev_max=zero_max, workspace=parts, tiled=tiled,
+                                halo_blocks=halo_blocks)
 
-    def partial_rows(self, W, width, tile_cols):
-        """Partial rows a column-tiled lagged round of ``width`` columns writes (its plan grid)."""
-        return int(self.E.plan_shape(W, width, deviation=True, tile_cols=tile_cols)["grid"])
+    def partial_rows_bound(self, W, width):
+        """At most this many partial rows a lagged round of ``width`` columns writes: the ABI's
+        own workspace bound (dl_mix_workspace_bytes) in rows of n_local floats."""
+        lib = self.E._lib.load()
+        nl = W.n_local
+        return int(lib.dl_mix_workspace_bytes(max(W.n_rows, nl), W.n_src - nl, int(width))) // \
+            (4 * nl) + 1
 
     def row_sums(self, parts, zeroed_max=None):
         """(sum over the rows of parts, max sqrt of it): a chunked round's deviation.
@@ -854,15 +860,15 @@ class HaloShard:
             dmax = torch.empty(1, dtype=torch.float32, device=self.device) if one else None
             prow = None if one else self._partial_rows(chunks)
             if prow is not None:
-                # column-tiled chunks: every chunk's kernel leaves its partial rows in its own
-                # slice of one buffer, and one row_sums reduces them all (no reduce per chunk)
-                # (flat, with slack: each chunk's slice runs to the end of the buffer, which
-                # covers the ABI's aligned size of its grid rows)
+                # column-tiled chunks: every chunk's kernel leaves its partial rows right after
+                # the previous chunk's in one buffer (the count each launch reports), and one
+                # row_sums reduces them all (no reduce per chunk).  Sized by the ABI's bound for
+                # every chunk, so a chunk's slice (to the end of the buffer) always holds its rows
                 nl = self.plan.n_local
-                flat = torch.empty(prow[-1] * nl + 64, dtype=torch.float32, device=self.device)
-                parts = flat[:prow[-1] * nl].view(prow[-1], nl)
+                flat = torch.empty(prow * nl + 64, dtype=torch.float32, device=self.device)
+                parts = None     # the rows actually written, after the chunks (_mix_all)
                 # the max's word, zeroed by the first chunk's kernel: no memset before the reduce
-                prow = (prow, flat, torch.empty(1, dtype=torch.float32, device=self.device))
+                prow = [0, flat, torch.empty(1, dtype=torch.float32, device=self.device)]
             else:
                 parts = torch.empty(len(chunks), self.plan.n_local, dtype=torch.float32,
                                     device=self.device)
@@ -879,7 +885,9 @@ class HaloShard:
         if dmax is not None:
             dev_sq, dev_max = parts[0], dmax
         elif lag[4] is not None:   # chunk partial rows: one launch, the max already zeroed
-            dev_sq, dev_max = self.ops.row_sums(parts, zeroed_max=lag[4][2])
+            rows, flat, zmax = lag[4]
+            parts = flat[:rows * self.plan.n_local].view(rows, self.plan.n_local)
+            dev_sq, dev_max = self.ops.row_sums(parts, zeroed_max=zmax)
         elif hasattr(self.ops, "row_sums"):   # chunks: one launch for the sum and the max
             dev_sq, dev_max = self.ops.row_sums(parts)
         else:
@@ -904,25 +912,87 @@ class HaloShard:
         must call this before the next ``round(deviation=True)``."""
         self._forget_mean()
 
+    # ---------------------------------------------------------------- Mixer.mix on the partition
+    # a lagged deviation this close to eps (relative, plus the mean-rounding floor) is
+    # re-evaluated exactly before the stop test uses it: the same rule as the single-device
+    # Mixer's traced passes (utils/consensus_simple/mixer.py, _TIE_RTOL)
+    TIE_RTOL = 2e-5
+
+    def mix(self, times=1, eps=None, max_rounds=1 << 20):
+        """``Mixer.mix(times, eps)`` (utils/consensus_simple/mixer.py:18-41) on the agent
+        partition: mix until ``(eps is None or max_a ||x_a - mean|| < eps) and done >= times``,
+        the deviation over ALL agents, and return ``times_done``; X is left at that iterate (the
+        reference writes it back into the models, :34-35).  Every rank calls it together.
+
+        With eps set, each round is a lagged one (``round(deviation=True)``): round k + 1 mixes
+        X_k and reports the deviation of X_k, so there is no deviation pass of its own.  When
+        that report meets the stop rule the loop has already computed X_{k+1}; X_k is still in
+        the ping-pong buffer and becomes X again -- the reference's iterate and round count,
+        at the price of one round beyond the reference's.  A report within rounding of eps is
+        re-evaluated on X_k with numpy's row-order column mean over every agent
+        (``exact_max_deviation``), so the integer round count does not depend on the lagged
+        mean's summation order.  The comparison is float32 against float32(eps), as numpy >= 2
+        compares the reference's np.float32 deviation with a Python float."""
+        n = int(self.n_total or 0)
+        if n <= 1:                       # len(topology) <= 1 (mixer.py:19-20)
+            return 0
+        target = int(np.ceil(times))     # `times_done >= times` with integer rounds
+        if eps is None:
+            for _ in range(target):
+                self.round()
+            return target
+        eps32 = np.float32(eps)
+        floor = None
+        k = 0
+        while True:
+            _, dmax = self.round(deviation=True)    # X_k -> X_{k+1}; reports X_k's deviation
+            d = np.float32(float(dmax.reshape(-1)[0]))
+            gap = abs(float(d) - float(eps32))
+            if gap <= 0.1 * abs(float(eps32)):
+                if floor is None:        # 8 sqrt(P) eps32 max|mean|, the Mixer's floor
+                    ref = self.mean_prev if self.mean_prev is not None else \
+                        self._global_mean(self.Y)
+                    floor = 8.0 * np.sqrt(self.P) * float(np.finfo(np.float32).eps) * \
+                        float(ref.abs().max())
+                if gap <= self.TIE_RTOL * abs(float(eps32)) + floor:
+                    d = self.exact_max_deviation(self.Y)
+            if d < eps32 and k >= target:
+                self.X, self.Y = self.Y, self.X      # back to X_k
+                self._forget_mean()
+                return k
+            k += 1
+            if k >= max_rounds:
+                raise RuntimeError(f"HaloShard.mix: no stop after {max_rounds} rounds "
+                                   f"(last max deviation {d}, eps {eps})")
+
+    def exact_max_deviation(self, A=None):
+        """max_a ||x_a - mean|| of the resident iterate A (default X) over every agent, with the
+        column mean summed in global agent order as numpy does (mixer.py:61) -- what
+        ``Mixer._recheck_deviation`` computes on one device.  Every rank places its rows at their
+        global ids in a zero matrix and the ranks all-reduce it (x + 0 is exact, so each rank then
+        holds the whole iterate), then the row-order column sum and the deviation.  A
+        collective, costing an N x P all-reduce: the stop rule calls it only on near-ties."""
+        A = self.X if A is None else A
+        n = int(self.n_total)
+        full = torch.zeros(n, self.P, dtype=torch.float32, device=self.device)
+        full[torch.as_tensor(np.asarray(self.plan.local, np.int64), device=self.device)] = \
+            self.rows(A)
+        self.transport.all_reduce_(full, "sum")
+        mean = self.ops.column_sum(full) / n
+        _, dmax = self.ops.deviation(full, mean)
+        return np.float32(float(dmax.reshape(-1)[0]))
+
     def _partial_rows(self, chunks):
-        """Row offsets of each column chunk's partial rows in one buffer ([0, g0, g0 + g1, ...]),
-        or None where chunks reduce one by one (row-major layout, ops without mix_partials,
-        rounds without halo rows)."""
+        """Rows of one buffer that holds every column chunk's partial rows back to back (the
+        ABI's bound per chunk, summed), or None where chunks reduce one by one (row-major
+        layout, ops without mix_partials, rounds without halo rows)."""
         # (n_local % 4: every chunk's slice starts 16-byte aligned; DLAMD_CHUNK_PARTIALS=0, a
         # measurement knob, keeps one reduce per chunk)
         if not (self.T and self.plan.n_halo and self.plan.n_local % 4 == 0 and
                 hasattr(self.ops, "mix_partials") and
                 os.environ.get("DLAMD_CHUNK_PARTIALS", "1") != "0"):
             return None
-        widths = sorted({c1 - c0 for c0, c1 in chunks})
-        key = (tuple(widths), self.T)
-        if getattr(self, "_prow_key", None) != key:
-            self._prow_grid = {w: self.ops.partial_rows(self.W, w, self.T) for w in widths}
-            self._prow_key = key
-        off = [0]
-        for c0, c1 in chunks:
-            off.append(off[-1] + self._prow_grid[c1 - c0])
-        return off
+        return sum(self.ops.partial_rows_bound(self.W, c1 - c0) for c0, c1 in chunks)
 
     def _mix_all(self, chunks, G, lr, lag):
         def post(j):
@@ -938,13 +1008,17 @@ class HaloShard:
             for w in works:
                 w.wait()
             if lag is not None and lag[4] is not None:   # partial rows, reduced after the loop
-                pr, flat, zmax = lag[4]
+                rows, flat, zmax = lag[4]
                 Gc = self._cols(G, c0, c1) if G is not None else None
-                self.ops.mix_partials(self.W, self._cols(self.X, c0, c1),
-                                      self._cols(self.Y, c0, c1), Gc, lr,
-                                      halo if self.plan.n_halo else None, lag[0][c0:c1],
-                                      lag[1][c0:c1], flat[pr[j] * self.plan.n_local:],
-                                      self.halo_blocks, zero_max=zmax if j == 0 else None)
+                got = self.ops.mix_partials(self.W, self._cols(self.X, c0, c1),
+                                            self._cols(self.Y, c0, c1), Gc, lr,
+                                            halo if self.plan.n_halo else None, lag[0][c0:c1],
+                                            lag[1][c0:c1], flat[rows * self.plan.n_local:],
+                                            self.halo_blocks, zero_max=zmax if j == 0 else None)
+                if not got or got < 0:
+                    raise RuntimeError(f"column chunk {j}: the lagged round reported {got} "
+                                       f"deviation partial rows")
+                lag[4][0] = rows + int(got)   # the next chunk's rows start after these
             else:
                 cl = None if lag is None else (lag[0][c0:c1], lag[1][c0:c1], lag[2][j], lag[3])
                 self.mix_chunk(c0, c1, halo, G, lr, cl)

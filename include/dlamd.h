@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define DLAMD_ABI_VERSION 8
+#define DLAMD_ABI_VERSION 9
 
 typedef void *dl_stream_t; /* hipStream_t; NULL = the legacy default stream */
 
@@ -128,11 +128,12 @@ typedef struct dl_mix_args {
                                the global column mean of x (the previous round's all-reduced
                                colsum_out / N): dev_sq[a] = ||x_a - mean_prev||^2, dev_max =
                                max sqrt (nullable).  With dev_sq NULL the round leaves its
-                               partial sums in the workspace instead -- rows [0, plan grid) of
-                               n_local_src floats, column-tiled layout only -- for the caller to
-                               reduce (one dl_row_sums over several column chunks' partial rows
-                               placed back to back); a dev_max is then only set to 0, for that
-                               dl_row_sums (max_zeroed = 1). */
+                               partial sums in the workspace instead -- rows [0, R) of
+                               n_local_src floats, column-tiled layout only, R written to
+                               *partial_rows_out (ABI 9: required in this mode) -- for the caller
+                               to reduce (one dl_row_sums over several column chunks' partial
+                               rows placed back to back); a dev_max is then only set to 0, for
+                               that dl_row_sums (max_zeroed = 1). */
     float *colsum_out;      /* nullable [n_params] (as mean_prev): sum over the local source rows of
                                the stepped inputs t = x - lr*g, in a fixed order.  Summed over all
                                ranks it is the column sum of the round's output when the global W
@@ -167,6 +168,13 @@ typedef struct dl_mix_args {
      * the last bits across n_hub_rows values.  The kernel uses fewer rows when their register
      * heads do not fit LDS. */
     int32_t n_hub_rows;
+    /* (ABI 9) nullable HOST pointer; REQUIRED in the partial-rows mode (a halo round with mean_prev
+     * and colsum_out but no dev_sq, see mean_prev), which is refused without it, so a caller that
+     * forgets dev_sq gets an error instead of a round with no deviation.  dl_mix_round writes the
+     * number of deviation partial rows the launch left in the workspace (0 when it wrote none)
+     * before it returns -- on the host, no synchronisation: a caller placing several column
+     * chunks' rows back to back starts the next chunk's slice there. */
+    int32_t *partial_rows_out;
 } dl_mix_args;
 
 /* Which kernel configuration dl_mix_round picks (introspection for tests and the bench). */
@@ -180,9 +188,11 @@ typedef struct dl_mix_plan {
     int32_t tile_cols;  /* T: columns per tile (path 1) */
     int32_t grid;       /* workgroups launched */
     int32_t lds_bytes;  /* dynamic LDS per workgroup */
-    int32_t n_tiles;    /* tiles one launch walks; a column-tiled halo round of few source rows
-                           walks groups of 2, 4 or 8 consecutive data tiles as one (n_params /
-                           (tile_cols x group)), tile_cols staying the data layout's width */
+    int32_t n_tiles;    /* tiles one launch walks.  (ABI 9) A column-tiled halo round of few
+                           source rows walks groups of 2, 4 or 8 consecutive data tiles as one
+                           kernel tile, so n_tiles = n_params / (tile_cols x group) and
+                           n_tiles x tile_cols < n_params there; tile_cols stays the data
+                           layout's width */
     int32_t regular;    /* 1 if every row has the same entry count (CSR row_ptr not staged) */
     int32_t head;       /* (ABI 8) path 5: CSR entries per row kept in registers (2, 3 or 5);
                            path 4: 5; else 0 */
@@ -346,7 +356,7 @@ int dl_from_tiled(const float *src, int32_t n_rows, int64_t n_params, int32_t ti
 int dl_column_sum(const float *x, int64_t ldx, int32_t n_rows, int64_t n_params, float *colsum,
                   dl_stream_t stream);
 
-/* sums[a] = sum_b parts[b][a] over n_parts rows of n_rows floats (fixed order, fp64), max_sqrt[0]
+/* (ABI 9) sums[a] = sum_b parts[b][a] over n_parts rows of n_rows floats (fixed order, fp64), max_sqrt[0]
  * = max_a sqrt(sums[a]); either output nullable.  The per-agent ||x_a - mean||^2 of a round run
  * as several column chunks (their partial rows back to back in parts, see mean_prev), and their
  * max -- the _get_max_deviation of mixer.py:51-55 over the whole round -- in one launch.

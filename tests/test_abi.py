@@ -27,8 +27,14 @@ def test_library_loads_and_exports_every_declared_symbol():
     for n in names:
         assert hasattr(lib, n), f"{n} declared in dlamd.h but not exported"
         assert n in _lib.SIGNATURES, f"{n} has no ctypes signature"
-    assert lib.dl_abi_version() == _lib.ABI_VERSION
+    assert lib.dl_abi_version() == _lib.ABI_VERSION == 9
     assert set(_lib.SIGNATURES) == set(names)
+    # (ABI 9) entries are tagged in the header
+    src = open(HEADER).read()
+    assert "#define DLAMD_ABI_VERSION 9" in src
+    for tagged in ("(ABI 9) sums[a] = sum_b parts", "(ABI 9) nullable HOST pointer",
+                   "(ABI 9) A column-tiled halo round"):
+        assert tagged in src, tagged
 
 
 def test_struct_layout_matches_c(tmp_path):
@@ -37,7 +43,7 @@ def test_struct_layout_matches_c(tmp_path):
     prog.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "dlamd.h"\n'
                     'int main(void){printf("%zu %zu %zu %zu %zu %zu %zu\\n",'
                     'sizeof(dl_csr), sizeof(dl_mix_args), offsetof(dl_mix_args, W),'
-                    'offsetof(dl_mix_args, lr), offsetof(dl_mix_args, mean),'
+                    'offsetof(dl_mix_args, lr), offsetof(dl_mix_args, partial_rows_out),'
                     'sizeof(dl_mix_plan), sizeof(dl_perron_args));'
                     'printf("%zu %zu %zu %zu %zu\\n", sizeof(dl_sgd_args), offsetof(dl_sgd_args, lr),'
                     'sizeof(dl_mlp_args), offsetof(dl_mlp_args, lr), sizeof(dl_bgemm_args));'
@@ -48,7 +54,8 @@ def test_struct_layout_matches_c(tmp_path):
     c = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True,
                                         check=True).stdout.split()]
     py = [ctypes.sizeof(_lib.DlCsr), ctypes.sizeof(_lib.DlMixArgs), _lib.DlMixArgs.W.offset,
-          _lib.DlMixArgs.lr.offset, _lib.DlMixArgs.mean.offset, ctypes.sizeof(_lib.DlMixPlan),
+          _lib.DlMixArgs.lr.offset, _lib.DlMixArgs.partial_rows_out.offset,
+          ctypes.sizeof(_lib.DlMixPlan),
           ctypes.sizeof(_lib.DlPerronArgs), ctypes.sizeof(_lib.DlSgdArgs),
           _lib.DlSgdArgs.lr.offset, ctypes.sizeof(_lib.DlMlpArgs), _lib.DlMlpArgs.lr.offset,
           ctypes.sizeof(_lib.DlBgemmArgs)]
@@ -262,8 +269,15 @@ def test_tiled_halo_arguments_validate_without_a_gpu():
     rc, msg = err(args(tile_cols=0, ldx=64, ldy=64, ldh=64, mean_prev=1 << 36,
                        colsum_out=(1 << 36) + 4096, dev_max=(1 << 36) + 8192))
     assert rc == _lib.DL_ERR_INVALID and b"column-tiled" in msg
+    # (ABI 9) the partial-rows mode needs partial_rows_out: a caller that forgets dev_sq gets an
+    # error, not a round whose deviation nobody reduces
     rc, msg = err(args(mean_prev=1 << 36, colsum_out=(1 << 36) + 4096))
+    assert rc == _lib.DL_ERR_INVALID and b"partial_rows_out" in msg
+    n_parts = ctypes.c_int32(-7)
+    rc, msg = err(args(mean_prev=1 << 36, colsum_out=(1 << 36) + 4096,
+                       partial_rows_out=ctypes.pointer(n_parts)))
     assert rc == _lib.DL_ERR_WORKSPACE, msg   # accepted: only the missing workspace is refused
+    assert n_parts.value == 0                  # cleared before anything can fail
     # dl_row_sums: outputs and sizes checked on the host
     assert lib.dl_row_sums(None, 2, 8, 1 << 20, None, 0, None) == _lib.DL_ERR_INVALID
     assert lib.dl_row_sums(1 << 20, 2, 8, None, None, 1, None) == _lib.DL_ERR_INVALID

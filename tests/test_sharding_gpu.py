@@ -314,3 +314,74 @@ def test_c4_ranks_full_size_tiled(cuda, overlap, world):
         for (dsq, dmax), (wsq, wmax) in zip(sh.got, want):
             np.testing.assert_allclose(dsq.cpu().numpy(), wsq[ids].cpu().numpy(), rtol=1e-5)
             assert float(dmax.item()) == pytest.approx(float(wmax.item()), rel=1e-5)
+
+
+class _Row(torch.nn.Module):
+    """One agent's flattened parameter vector as a model (Mixer flattens model.parameters())."""
+
+    def __init__(self, x):
+        super().__init__()
+        self.p = torch.nn.Parameter(x.clone())
+
+
+@pytest.mark.parametrize("overlap", ["split", "chunks"])
+@pytest.mark.parametrize("world", [8, 4, 2])
+def test_halo_mix_stop_rule_equals_single_device_mixer(cuda, world, overlap):
+    """HaloShard.mix(times, eps) -- Mixer.mix's stop rule (utils/consensus_simple/mixer.py:18-41)
+    on the agent partition, lagged rounds with a one-round rollback -- on 8 / 4 / 2 virtual ranks
+    of the c4 torus (64 x 64 agents, reduced to 4096 params): for several (times, eps), eps
+    strictly between two rounds' deviations and within a few ulps of one, times_done and every
+    agent's bits equal the single-device drop-in Mixer's on the same models."""
+    import logging
+    import math
+    from distributed_learning_amd.graph import from_edge_weights as few
+    from distributed_learning_amd.utils.consensus_simple import Mixer
+    from oracle import mixer_ref as M
+    rows = cols = 64
+    n, P = rows * cols, 4096
+    edges = torus_edges(rows, cols)
+    wc = 2.0 / (2.0 - 2.0 * math.cos(2 * math.pi / cols) + 8.0)
+    csr = few(edges, [wc] * len(edges), list(range(n)))
+    topo = {a: {int(csr.col[e]): float(csr.w[e]) for e in range(csr.rowptr[a], csr.rowptr[a + 1])}
+            for a in range(n)}
+    g = torch.Generator(device=cuda).manual_seed(17)
+    X0 = torch.randn(n, P, device=cuda, generator=g)
+    # the oracle's deviation sequence (mixer.py:51-66) picks the eps values
+    Xh, d = X0.cpu().numpy(), []
+    for _ in range(6):
+        d.append(np.float32(M.deviation(Xh).max()))
+        Xh = M.mix_once(Xh, csr.rowptr, csr.col, csr.w)
+    cases = [(1, float(np.sqrt(float(d[2]) * float(d[3])))), (4, float(np.sqrt(float(d[1]) *
+                                                                                float(d[2])))),
+             (0, float(d[0]) * 2), (1, float(d[4]) * (1 + 4e-7)), (2, None)]
+    plans = (sharding.split_halo_plans if overlap == "split" else sharding.halo_plans)(
+        csr, sharding.torus_block_partition(rows, cols, world))
+    for times, eps in cases:
+        models = {a: _Row(X0[a]) for a in range(n)}
+        want_n = Mixer(models, topo, logging.getLogger("test")).mix(times, eps)
+        want = torch.stack([models[a].p.data for a in range(n)])
+        tr = sharding.LocalTransport(world)
+        shards, errs = [], []
+        for pl in plans:
+            sh = sharding.HaloShard(pl, P, cuda, tr.endpoint(pl.rank), n_agents_total=n,
+                                    overlap=overlap,
+                                    chunk_cols=P // 2 if overlap == "chunks" else None)
+            ids = torch.as_tensor(pl.local, device=cuda)
+            sh.load_rows(X0[ids])
+            shards.append((sh, ids))
+
+        def run(sh):
+            try:
+                sh.done = sh.mix(times, eps)
+            except Exception as e:  # pragma: no cover
+                errs.append(e)
+        ths = [threading.Thread(target=run, args=(sh,)) for sh, _ in shards]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        assert not errs, errs
+        torch.cuda.synchronize()
+        for sh, ids in shards:
+            assert sh.done == want_n, (times, eps, sh.done, want_n)
+            assert torch.equal(sh.rows().view(torch.int32), want[ids].view(torch.int32))

@@ -40,6 +40,34 @@ __device__ __forceinline__ void nt_store4(float4 v, float4 *p) {
     __builtin_nontemporal_store(x, reinterpret_cast<f32x4 *>(p));
 }
 
+// FAST-path streams of a tile through buffer instructions whose cache policy is an immediate.
+// The non-temporal hint is a runtime choice (dl::TileArgs nt_load / nt_store), and two global
+// accesses that differ only in it are one instruction to the optimizer, which merged the two
+// arms of that choice and dropped the hint (round 5: every load and store of the c2 round plain,
+// 446 -> 427 rounds/s on one box).  Buffer loads and stores carry the policy as an operand that
+// must stay a constant, so the arms stay two instructions; tests/test_kernel_isa.py checks the
+// built code object for them.  Base = a uniform tile pointer, 32-bit offsets as for the global
+// forms (the host admits this path only when every operand spans < 4 GiB); the resource's
+// record count is the whole 32-bit range, so no access is clipped.
+constexpr int kBufNT = 2;   // cache-policy operand: nt (gfx950)
+typedef unsigned int u32x4v __attribute__((vector_size(16)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void *base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, -1, 0x00020000);
+}
+
+template <int AUX>
+__device__ __forceinline__ float4 buf_ld4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    const f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, AUX));
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+
+template <int AUX>
+__device__ __forceinline__ void buf_st4(float4 v, __amdgpu_buffer_rsrc_t r, uint32_t off) {
+    const f32x4 x = {v.x, v.y, v.z, v.w};
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, x), r, off, 0, AUX);
+}
+
 // Load 4 consecutive floats starting at column c0 of `row`; columns >= P read as 0.
 __device__ __forceinline__ float4 ld4(const float *__restrict__ row, int64_t c0, int64_t P,
                                       bool vec) {
@@ -94,6 +122,9 @@ __device__ __forceinline__ void add4(float4 &a, float4 b) {
 // order: the sum is the same IEEE add); xor 4 / 8 stay ds_bpermute.  Bit-identical to
 // v + __shfl_xor(v, m) (a + b == b + a).
 __device__ __forceinline__ float xor_add(float v, int m) {
+#ifdef DL_AB_SHFL
+    return v + __shfl_xor(v, m);
+#endif
     if (m == 1)
         return v + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true));
     if (m == 2)
@@ -117,16 +148,6 @@ __device__ __forceinline__ float4 shfl_xor4(float4 v, int m) {
     v.z = xor_add(v.z, m);
     v.w = xor_add(v.w, m);
     return v;
-}
-
-// Offsets of one operand matrix inside a column tile, in BYTES: per lane (row s, chunk c) and
-// per prefetch pass (SLOTS rows further down).  32-bit: the host only picks this kernel when
-// every operand spans < 4 GiB, so loads use the uniform-base + 32-bit VGPR-offset form.
-__device__ __forceinline__ const float4 *at(const float *base, uint32_t off) {
-    return reinterpret_cast<const float4 *>(reinterpret_cast<const char *>(base) + off);
-}
-__device__ __forceinline__ float4 *at(float *base, uint32_t off) {
-    return reinterpret_cast<float4 *>(reinterpret_cast<char *>(base) + off);
 }
 
 // C    : float4 chunks per row in a tile (T = 4*C columns)
@@ -359,7 +380,11 @@ mix_tile_kernel(TileArgs a) {
     // and the row group's C lanes are summed ONCE, after the last tile -- no cross-lane
     // reduction per pass and tile (log2 C ds_bpermutes per pass: at c3's 256 x 164,608 round
     // they were 20-30 us of a 117-us launch, scripts/c3_scale_probe.py)
+#ifdef DL_AB_NO_LD
+    constexpr bool LD = false;
+#else
     constexpr bool LD = DEV && C > 1 && KV <= 4;
+#endif
 
     float ldev[LD ? KV : 1];
 #pragma unroll
@@ -397,28 +422,24 @@ mix_tile_kernel(TileArgs a) {
                 }
             }
         } else if (FAST) {
-            const float *xt = reinterpret_cast<const float *>(tile_base(a.x, a.xts, tile_id));
-            const float *gtb =
-                SGD ? reinterpret_cast<const float *>(tile_base(a.g, a.gts, tile_id)) : nullptr;
+            const __amdgpu_buffer_rsrc_t rx = buf_rsrc(tile_base(a.x, a.xts, tile_id));
+            const __amdgpu_buffer_rsrc_t rg = buf_rsrc(SGD ? tile_base(a.g, a.gts, tile_id)
+                                                           : tile_base(a.x, a.xts, tile_id));
             // one straight-line loop per load policy (bit 0: x non-temporal, bit 1: g)
-            auto loads = [&](auto ntx, auto ntg) {
+            auto loads = [&](auto ax, auto ag) {
 #pragma unroll
                 for (int k = 0; k < KV; ++k) {
                     const bool ok = s + k * SLOTS < R;
-                    const float4 *p1 = at(xt, ok ? ox + k * sx : cx);
-                    px[k] = decltype(ntx)::value ? nt_load4(p1) : *p1;
-                    if (SGD) {
-                        const float4 *p2 = at(gtb, ok ? og + k * sg : cgx);
-                        pg[k] = decltype(ntg)::value ? nt_load4(p2) : *p2;
-                    }
+                    px[k] = buf_ld4<decltype(ax)::value>(rx, ok ? ox + k * sx : cx);
+                    if (SGD) pg[k] = buf_ld4<decltype(ag)::value>(rg, ok ? og + k * sg : cgx);
                 }
             };
-            using T1 = std::true_type;
-            using F0 = std::false_type;
-            if (a.nt_load == 3) loads(T1{}, T1{});
-            else if (a.nt_load == 1) loads(T1{}, F0{});
-            else if (a.nt_load == 2) loads(F0{}, T1{});
-            else loads(F0{}, F0{});
+            using NT = std::integral_constant<int, kBufNT>;
+            using PL = std::integral_constant<int, 0>;
+            if (a.nt_load == 3) loads(NT{}, NT{});
+            else if (a.nt_load == 1) loads(NT{}, PL{});
+            else if (a.nt_load == 2) loads(PL{}, NT{});
+            else loads(PL{}, PL{});
         } else {
             const int64_t cc = col0 + 4 * c;
 #pragma unroll
@@ -441,7 +462,11 @@ mix_tile_kernel(TileArgs a) {
     // weights: c2, c3, c4): the 5 weights in scalar registers from row 0's CSR, the row's 5
     // column ids and then its 5 tile values read back to back -- 6 LDS round trips a row
     // become 2 (the same products and sums in the same order: the same bits)
+#ifdef DL_AB_NO_REG5
+    const bool reg5 = false;
+#else
     const bool reg5 = MIX && RD == 0 && KV <= 4 && reg == 5 && wshared;
+#endif
     float w5[5];
 #pragma unroll
     for (int e = 0; e < 5; ++e) w5[e] = reg5 ? a.w[e] : 0.f;
@@ -653,16 +678,26 @@ mix_tile_kernel(TileArgs a) {
     };
 
     int tile_id = blockIdx.x;
-    if (tile_id < a.n_tiles) prefetch(tile_id);
-    // the LDS CSR is staged after the first tile's loads are issued: its loads (an L2 hit for
-    // every workgroup but the first) then wait behind the tile's instead of delaying them, and
-    // the first staging barrier below publishes it
+#ifdef DL_AB_CSR_EARLY
     if (RD == 0 && MIX) {
         for (int i = tid; i < a.n_w; i += NT) lw[i] = a.w[i];
         for (int i = tid; i < nnz; i += NT) lcol[i] = (uint16_t)a.col[i];
         if (!a.regular)
             for (int i = tid; i <= Nr; i += NT) lrp[i] = (uint16_t)a.rowptr[i];
     }
+#endif
+    if (tile_id < a.n_tiles) prefetch(tile_id);
+    // the LDS CSR is staged after the first tile's loads are issued: its loads (an L2 hit for
+    // every workgroup but the first) then wait behind the tile's instead of delaying them, and
+    // the first staging barrier below publishes it
+#ifndef DL_AB_CSR_EARLY
+    if (RD == 0 && MIX) {
+        for (int i = tid; i < a.n_w; i += NT) lw[i] = a.w[i];
+        for (int i = tid; i < nnz; i += NT) lcol[i] = (uint16_t)a.col[i];
+        if (!a.regular)
+            for (int i = tid; i <= Nr; i += NT) lrp[i] = (uint16_t)a.rowptr[i];
+    }
+#endif
     for (; tile_id < a.n_tiles; tile_id += gridDim.x) {
         // opaque per tile: keeps LICM from hoisting one offset register per pass
         asm volatile("" : "+v"(ox), "+v"(og), "+v"(oy));
@@ -706,7 +741,9 @@ mix_tile_kernel(TileArgs a) {
             // register-head + LDS-tail kernel, one workgroup per CU, 10 % slower too: c4-ba 327
             // vs 361 rounds/s).  And ahead of the tile mean's scratch reads (-1 to -5 us on c3's
             // 100-us round, profiles/r12)
+#ifndef DL_AB_PF_LATE
             if (nxt < a.n_tiles) prefetch(nxt);
+#endif
             float4 mean_t = zero4();
             if (mfi || lsum) {
 #pragma unroll
@@ -718,6 +755,9 @@ mix_tile_kernel(TileArgs a) {
                 mean_t.z = mean_t.z / n;
                 mean_t.w = mean_t.w / n;
             }
+#ifdef DL_AB_PF_LATE
+            if (nxt < a.n_tiles) prefetch(nxt);
+#endif
             float *yt = const_cast<float *>(
                 reinterpret_cast<const float *>(tile_base(a.y, a.yts, tile_id)));
             float4 cs = zero4();
@@ -737,12 +777,13 @@ mix_tile_kernel(TileArgs a) {
                     }
                 }
             }
+            const __amdgpu_buffer_rsrc_t ry = buf_rsrc(yt);
             auto store_y = [&](int k, int ag, const float4 &acc) {
                 if (FAST) {
                     if (a.nt_store)
-                        nt_store4(acc, at(yt, oy + (uint32_t)k * sy));
+                        buf_st4<kBufNT>(acc, ry, oy + (uint32_t)k * sy);
                     else
-                        *at(yt, oy + (uint32_t)k * sy) = acc;
+                        buf_st4<0>(acc, ry, oy + (uint32_t)k * sy);
                 } else {
                     st4(a.y + (int64_t)ag * a.ldy, col0 + 4 * c, P, false, acc);
                 }

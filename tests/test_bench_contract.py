@@ -162,3 +162,41 @@ def test_cpu_record_of_a_halo_rank(bench):
     whole = bench.cpu_record(csr, 64, 256, 64, 1e-3, "_get_deviation_dict")
     assert whole["value"] > 0 and "halo" not in whole["sample"]
     assert bench.sample_cols(type("A", (), {"cpu_cols": 1 << 18})(), 4096) == 1 << 15
+
+
+def _c2_evidence(bench):
+    """(the bench line saved beside the c2 profile, its kernel's summary entry): both from ONE
+    gpurun call (scripts/r13_c2.sh), the directory bench.PROFILE_C2 names."""
+    import json
+    d = os.path.dirname(bench.PROFILE_C2)
+    with open(os.path.join(d, "bench.json")) as f:
+        line = json.loads([ln for ln in f.read().splitlines() if ln.startswith("{")][-1])
+    name = bench.kernel_name({"tile_cols": 16, "path": 1}, sgd=True, dev=True, n_src=1024)
+    return line, bench.profile_entry(name)
+
+
+def test_c2_profile_backs_its_bench_line(bench):
+    """the headline's cited profile must be evidence for the line's time.  The
+    committed c2 profile was taken in the same call as the bench run saved beside it; its
+    mix_tile_kernel average may not imply a round slower than that run's HIP-event launch time
+    by more than 5 %, and the frac the line reports and the one the profile implies agree
+    within 3 %."""
+    line, e = _c2_evidence(bench)
+    assert e is not None and e["calls"] >= 20
+    rf = line["roofline"]
+    assert e["avg_us"] / 1e3 <= 1.05 * rf["launch_ms"], (e["avg_us"], rf["launch_ms"])
+    prof_frac = rf["bytes_per_launch"] / (e["avg_us"] / 1e6) / 1e9 / bench.HBM_PEAK_GBS
+    assert abs(prof_frac / rf["frac"] - 1) < 0.03, (prof_frac, rf["frac"])
+    # and the kernel average is no slower than the whole round the same run timed
+    assert e["avg_us"] / 1e3 <= line["ms_per_step"] * 1.0 + 1e-9
+
+
+def test_c2_line_reports_its_profile_fields(bench):
+    """rocprof_frac / rocprof_launch_ms on the c2 line come from the cited summary itself."""
+    _, e = _c2_evidence(bench)
+    name = bench.kernel_name({"tile_cols": 16, "path": 1}, sgd=True, dev=True, n_src=1024)
+    f = bench.rocprof_fields(name, 12 * 1024 * 2 ** 20)
+    assert f["rocprof_launch_ms"] == e["avg_us"] / 1e3
+    assert abs(f["rocprof_frac"] - 12 * 1024 * 2 ** 20 / (e["avg_us"] * 1e3) /
+               bench.HBM_PEAK_GBS) < 1e-12
+

@@ -1229,6 +1229,10 @@ int dl_mix_round(const dl_mix_args *args, void *workspace, size_t ws_bytes, dl_s
         if (grid_full > 0) {
             t.n_tiles = (int32_t)n_full;
             t.col_base = 0;
+            // DLAMD_TILE_RUN=1 (measurement knob): each workgroup walks one contiguous run of
+            // tiles instead of every grid-th tile
+            if (const char *v = getenv("DLAMD_TILE_RUN"))
+                if (v[0] == '1') t.tile_run = (int32_t)((n_full + grid_full - 1) / grid_full);
             t.dev_partial = partial;
             hipError_t e = reg_csr ? dl::launch_mix_tile_reg(t, pl.chunks, pl.head, pl.tail_fmt,
                                                              sgd, pl.dev, grid_full, lds, s)
@@ -1240,6 +1244,7 @@ int dl_mix_round(const dl_mix_args *args, void *workspace, size_t ws_bytes, dl_s
             if (reg_csr) return fail(DL_ERR_INVALID, "dl_mix_round: register-CSR plan with a tail");
             t.n_tiles = (int32_t)n_tail;
             t.col_base = n_full * T;
+            t.tile_run = 0;
             t.dev_partial = parts ? partial + (size_t)grid_full * Np : nullptr;
             hipError_t e = dl::launch_mix_tile(t, pl.chunks, sgd, pl.dev, true, grid_tail,
                                                lds, false, s);

@@ -71,6 +71,8 @@ struct TileArgs {
     // short launch moves grp times the bytes per pass; grp = 1 (the default) is the plain tile
     int32_t grp;
     int32_t cd_sh;
+    int32_t tile_run;          // 0: workgroup b walks tiles b, b + grid, ...; > 0: the run
+                               // [b * tile_run, (b + 1) * tile_run) (DLAMD_TILE_RUN, a knob)
 };
 constexpr int kMaxHaloBlocks = 16;
 

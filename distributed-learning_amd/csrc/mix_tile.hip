@@ -677,7 +677,10 @@ mix_tile_kernel(TileArgs a) {
         for (int j = 0; j < ND; ++j) dacc[j] += (mine && j == k / C) ? v : 0.f;
     };
 
-    int tile_id = blockIdx.x;
+    const int trun = a.tile_run;
+    int tile_id = trun ? (int)blockIdx.x * trun : (int)blockIdx.x;
+    const int tile_end = trun ? min(tile_id + trun, a.n_tiles) : a.n_tiles;
+    const int tstep = trun ? 1 : (int)gridDim.x;
 #ifdef DL_AB_CSR_EARLY
     if (RD == 0 && MIX) {
         for (int i = tid; i < a.n_w; i += NT) lw[i] = a.w[i];
@@ -686,7 +689,7 @@ mix_tile_kernel(TileArgs a) {
             for (int i = tid; i <= Nr; i += NT) lrp[i] = (uint16_t)a.rowptr[i];
     }
 #endif
-    if (tile_id < a.n_tiles) prefetch(tile_id);
+    if (tile_id < tile_end) prefetch(tile_id);
     // the LDS CSR is staged after the first tile's loads are issued: its loads (an L2 hit for
     // every workgroup but the first) then wait behind the tile's instead of delaying them, and
     // the first staging barrier below publishes it
@@ -698,11 +701,11 @@ mix_tile_kernel(TileArgs a) {
             for (int i = tid; i <= Nr; i += NT) lrp[i] = (uint16_t)a.rowptr[i];
     }
 #endif
-    for (; tile_id < a.n_tiles; tile_id += gridDim.x) {
+    for (; tile_id < tile_end; tile_id += tstep) {
         // opaque per tile: keeps LICM from hoisting one offset register per pass
         asm volatile("" : "+v"(ox), "+v"(og), "+v"(oy));
         const int64_t col0 = a.col_base + (int64_t)tile_id * T;
-        const int nxt = tile_id + gridDim.x;
+        const int nxt = tile_id + tstep;
         if (MIX) {
             // stage the (stepped) tile of every source row in LDS
             float4 cst = zero4();  // column partial sums of t (doubly stochastic W only)
@@ -742,7 +745,7 @@ mix_tile_kernel(TileArgs a) {
             // vs 361 rounds/s).  And ahead of the tile mean's scratch reads (-1 to -5 us on c3's
             // 100-us round, profiles/r12)
 #ifndef DL_AB_PF_LATE
-            if (nxt < a.n_tiles) prefetch(nxt);
+            if (nxt < tile_end) prefetch(nxt);
 #endif
             float4 mean_t = zero4();
             if (mfi || lsum) {
@@ -756,7 +759,7 @@ mix_tile_kernel(TileArgs a) {
                 mean_t.w = mean_t.w / n;
             }
 #ifdef DL_AB_PF_LATE
-            if (nxt < a.n_tiles) prefetch(nxt);
+            if (nxt < tile_end) prefetch(nxt);
 #endif
             float *yt = const_cast<float *>(
                 reinterpret_cast<const float *>(tile_base(a.y, a.yts, tile_id)));
@@ -826,7 +829,7 @@ mix_tile_kernel(TileArgs a) {
                 cur[k] = px[k];
                 if (s + k * SLOTS < Nr) add4(cs, cur[k]);
             }
-            if (nxt < a.n_tiles) prefetch(nxt);
+            if (nxt < tile_end) prefetch(nxt);
             const float4 mean = tile_mean(cs);
             if (a.mean != nullptr && s == 0) st4(a.mean, col0 + 4 * c, P, FAST, mean);
 #pragma unroll

@@ -551,10 +551,10 @@ def run_c3(args, dev, rank, world):
     gbs = mix_bytes / (mix_ms / 1e3) / 1e9
     if rank != 0:
         return
-    # HBM bytes per launch from the committed PMC passes of this workload (profiles/r11/c3: the
-    # round-4 build; the local-step emission's from r10), and the kernel's rocprofv3 average over
+    # HBM bytes per launch from the committed PMC passes of this workload (profiles/r13/c3: the
+    # round-6 build; the local-step emission's from r10), and the kernel's rocprofv3 average over
     # the same command's timed graph steps
-    c3_path = (os.path.join(ROOT, "profiles", "r12", "c3", "summary.json") if sgd.emit == "grad"
+    c3_path = (os.path.join(ROOT, "profiles", "r13", "c3", "summary.json") if sgd.emit == "grad"
                else os.path.join(ROOT, "profiles", "r10", "c3_step", "summary.json"))
     if not os.path.exists(c3_path) and sgd.emit == "grad":
         c3_path = os.path.join(ROOT, "profiles", "r10", "c3", "summary.json")
@@ -888,9 +888,9 @@ def run_c4(args, dev, rank, world):
         return
     achieved = bytes_per_round / (launch_ms / 1e3) / 1e9
     # single GPU: HBM bytes per launch from the committed PMC passes of this kernel instance
-    # (profiles/r11/c4)
+    # (profiles/r13/c4)
     c4_traffic, c4_src = (traffic_from_profile(
-        kernel_name(plan, True, True, n), os.path.join(ROOT, "profiles", "r12", "c4",
+        kernel_name(plan, True, True, n), os.path.join(ROOT, "profiles", "r13", "c4",
                                                        "summary.json"))
         if world == 1 else (None, None))
     xgmi = _halo_xgmi(schemes, plan["overlap"], P, launch_ms) if world > 1 else None
@@ -1035,7 +1035,7 @@ def run_c4rank(args, dev, rank, world):
         v["round_hbm_frac"] = v["round_hbm_bytes"] / (v["round_ms"] / 1e3) / 1e9 / HBM_PEAK_GBS
     achieved = kern["mix_bytes"] / (kern["mix_ms"] / 1e3) / 1e9
     traffic, src = traffic_from_profile(kern["kernel_instance"], os.path.join(
-        ROOT, "profiles", "r12", "c4rank", "summary.json"), bytes_hint=kern["mix_bytes"])
+        ROOT, "profiles", "r13", "c4rank", "summary.json"), bytes_hint=kern["mix_bytes"])
     cpu = None
     if not args.no_cpu and world == 1:   # this rank's round on one host core
         rp = sharding.split_halo_plans(csr, parts)[0]

@@ -29,7 +29,7 @@ def test_c2_headline_kernel_has_committed_traffic(bench):
 
 
 def test_c3_kernels_have_committed_traffic(bench):
-    path = os.path.join(ROOT, "profiles", "r09", "c3", "summary.json")
+    path = os.path.join(ROOT, "profiles", "r13", "c3", "summary.json")
     for k in ("mlp_fused_kernel", "mix_tile_kernel<"):
         traffic, _ = bench.traffic_from_profile(k, path)
         assert traffic is not None and traffic > 0, k
@@ -103,7 +103,7 @@ def test_c4_rank_kernel_has_committed_traffic(bench):
     alg = 4 * 2 ** 18 * (3 * 512 + 96) + 8 * 2 ** 18
     name = bench.kernel_name({"path": 1, "tile_cols": 16}, True, False, 608, halo=2, lag=True)
     traffic, src = bench.traffic_from_profile(
-        name, os.path.join(ROOT, "profiles", "r12", "c4rank", "summary.json"), bytes_hint=alg)
+        name, os.path.join(ROOT, "profiles", "r13", "c4rank", "summary.json"), bytes_hint=alg)
     assert traffic is not None and src.startswith("profiles/")
     assert abs(traffic / alg - 1) < 0.01
 
@@ -122,18 +122,18 @@ def test_c4_ba_kernel_has_committed_traffic(bench):
     assert abs(traffic / alg - 1) < 0.02
 
 
-@pytest.mark.parametrize("workload,plan,n,alg", [
-    ("c3", {"path": 1, "tile_cols": 64}, 256, 12 * 256 * 164608),
-    ("c4", {"path": 1, "tile_cols": 4}, 4096, 12 * 4096 * 2 ** 18),
-    ("c4gather", {"path": 4, "tile_cols": 4, "head": 5, "tail_fmt": 0}, 4096,
+@pytest.mark.parametrize("rnd,workload,plan,n,alg", [
+    ("r13", "c3", {"path": 1, "tile_cols": 64}, 256, 12 * 256 * 164608),
+    ("r13", "c4", {"path": 1, "tile_cols": 4}, 4096, 12 * 4096 * 2 ** 18),
+    ("r12", "c4gather", {"path": 4, "tile_cols": 4, "head": 5, "tail_fmt": 0}, 4096,
      12 * 4096 * 2 ** 18)])
-def test_c3_c4_round_kernels_have_committed_traffic(bench, workload, plan, n, alg):
+def test_c3_c4_round_kernels_have_committed_traffic(bench, rnd, workload, plan, n, alg):
     """The c3, c4 and c4-gather lines' round kernels (full instance names from the plan) are in
     the round-5 profiles, within 1 % of the algorithmic 12 B per element."""
     traffic, src = bench.traffic_from_profile(
         bench.kernel_name(plan, True, True, n),
-        os.path.join(ROOT, "profiles", "r12", workload, "summary.json"))
-    assert traffic is not None and src.startswith("profiles/r12/")
+        os.path.join(ROOT, "profiles", rnd, workload, "summary.json"))
+    assert traffic is not None and src.startswith(f"profiles/{rnd}/")
     assert abs(traffic / alg - 1) < 0.01
 
 

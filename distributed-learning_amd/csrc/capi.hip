@@ -1229,10 +1229,14 @@ int dl_mix_round(const dl_mix_args *args, void *workspace, size_t ws_bytes, dl_s
         if (grid_full > 0) {
             t.n_tiles = (int32_t)n_full;
             t.col_base = 0;
-            // DLAMD_TILE_RUN=1 (measurement knob): each workgroup walks one contiguous run of
-            // tiles instead of every grid-th tile
-            if (const char *v = getenv("DLAMD_TILE_RUN"))
-                if (v[0] == '1') t.tile_run = (int32_t)((n_full + grid_full - 1) / grid_full);
+            // row-major operands: each workgroup walks one contiguous run of tiles instead of
+            // every grid-th tile, so its row segments follow each other in every row (c3's
+            // 256 x 164,608 round: 103.8 against 105.3-107.3 us between events,
+            // profiles/r13/c3_env/); the column-tiled layout keeps the grid stride (+0.4 % with
+            // runs on c2, within noise).  DLAMD_TILE_RUN=0 / 1 forces it off / on.
+            const char *v = getenv("DLAMD_TILE_RUN");
+            const bool runs = v ? v[0] == '1' : !t.tiled;
+            if (runs) t.tile_run = (int32_t)((n_full + grid_full - 1) / grid_full);
             t.dev_partial = partial;
             hipError_t e = reg_csr ? dl::launch_mix_tile_reg(t, pl.chunks, pl.head, pl.tail_fmt,
                                                              sgd, pl.dev, grid_full, lds, s)

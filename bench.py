@@ -175,17 +175,16 @@ def fdla_probe(dev, n, P, lr, steps=20, warmup=3):
     for _ in range(warmup):
         eng.round(G=G, lr=lr, deviation=True)
     stream = torch.cuda.current_stream(dev)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(steps)]
+    sp = SpanEvents(steps, stream)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for a, b in evs:
-        a.record(stream)
+    for i in range(steps):
+        sp.before(i)
         eng.round(G=G, lr=lr, deviation=True)
-        b.record(stream)
+        sp.after(i)
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t0) / steps
-    launch_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    launch_ms = sp.ms()
     achieved = 12 * n * P / (launch_ms / 1e3) / 1e9
     del eng, G
     torch.cuda.empty_cache()
@@ -421,6 +420,30 @@ def timed_loop(step, args, world, dev):
 
 def event_pairs(k, n):
     return [[torch.cuda.Event(enable_timing=True) for _ in range(n)] for _ in range(k)]
+
+
+class SpanEvents:
+    """One HIP timing-event pair around the K timed steps (``ms()`` = GPU time per step).  A pair
+    around EVERY step would put two barrier packets between consecutive launches: 8-10 us of
+    GPU idle a step, which the wall clock of the timed loop -- the line's ``value`` -- includes
+    (c4-rank 0.368-0.378 against 0.359-0.360 ms a round, c2 +0.3 %; scripts/event_probe.py,
+    profiles/r13/event_probe.log)."""
+
+    def __init__(self, steps, stream):
+        self.k, self.stream = steps, stream
+        self.a = torch.cuda.Event(enable_timing=True)
+        self.b = torch.cuda.Event(enable_timing=True)
+
+    def before(self, i):
+        if i == 0:
+            self.a.record(self.stream)
+
+    def after(self, i):
+        if i == self.k - 1:
+            self.b.record(self.stream)
+
+    def ms(self):
+        return self.a.elapsed_time(self.b) / self.k
 
 
 def c3_init_rows(ann, gen):
@@ -692,16 +715,16 @@ def run_gather(args, dev, rank, world):
     stream = torch.cuda.current_stream(dev)
 
     def timed(round_fn):
-        evs = event_pairs(args.steps, 2)
+        sp = SpanEvents(args.steps, stream)
 
         def step(i):
             if i is not None:
-                evs[i][0].record(stream)
+                sp.before(i)
             round_fn()
             if i is not None:
-                evs[i][1].record(stream)
+                sp.after(i)
         elapsed = timed_loop(step, args, world, dev)
-        return elapsed, float(np.mean([a.elapsed_time(b) for a, b, *_ in evs]))
+        return elapsed, sp.ms()
 
     # product path: register-CSR tile kernel, tiled layout, fused deviation
     eng = engine.GossipEngine(csr, P, device=dev, X=torch.randn(n, P, device=dev, generator=gen),
@@ -790,16 +813,16 @@ def _halo_schemes(args, dev, rank, world, csr, parts, P, lr, gen):
         shard.X.normal_(generator=gen)
         if G is None:   # synthetic gradient rows, shared by both schemes (same shape and layout)
             G = engine.staggered_zeros(shard._shape(rp.n_local), 2, dev).normal_(generator=gen)
-        evs = event_pairs(args.steps, 2)
+        sp = SpanEvents(args.steps, stream)
 
-        def step(i, shard=shard, evs=evs):
+        def step(i, shard=shard, sp=sp):
             if i is not None:
-                evs[i][0].record(stream)
+                sp.before(i)
             shard.round(G=G, lr=lr, deviation=True)   # lagged deviation, in the round
             if i is not None:
-                evs[i][1].record(stream)
+                sp.after(i)
         el = timed_loop(step, args, world, dev)
-        lm = max_over_ranks(float(np.mean([a.elapsed_time(b) for a, b in evs])), world, dev)
+        lm = max_over_ranks(sp.ms(), world, dev)
         extra = 8 * (rp.n_local - rp.n_deep) * P if name == "split" else 0
         schemes[name] = {"rounds_per_s": args.steps / el, "elapsed_s": el, "launch_ms": lm,
                          "layout": shard.layout, "tile_cols": shard.T,
@@ -845,7 +868,7 @@ def _single_gpu_round(args, dev, csr, P, lr, gen):
     from distributed_learning_amd import engine
     stream = torch.cuda.current_stream(dev)
     n = csr.n_rows
-    evs = event_pairs(args.steps, 2)
+    sp = SpanEvents(args.steps, stream)
     X = torch.randn(n, P, device=dev, generator=gen)
     eng = engine.GossipEngine(csr, P, device=dev, X=X)
     G = eng.layout_like(torch.randn(n, P, device=dev, generator=gen))
@@ -854,12 +877,12 @@ def _single_gpu_round(args, dev, csr, P, lr, gen):
 
     def step(i):
         if i is not None:
-            evs[i][0].record(stream)
+            sp.before(i)
         eng.round(G=G, lr=lr, deviation=True)
         if i is not None:
-            evs[i][1].record(stream)
+            sp.after(i)
     elapsed = timed_loop(step, args, 1, dev)
-    return elapsed, float(np.mean([a.elapsed_time(b) for a, b in evs])), plan
+    return elapsed, sp.ms(), plan
 
 
 def run_c4(args, dev, rank, world):
@@ -983,16 +1006,16 @@ def run_c4rank(args, dev, rank, world):
             for slot in (0, 1):
                 _, halo, _ = shard._buffers(slot, c1 - c0)
                 halo.normal_(generator=gen)     # the resident halo (an exchange's payload)
-        evs = event_pairs(args.steps, 2)
+        sp = SpanEvents(args.steps, stream)
 
-        def step(i, shard=shard, evs=evs):
+        def step(i, shard=shard, sp=sp):
             if i is not None:
-                evs[i][0].record(stream)
+                sp.before(i)
             shard.round(G=G, lr=lr, deviation=True)
             if i is not None:
-                evs[i][1].record(stream)
+                sp.after(i)
         el = timed_loop(step, args, 1, dev)
-        lm = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+        lm = sp.ms()
         schemes[name] = {"overlap": overlap, "chunk_cols": shard.chunk, "rounds_per_s":
                          args.steps / el, "elapsed_s": el, "round_ms": lm,
                          "layout": shard.layout, "tile_cols": shard.T,
@@ -1466,7 +1489,7 @@ def run_gossip(args, dev, rank, world):
     eng = engine.GossipEngine(csr, P, device=dev, X=torch.randn(n, P, device=dev, generator=g),
                               order=order, layout=args.layout)
     stream = torch.cuda.current_stream(dev)
-    evs = event_pairs(args.steps, 2)
+    sp = SpanEvents(args.steps, stream)
     if args.trace:
         # Mixer.mix(times, eps) as the drop-in runs it for X too large for one workgroup: one
         # traced pass of K rounds + one readback of the K per-round max deviations per step
@@ -1481,10 +1504,10 @@ def run_gossip(args, dev, rank, world):
 
         def step(i):
             if i is not None:
-                evs[i][0].record(stream)
+                sp.before(i)
             eng.rounds_traced(K, trace)
             if i is not None:
-                evs[i][1].record(stream)
+                sp.after(i)
             last[:] = trace.tolist()     # the host stop test reads the K values every pass
     else:
         plan = engine.rounds_plan(eng.W, eng.X, eng.Y, deviation=True, tiled=(eng.P, eng.T))
@@ -1493,13 +1516,13 @@ def run_gossip(args, dev, rank, world):
 
         def step(i):
             if i is not None:
-                evs[i][0].record(stream)
+                sp.before(i)
             eng.rounds(K, deviation=True)
             if i is not None:
-                evs[i][1].record(stream)
+                sp.after(i)
 
     elapsed = timed_loop(step, args, world, dev)
-    launch_ms = max_over_ranks(float(np.mean([a.elapsed_time(b) for a, b in evs])), world, dev)
+    launch_ms = max_over_ranks(sp.ms(), world, dev)
     if rank != 0:
         return
     cpu = None
@@ -1744,14 +1767,13 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream(dev)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
+    sp = SpanEvents(args.steps, stream)
     t0 = time.perf_counter()
     pending.clear()
     for i in range(args.steps):
-        evs[i][0].record(stream)
+        sp.before(i)
         eng.round(G=G, lr=lr, deviation=True)
-        evs[i][1].record(stream)
+        sp.after(i)
         reduce_dev()
     for w, _ in pending:
         w.wait()
@@ -1760,7 +1782,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    launch_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    launch_ms = sp.ms()
     dev_sq_global = pending[-1][1] if pending else eng.dev_sq
     dev_max = float(torch.sqrt(dev_sq_global.max()).item())
     if world > 1:
@@ -1819,7 +1841,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_source": traffic_src, "kernel_instance": kname,
-                         "kernel": "mix_tile_kernel (+dev_reduce) per-round HIP-event time",
+                         "kernel": "mix_tile_kernel (+dev_reduce): HIP events around the K "
+                                   "timed rounds / K",
                          "bytes_per_launch": bytes_per_round, "launch_ms": launch_ms,
                          "measured_copy_ceiling_GBs": ceiling,
                          "measured_triad_ceiling_GBs": triad,

@@ -122,9 +122,6 @@ __device__ __forceinline__ void add4(float4 &a, float4 b) {
 // order: the sum is the same IEEE add); xor 4 / 8 stay ds_bpermute.  Bit-identical to
 // v + __shfl_xor(v, m) (a + b == b + a).
 __device__ __forceinline__ float xor_add(float v, int m) {
-#ifdef DL_AB_SHFL
-    return v + __shfl_xor(v, m);
-#endif
     if (m == 1)
         return v + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true));
     if (m == 2)
@@ -380,11 +377,7 @@ mix_tile_kernel(TileArgs a) {
     // and the row group's C lanes are summed ONCE, after the last tile -- no cross-lane
     // reduction per pass and tile (log2 C ds_bpermutes per pass: at c3's 256 x 164,608 round
     // they were 20-30 us of a 117-us launch, scripts/c3_scale_probe.py)
-#ifdef DL_AB_NO_LD
-    constexpr bool LD = false;
-#else
     constexpr bool LD = DEV && C > 1 && KV <= 4;
-#endif
 
     float ldev[LD ? KV : 1];
 #pragma unroll
@@ -462,11 +455,7 @@ mix_tile_kernel(TileArgs a) {
     // weights: c2, c3, c4): the 5 weights in scalar registers from row 0's CSR, the row's 5
     // column ids and then its 5 tile values read back to back -- 6 LDS round trips a row
     // become 2 (the same products and sums in the same order: the same bits)
-#ifdef DL_AB_NO_REG5
-    const bool reg5 = false;
-#else
     const bool reg5 = MIX && RD == 0 && KV <= 4 && reg == 5 && wshared;
-#endif
     float w5[5];
 #pragma unroll
     for (int e = 0; e < 5; ++e) w5[e] = reg5 ? a.w[e] : 0.f;
@@ -681,26 +670,16 @@ mix_tile_kernel(TileArgs a) {
     int tile_id = trun ? (int)blockIdx.x * trun : (int)blockIdx.x;
     const int tile_end = trun ? min(tile_id + trun, a.n_tiles) : a.n_tiles;
     const int tstep = trun ? 1 : (int)gridDim.x;
-#ifdef DL_AB_CSR_EARLY
-    if (RD == 0 && MIX) {
-        for (int i = tid; i < a.n_w; i += NT) lw[i] = a.w[i];
-        for (int i = tid; i < nnz; i += NT) lcol[i] = (uint16_t)a.col[i];
-        if (!a.regular)
-            for (int i = tid; i <= Nr; i += NT) lrp[i] = (uint16_t)a.rowptr[i];
-    }
-#endif
     if (tile_id < tile_end) prefetch(tile_id);
     // the LDS CSR is staged after the first tile's loads are issued: its loads (an L2 hit for
     // every workgroup but the first) then wait behind the tile's instead of delaying them, and
     // the first staging barrier below publishes it
-#ifndef DL_AB_CSR_EARLY
     if (RD == 0 && MIX) {
         for (int i = tid; i < a.n_w; i += NT) lw[i] = a.w[i];
         for (int i = tid; i < nnz; i += NT) lcol[i] = (uint16_t)a.col[i];
         if (!a.regular)
             for (int i = tid; i <= Nr; i += NT) lrp[i] = (uint16_t)a.rowptr[i];
     }
-#endif
     for (; tile_id < tile_end; tile_id += tstep) {
         // opaque per tile: keeps LICM from hoisting one offset register per pass
         asm volatile("" : "+v"(ox), "+v"(og), "+v"(oy));
@@ -744,9 +723,7 @@ mix_tile_kernel(TileArgs a) {
             // register-head + LDS-tail kernel, one workgroup per CU, 10 % slower too: c4-ba 327
             // vs 361 rounds/s).  And ahead of the tile mean's scratch reads (-1 to -5 us on c3's
             // 100-us round, profiles/r12)
-#ifndef DL_AB_PF_LATE
             if (nxt < tile_end) prefetch(nxt);
-#endif
             float4 mean_t = zero4();
             if (mfi || lsum) {
 #pragma unroll
@@ -758,9 +735,6 @@ mix_tile_kernel(TileArgs a) {
                 mean_t.z = mean_t.z / n;
                 mean_t.w = mean_t.w / n;
             }
-#ifdef DL_AB_PF_LATE
-            if (nxt < tile_end) prefetch(nxt);
-#endif
             float *yt = const_cast<float *>(
                 reinterpret_cast<const float *>(tile_base(a.y, a.yts, tile_id)));
             float4 cs = zero4();

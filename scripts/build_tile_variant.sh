@@ -1,7 +1,7 @@
 #!/bin/bash
-# Measurement build of libdlamd.so with extra -D flags on mix_tile.hip only (its A/B knobs,
-# DL_AB_*), linked with the default build's other objects:
-#   scripts/build_tile_variant.sh <name> -DDL_AB_NO_LD ...  ->  scripts/_build/<name>/libdlamd.so
+# Measurement build of libdlamd.so with extra -D flags on mix_tile.hip only (A/B builds,
+# -D knobs), linked with the default build's other objects:
+#   scripts/build_tile_variant.sh <name> -DFOO=1 ...  ->  scripts/_build/<name>/libdlamd.so
 set -e
 cd "$(dirname "$0")/.."
 NAME=$1; shift

@@ -543,11 +543,16 @@ dl::TileArgs tile_args(const dl_mix_args *a) {
         // X, G and X' are streamed exactly once per round: non-temporal loads and stores keep
         // them out of L2/MALL (measured +1.5 % on c2).  An X' that fits the 256-MB MALL is
         // stored plainly instead, so the next kernel's reads of it (the c3 gradient launch
-        // reading X' as its parameters) can hit there: c3 +2 % steps/s (3743 vs 3668).
-        // DLAMD_NT_STORE=0/1 and DLAMD_NT_LOAD=0 force them.
+        // reading X' as its parameters) can hit there: c3 +2 % steps/s (3743 vs 3668) -- but
+        // not in a partitioned round, whose next launch is the next column chunk's pack and mix
+        // (other columns): plain stores there left the following launch 16 % slower (one rank
+        // of 8, two chunks of 256 MB: 421.7 against 383.5-387.5 us a round with them
+        // non-temporal, profiles/r13/c4rank_env/).  DLAMD_NT_STORE=0/1 and DLAMD_NT_LOAD=0
+        // force them.
         const char *nt = getenv("DLAMD_NT_STORE");
         const size_t y_bytes = (size_t)a->W.n_rows * (size_t)a->n_params * 4;
-        t.nt_store = nt ? (nt[0] == '0' ? 0 : 1) : (y_bytes > kMallBytes ? 1 : 0);
+        const bool partitioned = a->n_halo > 0 || (a->n_local_src && a->n_local_src != a->W.n_rows);
+        t.nt_store = nt ? (nt[0] == '0' ? 0 : 1) : (y_bytes > kMallBytes || partitioned ? 1 : 0);
         const char *ntl = getenv("DLAMD_NT_LOAD");
         t.nt_load = !ntl ? 3 : ntl[0] == '0' ? 0 : ntl[0] == 'x' ? 1 : ntl[0] == 'g' ? 2 : 3;
     }

@@ -15,7 +15,9 @@ tail -c 600 $O/bench.json
 prof() {
     local name=$1; shift
     echo "=== $name"
-    timeout -k 10 400 rocprofv3 "$@" --output-format csv -d $O/$name -o run -- python bench.py $ARGS --no-cpu > $O/$name.log 2>&1
+    # (--no-fdla-probe: the per-edge-weight probe launches the same kernel instance on another
+    # graph, and its launches would mix into the instance's average)
+    timeout -k 10 400 rocprofv3 "$@" --output-format csv -d $O/$name -o run -- python bench.py $ARGS --no-cpu --no-fdla-probe > $O/$name.log 2>&1
     local rc=$?
     echo "rc=$rc"
     if [ $rc -ne 0 ]; then tail -20 $O/$name.log; exit $rc; fi

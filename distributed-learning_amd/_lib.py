@@ -97,7 +97,8 @@ class DlMlpArgs(ctypes.Structure):
     _fields_ = [("n_agents", _i32), ("batch", _i32), ("input_dim", _i32), ("hidden_dim", _i32),
                 ("output_dim", _i32), ("X", _vp), ("ldx", _i64), ("data", _vp), ("s_data", _i64),
                 ("labels", _vp), ("s_labels", _i64), ("G", _vp), ("ldg", _i64), ("loss", _vp),
-                ("tile_cols", _i32), ("out_mode", _i32), ("lr", ctypes.c_float)]
+                ("tile_cols", _i32), ("out_mode", _i32), ("lr", ctypes.c_float),
+                ("workspace", _vp)]
 
 
 EPI = {"none": 0, "bias": 1, "bias_relu": 2, "bias_tanh": 3, "bias_elu": 4, "drelu": 5,
@@ -138,6 +139,7 @@ SIGNATURES = {
                                         _i32, _vp]),
     "dl_stream_copy": (_i32, [_vp, _vp, _i64, _i32, _vp]),
     "dl_sgd_step": (_i32, [ctypes.POINTER(DlSgdArgs), _vp]),
+    "dl_mlp_workspace_bytes": (_sz, [_i32]),
     "dl_mlp_grad": (_i32, [ctypes.POINTER(DlMlpArgs), _vp]),
     "dl_bgemm": (_i32, [ctypes.POINTER(DlBgemmArgs), _vp]),
     "dl_xent_grad": (_i32, [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _i32, _i32, _i32, _vp]),
@@ -149,7 +151,7 @@ SIGNATURES = {
     "dl_lds_slot_order": (_i32, [_i32, _i32, _vp, _i32, _i64, ctypes.c_uint64, _vp, _vp]),
 }
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 _lib = None
 
 
@@ -174,9 +176,9 @@ def load():
         fn.restype = res
         fn.argtypes = args
     v = lib.dl_abi_version()
-    # (an older build under A/B, DLAMD_LIB: ABI 8 reads dl_mix_args up to n_hub_rows and never
-    # sees the fields added after it; the bench's rounds pass none of them)
-    if v != ABI_VERSION and not (os.environ.get("DLAMD_LIB") and v == 8):
+    # (an older build under A/B, DLAMD_LIB: ABI 8 reads dl_mix_args up to n_hub_rows, ABI 9
+    # dl_mlp_args up to lr, and never sees the fields added after them)
+    if v != ABI_VERSION and not (os.environ.get("DLAMD_LIB") and v in (8, 9)):
         raise ImportError(f"libdlamd ABI {lib.dl_abi_version()} != expected {ABI_VERSION}")
     _lib = lib
     return lib

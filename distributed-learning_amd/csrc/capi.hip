@@ -1561,6 +1561,10 @@ int dl_sgd_step(const dl_sgd_args *a, dl_stream_t stream) {
     return e == hipSuccess ? DL_OK : hip_fail(e, "sgd_step launch");
 }
 
+size_t dl_mlp_workspace_bytes(int32_t n_agents) {
+    return n_agents > 0 ? dl::mlp_workspace_floats(n_agents) * sizeof(float) : 0;
+}
+
 int dl_mlp_grad(const dl_mlp_args *a, dl_stream_t stream) {
     g_err.clear();
     if (!a) return fail(DL_ERR_INVALID, "dl_mlp_grad: null args");
@@ -1595,10 +1599,15 @@ int dl_mlp_grad(const dl_mlp_args *a, dl_stream_t stream) {
         return fail(DL_ERR_INVALID, "dl_mlp_grad: out_mode must be 0 (gradient) or 1 (step)");
     if (a->out_mode == 1 && T == 0 && a->ldg != a->ldx)
         return fail(DL_ERR_INVALID, "dl_mlp_grad: out_mode 1 needs ldg == ldx");
+    if (a->workspace && (!aligned16(a->workspace) ||
+                         overlaps(a->workspace, dl_mlp_workspace_bytes(a->n_agents), a->X, xb) ||
+                         overlaps(a->workspace, dl_mlp_workspace_bytes(a->n_agents), a->G, gb)))
+        return fail(DL_ERR_INVALID, "dl_mlp_grad: workspace must be 16-byte aligned and disjoint "
+                                    "from X and G");
     hipError_t e = dl::launch_mlp_fused(a->X, a->ldx, a->data, a->s_data, a->labels, a->s_labels,
                                         a->G, a->ldg, a->loss, a->n_agents, a->input_dim,
                                         a->hidden_dim, a->output_dim, T, a->out_mode == 1,
-                                        a->lr, static_cast<hipStream_t>(stream));
+                                        a->lr, a->workspace, static_cast<hipStream_t>(stream));
     return e == hipSuccess ? DL_OK : hip_fail(e, "mlp_fused launch");
 }
 

@@ -293,7 +293,9 @@ int mlp_fused_supported(int batch, int din, int dh, int dout);
 hipError_t launch_mlp_fused(const float *X, int64_t ldx, const float *data, int64_t s_data,
                             const int32_t *labels, int64_t s_lab, float *G, int64_t ldg,
                             float *loss, int n_agents, int din, int dh, int dout, int tile_cols,
-                            bool step, float lr, hipStream_t s);
+                            bool step, float lr, float *ws, hipStream_t s);
+// the split gradient path's workspace (dl_mlp_args.workspace), in floats
+size_t mlp_workspace_floats(int n_agents);
 
 // sets dl_last_error()'s message (capi.hip) and returns code: for host-only entry points
 // defined outside capi.hip

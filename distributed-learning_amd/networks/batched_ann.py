@@ -10,6 +10,7 @@ gradients written directly into each agent's row of G -- the G that the fused lo
 ``dl_mix_round`` consumes.  No per-agent Python loop, no autograd graph.
 """
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -24,12 +25,16 @@ def fused_supported(batch, input_dim, hidden_dim, output_dim):
 
 
 class BatchedANN:
-    """path: "fused" (one dl_mlp_grad launch per step: every agent's forward + loss + backward in
-    one workgroup, activations in LDS), "layers" (11 dl_bgemm launches) or "auto" (fused when the
-    shapes allow it)."""
+    """path: "fused" (dl_mlp_grad: every agent's forward + loss + backward, activations in LDS),
+    "layers" (11 dl_bgemm launches) or "auto" (fused when the shapes allow it).
+
+    split (fused path, gradient output): run dl_mlp_grad's three-launch form -- layer 1, the
+    hidden phases, dW1 -- with a workspace (dl_mlp_args.workspace), so that its two HBM phases
+    run several workgroups per CU; the same bits as the one-launch form.  "auto": on unless
+    DLAMD_MLP_SPLIT=0 (a measurement knob)."""
 
     def __init__(self, n_agents, batch, input_dim=784, hidden_dim=150, output_dim=10,
-                 device="cuda", path="auto"):
+                 device="cuda", path="auto", split="auto"):
         self.N, self.B = int(n_agents), int(batch)
         self.din, self.dh, self.dout = int(input_dim), int(hidden_dim), int(output_dim)
         if self.dout > 64:
@@ -53,6 +58,12 @@ class BatchedANN:
         if path == "fused" and not ok:
             raise ValueError("these shapes are not covered by the fused kernel")
         self.path = "fused" if (path == "auto" and ok) else ("layers" if path == "auto" else path)
+        if split == "auto":
+            split = os.environ.get("DLAMD_MLP_SPLIT", "1") != "0"
+        self.ws = None
+        if split and self.path == "fused":
+            nb = _lib.load().dl_mlp_workspace_bytes(self.N)
+            self.ws = torch.empty(-(-nb // 4), dtype=torch.float32, device=self.device)
 
     # -------------------------------------------------------------- helpers
     def _gemm(self, M, N, K, A, lda, sA, ta, B, ldb, sB, tb, C, ldc, sC, epi="none", bias=None,
@@ -87,6 +98,7 @@ class BatchedANN:
         if step and self.path != "fused":
             raise ValueError("the local-step output (lr=...) needs the fused kernel")
         mode = (1, float(lr)) if step else (0, 0.0)
+        ws = _lib.ptr(self.ws) if self.ws is not None else None
         N, B, din, dh, dout, P = self.N, self.B, self.din, self.dh, self.dout, self.P
         if tuple(data.shape) != (N, B, din) or not data.is_contiguous():
             raise ValueError(f"data must be contiguous [{N}, {B}, {din}] fp32")
@@ -103,7 +115,7 @@ class BatchedANN:
                                  "columns")
             args = _lib.DlMlpArgs(N, B, din, dh, dout, _lib.ptr(X), 0, _lib.ptr(data), B * din,
                                   _lib.ptr(labels), labels.stride(0), _lib.ptr(G), 0,
-                                  _lib.ptr(self.loss), T, *mode)
+                                  _lib.ptr(self.loss), T, *mode, ws)
             _lib.check(lib.dl_mlp_grad(ctypes.byref(args), _lib.stream_handle(self.device)),
                        "dl_mlp_grad")
             return self.loss
@@ -118,7 +130,7 @@ class BatchedANN:
         if self.path == "fused":
             args = _lib.DlMlpArgs(N, B, din, dh, dout, _lib.ptr(X), X.stride(0), _lib.ptr(data),
                                   B * din, _lib.ptr(labels), labels.stride(0), _lib.ptr(G),
-                                  G.stride(0), _lib.ptr(self.loss), 0, *mode)
+                                  G.stride(0), _lib.ptr(self.loss), 0, *mode, ws)
             _lib.check(lib.dl_mlp_grad(ctypes.byref(args), _lib.stream_handle(self.device)),
                        "dl_mlp_grad")
             return self.loss

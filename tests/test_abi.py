@@ -27,13 +27,14 @@ def test_library_loads_and_exports_every_declared_symbol():
     for n in names:
         assert hasattr(lib, n), f"{n} declared in dlamd.h but not exported"
         assert n in _lib.SIGNATURES, f"{n} has no ctypes signature"
-    assert lib.dl_abi_version() == _lib.ABI_VERSION == 9
+    assert lib.dl_abi_version() == _lib.ABI_VERSION == 10
     assert set(_lib.SIGNATURES) == set(names)
-    # (ABI 9) entries are tagged in the header
+    # (ABI 9, 10) entries are tagged in the header
     src = open(HEADER).read()
-    assert "#define DLAMD_ABI_VERSION 9" in src
+    assert "#define DLAMD_ABI_VERSION 10" in src
     for tagged in ("(ABI 9) sums[a] = sum_b parts", "(ABI 9) nullable HOST pointer",
-                   "(ABI 9) A column-tiled halo round"):
+                   "(ABI 9) A column-tiled halo round", "(ABI 10) nullable: the three-launch",
+                   "size_t dl_mlp_workspace_bytes(int32_t n_agents);   /* (ABI 10) */"):
         assert tagged in src, tagged
 
 
@@ -45,8 +46,9 @@ def test_struct_layout_matches_c(tmp_path):
                     'sizeof(dl_csr), sizeof(dl_mix_args), offsetof(dl_mix_args, W),'
                     'offsetof(dl_mix_args, lr), offsetof(dl_mix_args, partial_rows_out),'
                     'sizeof(dl_mix_plan), sizeof(dl_perron_args));'
-                    'printf("%zu %zu %zu %zu %zu\\n", sizeof(dl_sgd_args), offsetof(dl_sgd_args, lr),'
-                    'sizeof(dl_mlp_args), offsetof(dl_mlp_args, lr), sizeof(dl_bgemm_args));'
+                    'printf("%zu %zu %zu %zu %zu %zu\\n", sizeof(dl_sgd_args), offsetof(dl_sgd_args, lr),'
+                    'sizeof(dl_mlp_args), offsetof(dl_mlp_args, lr),'
+                    'offsetof(dl_mlp_args, workspace), sizeof(dl_bgemm_args));'
                     'return 0;}\n')
     exe = tmp_path / "layout"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(prog), "-o", str(exe)],
@@ -58,7 +60,7 @@ def test_struct_layout_matches_c(tmp_path):
           ctypes.sizeof(_lib.DlMixPlan),
           ctypes.sizeof(_lib.DlPerronArgs), ctypes.sizeof(_lib.DlSgdArgs),
           _lib.DlSgdArgs.lr.offset, ctypes.sizeof(_lib.DlMlpArgs), _lib.DlMlpArgs.lr.offset,
-          ctypes.sizeof(_lib.DlBgemmArgs)]
+          _lib.DlMlpArgs.workspace.offset, ctypes.sizeof(_lib.DlBgemmArgs)]
     assert c == py
 
 
@@ -165,6 +167,17 @@ def test_new_entry_points_validate_before_any_device_call():
     m.out_mode, m.ldg = 1, P + 112                                          # step, ldg != ldx
     assert lib.dl_mlp_grad(ctypes.byref(m), None) == _lib.DL_ERR_INVALID
     assert b"ldg == ldx" in lib.dl_last_error()
+    # (ABI 10) the three-launch workspace: one [64][156] fp32 image per agent, 16-byte aligned,
+    # disjoint from X and G
+    assert lib.dl_mlp_workspace_bytes(256) == 256 * 64 * 156 * 4
+    assert lib.dl_mlp_workspace_bytes(0) == 0
+    m.out_mode, m.ldg = 0, P + 48
+    m.workspace = (1 << 42) + 4                                             # misaligned
+    assert lib.dl_mlp_grad(ctypes.byref(m), None) == _lib.DL_ERR_INVALID
+    assert b"workspace" in lib.dl_last_error()
+    m.workspace = (1 << 40) + 4096                                          # inside G
+    assert lib.dl_mlp_grad(ctypes.byref(m), None) == _lib.DL_ERR_INVALID
+    assert b"workspace" in lib.dl_last_error()
     x = _lib.DlMixArgs()
     x.x, x.y, x.n_params, x.ldx, x.ldy = 256, 1 << 20, 64, 64, 64
     x.W = _lib.DlCsr(16, 16, 16, 4, 12, 3, 1, 1)

@@ -300,3 +300,52 @@ def test_mlp_consensus_follows_the_engine_row_order(cuda, layout):
     assert torch.equal(res["agents"][0], res["perm"][0])
     assert torch.equal(res["agents"][1], res["perm"][1])
     torch.testing.assert_close(res["agents"][2], res["perm"][2], rtol=1e-5, atol=0)
+
+
+@pytest.mark.parametrize("layout", ["rows", "tiled"])
+@pytest.mark.parametrize("n,dims", [(256, (784, 150, 10)), (16, (784, 150, 10)),
+                                    (5, (52, 40, 7)), (3, (16, 152, 16)), (24, (100, 60, 10))])
+def test_split_gradients_equal_the_one_launch_kernel(cuda, n, dims, layout):
+    """dl_mlp_grad with a workspace runs three launches (layer 1 on two workgroups per agent, the
+    hidden phases, dW1 over x's column tiles); every split, product and summation order is the
+    one-launch kernel's, so gradients and losses are bit-identical, and nothing is written past
+    the parameter columns.  n = 256 and 16 use the XCD-paired layer-1 mapping, 5, 3 and 24 the
+    plain one."""
+    from distributed_learning_amd import engine
+    from distributed_learning_amd.networks.batched_ann import BatchedANN
+    din, dh, dout = dims
+    gen = torch.Generator(device=cuda).manual_seed(29)
+    one = BatchedANN(n, 64, din, dh, dout, device=cuda, path="fused", split=False)
+    three = BatchedANN(n, 64, din, dh, dout, device=cuda, path="fused", split=True)
+    assert one.ws is None and three.ws is not None
+    P = one.P
+    X0 = 0.1 * torch.randn(n, P, device=cuda, generator=gen)
+    data = torch.randn(n, 64, din, device=cuda, generator=gen)
+    labels = torch.randint(0, dout, (n, 64), device=cuda, generator=gen, dtype=torch.int32)
+    out = []
+    for bann in (one, three):
+        if layout == "rows":
+            ld = -(-P // 64) * 64
+            X = torch.zeros(n, ld, device=cuda)
+            X[:, :P] = X0
+            G = torch.full((n, ld), float("nan"), device=cuda)
+            loss = bann.gradients(X[:, :P], data, labels, G[:, :P]).clone()
+            torch.cuda.synchronize()
+            assert torch.isnan(G[:, P:]).all()
+            g = G[:, :P]
+        else:
+            X = engine.to_tiled(X0, 8)
+            G = torch.full_like(X, float("nan"))
+            loss = bann.gradients(X, data, labels, G).clone()
+            torch.cuda.synchronize()
+            g = engine.from_tiled(G, P)
+        assert torch.isfinite(g).all()
+        out.append((g.clone(), loss))
+    assert torch.equal(out[0][0], out[1][0])
+    assert torch.equal(out[0][1], out[1][1])
+    # the workspace is reused step after step: a second call gives the same bits again
+    if layout == "rows":
+        G2 = torch.full((n, ld), float("nan"), device=cuda)
+        three.gradients(X[:, :P], data, labels, G2[:, :P])
+        torch.cuda.synchronize()
+        assert torch.equal(G2[:, :P], out[0][0])

@@ -719,9 +719,8 @@ struct MlpArgs {
 // both batch-strided operands measured no faster); false = everything on the fp32 MFMA
 // (DLAMD_MLP_L1=fp32, a measurement knob)
 // STEP: G receives the local step T = X - lr G instead of the gradient (GOut)
-// MID: the split path's middle launch (below): H1 from p.ws instead of layer 1, dZ1 back into
-// p.ws instead of dW1; everything between is this kernel's own code
-template <bool TILED, bool L1X6, bool STEP, bool MID = false>
+// DZ1_OUT: the two-launch path's first launch (below): dZ1 into p.ws instead of dW1
+template <bool TILED, bool L1X6, bool STEP, bool DZ1_OUT = false>
 __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     float *H1 = lds, *H2 = lds + H_FLOATS, *H3 = lds + 2 * H_FLOATS;
@@ -756,21 +755,16 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
     WSet w5[NSL];
     TSet t5[NSL];
     ColSlice ta;            // dZ3's W4^T slice (K = dout)
-    if constexpr (MID) load_all_w(w5, mat(Xr, o_w2, dh), dh);   // layer 2's weights, first
     // zero all of LDS: K tails and padded tiles then read only finite values (zeros where
-    // they meet a zero-filled staged operand), and the activation pads start at zero.  MID: H1
-    // is the first launch's image (its pad columns are zeros)
-    const f32x4 *h1in = reinterpret_cast<const f32x4 *>(p.ws + (int64_t)a * H_FLOATS);
+    // they meet a zero-filled staged operand), and the activation pads start at zero
     for (int e = tid; e < LDS_FLOATS / 4; e += NTHR)
-        reinterpret_cast<f32x4 *>(lds)[e] =
-            MID && e < H_FLOATS / 4 ? h1in[e] : f32x4{0.f, 0.f, 0.f, 0.f};
+        reinterpret_cast<f32x4 *>(lds)[e] = f32x4{0.f, 0.f, 0.f, 0.f};
     __syncthreads();
     if (tid < MB) H1[tid * LDH + dh] = 1.f;   // ones column: db2 in dW2's MFMAs
 
     // ---- layer 1: H1 = relu(x W1^T + b1), K = din from HBM: x and W1 slices double-buffered in
     // LDS (the H2/H3 space, free until layer 2), the next two register-prefetched
-    if constexpr (MID) {
-    } else if constexpr (L1X6) {
+    if constexpr (L1X6) {
         // Warp-specialised: waves 4-7 (one per SIMD) load slice s + 2 from HBM and split slice
         // s into bf16 planes while waves 0-3 (the other wave of each SIMD) run slice s - 1's
         // MFMAs, one barrier per slice.  (Both roles in every wave, split between barriers,
@@ -1032,7 +1026,7 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
     __syncthreads();
     STAMP(9);
     // ---- dW1 = dZ1^T x [dh x din], K = the 64 batch rows.
-    if constexpr (MID) {   // dZ1 (with H1's ones column and zero pads) for the third launch
+    if constexpr (DZ1_OUT) {   // dZ1 (with H1's ones column and zero pads) for mlp_dw1_kernel
         f32x4 *out = reinterpret_cast<f32x4 *>(p.ws + (int64_t)a * H_FLOATS);
         for (int e = tid; e < H_FLOATS / 4; e += NTHR) out[e] = reinterpret_cast<const f32x4 *>(H1)[e];
     } else if constexpr (L1X6) {
@@ -1204,179 +1198,91 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
     if (p.stamps && threadIdx.x == 0) p.stamps[(int64_t)blockIdx.x * 16 + 15] = __builtin_amdgcn_s_memtime();
 }
 
-// ---------------------------------------------------------------- split path (three launches)
-// With a workspace (dl_mlp_args.workspace) the gradients run as three launches instead of one:
-//   mlp_l1_kernel            H1 = relu(x W1^T + b1): two workgroups per agent, 80 output columns
-//                            each, into the agent's workspace image;
-//   mlp_fused_kernel<MID>    the hidden phases, H1 -> dZ1 (the fused kernel's own code), dZ1 back
-//                            into the same image;
-//   mlp_dw1_kernel           dW1 = dZ1^T x and db1: x's 32-column tiles spread over workgroups.
-// Layer 1 and dW1 are the gradient's two HBM phases.  In the fused launch each runs on one
-// workgroup per CU at the per-CU request ceiling; split, they run with
-// several workgroups per CU and small LDS images.  Every split, product and summation order is
-// the fused kernel's, so both paths give the same bits (tests/test_batched_ann_gpu.py).
-constexpr int L1S_COLS = 80;                        // layer-1 output columns per workgroup
-constexpr int L1S_XPL = MB * BK * 2;                // x plane bytes (4096)
-constexpr int L1S_WPL = L1S_COLS * BK * 2;          // W1 plane bytes (5120)
-constexpr int L1S_IMG = 3 * L1S_XPL + 3 * L1S_WPL;  // one slice image (27648)
-
-// workgroup -> (agent, half): both halves of an agent on one XCD (dispatch deals workgroups to
-// the 8 XCDs round-robin), so the second half reads x from that XCD's L2
-__device__ __forceinline__ void l1_split_map(int b, int nb, int &a, int &half) {
-    if ((nb & 15) == 0) {
-        const int l = b >> 3;
-        half = l & 1;
-        a = (l >> 1) * 8 + (b & 7);
-    } else {
-        a = b >> 1;
-        half = b & 1;
-    }
-}
-
-// Layer 1 of one agent's output columns [n0, n0 + 80): the fused kernel's warp-specialised
-// layer 1 (waves 4-7 load and split slices into bf16 planes, waves 0-3 run the MFMAs, one
-// barrier per slice) on half the W1 rows, with two 27 KB images instead of two 43 KB ones.
-template <bool TILED>
-__global__ void __launch_bounds__(NTHR) mlp_l1_kernel(MlpArgs p) {
-    __shared__ __attribute__((aligned(16))) char img0[2 * L1S_IMG];
-    int a, half;
-    l1_split_map(blockIdx.x, gridDim.x, a, half);
-    const int din = p.din, dh = p.dh, n0 = half * L1S_COLS;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    PRow<TILED> Xr;
-    if constexpr (TILED) Xr = {const_cast<float *>(p.X) + ((int64_t)a << p.tsh), (int)p.tstride, p.tsh};
-    else Xr = {const_cast<float *>(p.X) + (int64_t)a * p.ldx, 0, 0};
-    const float *x = p.data + (int64_t)a * p.s_data;
-    const ParMat<TILED> W1{Xr, 0, din};
-    const int ns = (din + BK - 1) / BK;
-    if (wave >= 4) {
-        const int pt = tid - NTHR / 2;                           // 0..255
-        constexpr int XQ = MB * BK / 4 / (NTHR / 2);             // 2 float4 of x per thread
-        constexpr int WE = L1S_COLS * BK / 4;                    // 640 float4 of W1 per slice
-        constexpr int WQ = (WE + NTHR / 2 - 1) / (NTHR / 2);     // 3 (the third: pt < 128)
-        f32x4 rx[L1_RING][XQ], rw[L1_RING][WQ];
-        // unconditional loads from clamped addresses, zeroing at the single use (fused layer 1)
-        auto load = [&](int set, int sl) {
-            const int k0 = sl * BK;
-#pragma unroll
-            for (int i = 0; i < XQ; ++i) {
-                const int e = pt + i * (NTHR / 2), r = e / 8, c = 4 * (e % 8);
-                rx[set][i] = *reinterpret_cast<const f32x4 *>(
-                    x + (int64_t)r * din + (k0 + c < din ? k0 + c : din - 4));
-            }
-#pragma unroll
-            for (int i = 0; i < WQ; ++i) {
-                const int e = min(pt + i * (NTHR / 2), WE - 1), r = e / 8, c = 4 * (e % 8);
-                const int n = n0 + r;
-                rw[set][i] = *reinterpret_cast<const f32x4 *>(
-                    W1.at(n < dh ? n : dh - 1, k0 + c < din ? k0 + c : din - 4));
-            }
-        };
-        auto store = [&](int set, int sl, char *img) {
-            const int k0 = sl * BK;
-            const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int i = 0; i < XQ; ++i) {
-                const int e = pt + i * (NTHR / 2), r = e / 8, c = 4 * (e % 8);
-                bf16x4 h, m, l;
-                split4(k0 + c < din ? rx[set][i] : z, h, m, l);
-                const uint32_t o = l1_wofs(r, c);
-                *reinterpret_cast<bf16x4 *>(img + o) = h;
-                *reinterpret_cast<bf16x4 *>(img + L1S_XPL + o) = m;
-                *reinterpret_cast<bf16x4 *>(img + 2 * L1S_XPL + o) = l;
-            }
-            char *wpl = img + 3 * L1S_XPL;
-#pragma unroll
-            for (int i = 0; i < WQ; ++i) {
-                const int e = pt + i * (NTHR / 2), r = e / 8, c = 4 * (e % 8);
-                if (e < WE) {
-                    bf16x4 h, m, l;
-                    split4(n0 + r < dh && k0 + c < din ? rw[set][i] : z, h, m, l);
-                    const uint32_t o = l1_wofs(r, c);
-                    *reinterpret_cast<bf16x4 *>(wpl + o) = h;
-                    *reinterpret_cast<bf16x4 *>(wpl + L1S_WPL + o) = m;
-                    *reinterpret_cast<bf16x4 *>(wpl + 2 * L1S_WPL + o) = l;
-                }
-            }
-        };
-#pragma unroll
-        for (int j = 0; j < L1_RING; ++j) load(j, j < ns ? j : ns - 1);
-        for (int s0 = 0; s0 < ns; s0 += L1_RING) {
-#pragma unroll
-            for (int j = 0; j < L1_RING; ++j) {   // register set j holds slice s0 + j
-                const int sl = s0 + j;
-                if (sl < ns) store(j, sl, img0 + (sl & 1) * L1S_IMG);
-                load(j, sl + L1_RING < ns ? sl + L1_RING : ns - 1);
-                if (sl < ns) __syncthreads();
-            }
-        }
-    } else {
-        // wave c: M-tile c (rows 16c..16c+15) x the five 16-column N-tiles of this half
-        f32x4 acc[5], sml[5];
-#pragma unroll
-        for (int t = 0; t < 5; ++t) acc[t] = sml[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-        float bv[5];
-#pragma unroll
-        for (int t = 0; t < 5; ++t) {
-            const int n = n0 + 16 * t + (lane & 15);
-            bv[t] = n < dh ? *Xr.at(dh * din + n) : 0.f;
-        }
-        const int m = wave * 16 + (lane & 15), hq = lane >> 4;
-        auto compute = [&](const char *img) {
-            const uint32_t oa = l1_wofs(m, 8 * hq);
-            const bf16x8 ah = *reinterpret_cast<const bf16x8 *>(img + oa);
-            const bf16x8 am = *reinterpret_cast<const bf16x8 *>(img + L1S_XPL + oa);
-            const bf16x8 al = *reinterpret_cast<const bf16x8 *>(img + 2 * L1S_XPL + oa);
-            const char *wpl = img + 3 * L1S_XPL;
-#pragma unroll
-            for (int t = 0; t < 5; ++t) {
-                const uint32_t ob = l1_wofs(16 * t + (lane & 15), 8 * hq);
-                const bf16x8 bh = *reinterpret_cast<const bf16x8 *>(wpl + ob);
-                const bf16x8 bm = *reinterpret_cast<const bf16x8 *>(wpl + L1S_WPL + ob);
-                const bf16x8 bl = *reinterpret_cast<const bf16x8 *>(wpl + 2 * L1S_WPL + ob);
-                mfma_x6(ah, am, al, bh, bm, bl, acc[t], sml[t]);
-            }
-        };
-        for (int sl = 0; sl < ns; ++sl) {
-            if (sl > 0) compute(img0 + ((sl - 1) & 1) * L1S_IMG);
-            __syncthreads();
-        }
-        compute(img0 + ((ns - 1) & 1) * L1S_IMG);
-        // the image's columns: H1 below dh, zeros from dh to the row's end (LDH)
-        float *h1 = p.ws + (int64_t)a * H_FLOATS;
-#pragma unroll
-        for (int t = 0; t < 5; ++t) {
-            acc[t] += sml[t];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int row = wave * 16 + 4 * hq + r, n = n0 + 16 * t + (lane & 15);
-                if (n < LDH) h1[row * LDH + n] = n < dh ? act_fwd(0, acc[t][r] + bv[t]) : 0.f;
-            }
-        }
-    }
-}
-
-// dW1 = dZ1^T x [dh x din] and db1 (x's ones column din) for one agent's 32-column tiles
-// [j0, j1) of x: wave w owns dW1 rows 32w .. 32w + 31, its dZ1^T operand split into bf16 planes
-// once, in registers (4 k-steps x 3 planes); each x tile is staged as transposed bf16 planes
-// (double-buffered, 24 KB) while the previous tile's MFMAs run.  The fused dW1's tiles, one
-// 32 x 32 tile per wave per x tile, stored straight into G (store_tile).
-constexpr int DW_THR = 320;
+// ---------------------------------------------------------------- two-launch path
+// With a workspace (dl_mlp_args.workspace) dW1 -- the gradient's last phase, 470 KB of G writes
+// and the 200 KB batch re-read per agent -- runs as a launch of its own: mlp_fused_kernel<DZ1_OUT>
+// writes each agent's dZ1 image ([MB][LDH], H1's ones column at dh, zero pads) into the
+// workspace, and mlp_dw1_kernel spreads x's 32-column tiles over two workgroups per agent, each
+// with one producer wave staging tiles and five MFMA waves, small LDS, two per CU.  Every split,
+// product and summation order is the fused dW1's, so both paths give the same bits
+// (tests/test_batched_ann_gpu.py).
+constexpr int DW_THR = 384;            // wave 5 stages x tiles, waves 0-4 own dW1 rows 32w..
+constexpr int DW_RING = 3;             // x tiles in flight in the producer's registers
 constexpr int DW_ROWB = MB * 2;        // 128 bytes per transposed plane row
 constexpr int DW_XP = 32 * DW_ROWB;    // one x tile's plane (4096)
 __device__ __forceinline__ uint32_t dw_tofs(int r, int b) {   // the fused dW1's plane layout
     return (uint32_t)(r * DW_ROWB + ((((b >> 3) ^ (r >> 1)) & 7) << 4) + (b & 7) * 2);
 }
 
-template <bool TILED, bool STEP>
+template <bool TILED>
 __global__ void __launch_bounds__(DW_THR, 3) mlp_dw1_kernel(MlpArgs p) {
     __shared__ __attribute__((aligned(16))) char xpl[2 * 3 * DW_XP];
     const int din = p.din, dh = p.dh, ct = p.dw_ct;
     const int ntiles = (din + 1 + 31) / 32;          // through the ones column din
     const int wpa = (ntiles + ct - 1) / ct;
     const int a = blockIdx.x / wpa, part = blockIdx.x - a * wpa;
-    const int j0 = part * ct, j1 = min(ntiles, j0 + ct);
+    const int j0 = part * ct, nt = min(ntiles, j0 + ct) - j0;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const float *x = p.data + (int64_t)a * p.s_data;
+    if (wave == 5) {
+        // items of 2 batch rows x 4 columns, four per lane (256 per tile); every load issues
+        // unconditionally from a clamped address, the columns from din on (the ones column din,
+        // then zeros) substituted at the single use (fused dW1)
+        constexpr int Q = 4;
+        f32x4 xv[DW_RING][Q][2];
+        auto load = [&](int set, int t) {
+            const int j = j0 + t;
+#pragma unroll
+            for (int q = 0; q < Q; ++q) {
+                const int idx = lane + 64 * q, b0 = 2 * (idx >> 3), xc = 4 * (idx & 7);
+                const int c = 32 * j + xc < din ? 32 * j + xc : din - 4;
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+                    xv[set][q][i] = *reinterpret_cast<const f32x4 *>(x + (int64_t)(b0 + i) * din + c);
+            }
+        };
+        auto store = [&](int set, int t) {
+            const int j = j0 + t;
+            char *pl = xpl + (t & 1) * (3 * DW_XP);
+#pragma unroll
+            for (int q = 0; q < Q; ++q) {
+                const int idx = lane + 64 * q, b0 = 2 * (idx >> 3), xc = 4 * (idx & 7);
+                const int c = 32 * j + xc;
+                f32x4 v[2];
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+                    v[i] = c < din ? xv[set][q][i]
+                           : c == din ? f32x4{1.f, 0.f, 0.f, 0.f} : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                    bf16x2 h, m, l;
+                    split2(v[0][jj], v[1][jj], h, m, l);
+                    const uint32_t o = dw_tofs(xc + jj, b0);
+                    *reinterpret_cast<bf16x2 *>(pl + o) = h;
+                    *reinterpret_cast<bf16x2 *>(pl + DW_XP + o) = m;
+                    *reinterpret_cast<bf16x2 *>(pl + 2 * DW_XP + o) = l;
+                }
+            }
+        };
+        // (loads past the last tile re-read it: unconditional issue.)  The scheduling barriers
+        // keep the first sets' loads in set order: interleaved, the wait before set 0's LDS
+        // store at the loop head became vmcnt(0), draining the whole ring every DW_RING tiles.
+#pragma unroll
+        for (int k = 0; k < DW_RING; ++k) {
+            load(k, k < nt ? k : nt - 1);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        for (int s0 = 0; s0 < nt; s0 += DW_RING) {
+#pragma unroll
+            for (int k = 0; k < DW_RING; ++k) {   // register set k holds tile s0 + k
+                const int t = s0 + k;
+                if (t < nt) store(k, t);
+                load(k, t + DW_RING < nt ? t + DW_RING : nt - 1);
+                if (t < nt) __syncthreads();
+            }
+        }
+        return;
+    }
     PRow<TILED> Xr, Gr;
     if constexpr (TILED) {
         Xr = {const_cast<float *>(p.X) + ((int64_t)a << p.tsh), (int)p.tstride, p.tsh};
@@ -1385,25 +1291,11 @@ __global__ void __launch_bounds__(DW_THR, 3) mlp_dw1_kernel(MlpArgs p) {
         Xr = {const_cast<float *>(p.X) + (int64_t)a * p.ldx, 0, 0};
         Gr = {p.G + (int64_t)a * p.ldg, 0, 0};
     }
-    const float *x = p.data + (int64_t)a * p.s_data;
-    const GOut<STEP> go{p.lr, (int64_t)(Gr.base - Xr.base)};
+    const GOut<false> go{0.f, 0};
     const ParMat<TILED> gw1{Gr, 0, din}, gb1{Gr, dh * din, 0};
     const int r = lane & 31, hh = lane >> 5;
-    // x tile staging items: 2 batch rows x 4 columns, 256 per tile (threads 0..255); the other
-    // lanes load an item's address too and never use it (unconditional issue, fused dW1)
-    const bool xt = tid < 256;
-    const int xi = tid & 255;
-    const int xb0 = 2 * (xi >> 3), xc = 4 * (xi & 7);
-    f32x4 xv[2];
-    auto load = [&](int j) {
-        const int c = 32 * j + xc < din ? 32 * j + xc : din - 4;
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-            xv[i] = *reinterpret_cast<const f32x4 *>(x + (int64_t)(xb0 + i) * din + c);
-    };
-    load(j0);
     // A: dZ1^T rows 32 wave + r (zero from LDH on, as the fused planes), batch rows
-    // 16 ks + 8 hh .. + 7
+    // 16 ks + 8 hh .. + 7, split once into registers
     bf16x8 ah[MB / 16], am[MB / 16], al[MB / 16];
     {
         const float *dz = p.ws + (int64_t)a * H_FLOATS;
@@ -1421,32 +1313,12 @@ __global__ void __launch_bounds__(DW_THR, 3) mlp_dw1_kernel(MlpArgs p) {
                    al[ks]);
         }
     }
-    for (int j = j0; j < j1; ++j) {
-        char *pl = xpl + (j & 1) * (3 * DW_XP);
-        if (xt) {
-            // column din is the ones column (db1); din % 4 == 0 puts it at a float4 start
-            const int c = 32 * j + xc;
-            f32x4 v[2];
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-                v[i] = c < din ? xv[i]
-                       : c == din ? f32x4{1.f, 0.f, 0.f, 0.f} : f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int jj = 0; jj < 4; ++jj) {
-                bf16x2 h, m, l;
-                split2(v[0][jj], v[1][jj], h, m, l);
-                const uint32_t o = dw_tofs(xc + jj, xb0);
-                *reinterpret_cast<bf16x2 *>(pl + o) = h;
-                *reinterpret_cast<bf16x2 *>(pl + DW_XP + o) = m;
-                *reinterpret_cast<bf16x2 *>(pl + 2 * DW_XP + o) = l;
-            }
-        }
-        __syncthreads();
-        load(j + 1 < j1 ? j + 1 : j1 - 1);   // (the last re-reads its own tile, never used)
-        f32x16 big, sml, xo;
+    auto compute = [&](int t) {
+        const int j = j0 + t;
+        const char *pl = xpl + (t & 1) * (3 * DW_XP);
+        f32x16 big, sml, xo = {};   // (xo: the step output's x values, unused here)
 #pragma unroll
         for (int q = 0; q < 16; ++q) big[q] = sml[q] = 0.f;
-        go.prefetch(xo, 32 * wave + 4 * hh, 32 * j + r, gw1, dh, din, gb1);
 #pragma unroll
         for (int ks = 0; ks < MB / 16; ++ks) {
             const uint32_t ob = dw_tofs(r, 16 * ks + 8 * hh);
@@ -1457,7 +1329,12 @@ __global__ void __launch_bounds__(DW_THR, 3) mlp_dw1_kernel(MlpArgs p) {
         }
         big += sml;
         store_tile(big, xo, 32 * wave + 4 * hh, 32 * j + r, gw1, dh, din, gb1, go);
+    };
+    for (int t = 0; t < nt; ++t) {
+        if (t > 0) compute(t - 1);
+        __syncthreads();
     }
+    compute(nt - 1);
 }
 
 }  // namespace
@@ -1494,22 +1371,18 @@ hipError_t launch_mlp_fused(const float *X, int64_t ldx, const float *data, int6
                            LDS_FLOATS * sizeof(float), s, p);
         return hipGetLastError();
     };
-    auto split = [&](auto l1, auto mid, auto dw1) {
-        hipLaunchKernelGGL(l1, dim3(2u * (unsigned)n_agents), dim3(NTHR), 0, s, p);
-        hipError_t e = hipGetLastError();
+    auto split = [&](auto head, auto dw1) {
+        hipError_t e = go(head);
         if (e != hipSuccess) return e;
-        if ((e = go(mid)) != hipSuccess) return e;
         const int wpa = ((din + 1 + 31) / 32 + dw_ct - 1) / dw_ct;
         hipLaunchKernelGGL(dw1, dim3((unsigned)(n_agents * wpa)), dim3(DW_THR), 0, s, p);
         return hipGetLastError();
     };
     auto pick = [&](auto tiled) {
         constexpr bool T = decltype(tiled)::value;
-        // (the local-step output keeps one launch: its x prefetch spills the dW1 kernel's
-        // registers at three waves per SIMD)
+        // (the local-step output keeps one launch)
         if (ws && !l1_fp32 && !step)
-            return split(mlp_l1_kernel<T>, mlp_fused_kernel<T, true, false, true>,
-                         mlp_dw1_kernel<T, false>);
+            return split(mlp_fused_kernel<T, true, false, true>, mlp_dw1_kernel<T>);
         if (step)
             return l1_fp32 ? go(mlp_fused_kernel<T, false, true>) : go(mlp_fused_kernel<T, true, true>);
         return l1_fp32 ? go(mlp_fused_kernel<T, false, false>) : go(mlp_fused_kernel<T, true, false>);

@@ -28,10 +28,11 @@ class BatchedANN:
     """path: "fused" (dl_mlp_grad: every agent's forward + loss + backward, activations in LDS),
     "layers" (11 dl_bgemm launches) or "auto" (fused when the shapes allow it).
 
-    split (fused path, gradient output): run dl_mlp_grad's three-launch form -- layer 1, the
-    hidden phases, dW1 -- with a workspace (dl_mlp_args.workspace), so that its two HBM phases
-    run several workgroups per CU; the same bits as the one-launch form.  "auto": on unless
-    DLAMD_MLP_SPLIT=0 (a measurement knob)."""
+    split (fused path, gradient output): run dl_mlp_grad's two-launch form -- everything up to
+    dZ1, then dW1 over x's column tiles on two workgroups per agent -- with a workspace
+    (dl_mlp_args.workspace); the same bits as the one-launch form.  Measured slower (dW1 52.8 us
+    as a launch of its own against ~42 inside the fused one, profiles/r14/README.md), so "auto"
+    is off unless DLAMD_MLP_SPLIT=1 (a measurement knob)."""
 
     def __init__(self, n_agents, batch, input_dim=784, hidden_dim=150, output_dim=10,
                  device="cuda", path="auto", split="auto"):
@@ -59,7 +60,7 @@ class BatchedANN:
             raise ValueError("these shapes are not covered by the fused kernel")
         self.path = "fused" if (path == "auto" and ok) else ("layers" if path == "auto" else path)
         if split == "auto":
-            split = os.environ.get("DLAMD_MLP_SPLIT", "1") != "0"
+            split = os.environ.get("DLAMD_MLP_SPLIT", "0") == "1"
         self.ws = None
         if split and self.path == "fused":
             nb = _lib.load().dl_mlp_workspace_bytes(self.N)

@@ -589,10 +589,10 @@ int dl_xent_grad(const float *Z, int64_t sZ, const int32_t *y, int64_t sY, float
  *     (dl_mix_round with G = NULL) gives bit-for-bit the X' of the fused round of X and G while
  *     streaming one matrix instead of two; row-major needs ldg == ldx.  0: the gradient.
  *   workspace (ABI 10) nullable, else dl_mlp_workspace_bytes(n_agents) 16-byte aligned bytes:
- *     the gradients run as three launches instead of one -- layer 1, the hidden phases, dW1 --
- *     so that the two HBM phases (layer 1, dW1) run several workgroups per CU; the same bits as
- *     the one-launch path.  The workspace holds each agent's H1, then dZ1, between launches.
- *     out_mode 1 ignores it (one launch).
+ *     the gradients run as two launches instead of one -- everything up to dZ1, then dW1 with
+ *     x's column tiles spread over two workgroups per agent; the same bits as the one-launch
+ *     path (measured slower at c3's shapes: an experiment's reproducible form).  The workspace
+ *     holds each agent's dZ1 between the launches.  out_mode 1 ignores it (one launch).
  * X, data and G 16-byte aligned, ldx, ldg and s_data multiples of 4, G disjoint from X. */
 typedef struct dl_mlp_args {
     int32_t n_agents, batch, input_dim, hidden_dim, output_dim;
@@ -604,7 +604,7 @@ typedef struct dl_mlp_args {
     int32_t tile_cols;   /* 0 = row-major X, G;  T > 0 = column-tiled (see above) */
     int32_t out_mode;    /* 0 = gradient, 1 = local step X - lr G (ABI 7) */
     float lr;            /* out_mode 1: the step size */
-    float *workspace;    /* (ABI 10) nullable: the three-launch path (above) */
+    float *workspace;    /* (ABI 10) nullable: the two-launch path (above) */
 } dl_mlp_args;
 size_t dl_mlp_workspace_bytes(int32_t n_agents);   /* (ABI 10) */
 int dl_mlp_grad(const dl_mlp_args *args, dl_stream_t stream);

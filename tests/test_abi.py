@@ -33,7 +33,7 @@ def test_library_loads_and_exports_every_declared_symbol():
     src = open(HEADER).read()
     assert "#define DLAMD_ABI_VERSION 10" in src
     for tagged in ("(ABI 9) sums[a] = sum_b parts", "(ABI 9) nullable HOST pointer",
-                   "(ABI 9) A column-tiled halo round", "(ABI 10) nullable: the three-launch",
+                   "(ABI 9) A column-tiled halo round", "(ABI 10) nullable: the two-launch",
                    "size_t dl_mlp_workspace_bytes(int32_t n_agents);   /* (ABI 10) */"):
         assert tagged in src, tagged
 
@@ -167,7 +167,7 @@ def test_new_entry_points_validate_before_any_device_call():
     m.out_mode, m.ldg = 1, P + 112                                          # step, ldg != ldx
     assert lib.dl_mlp_grad(ctypes.byref(m), None) == _lib.DL_ERR_INVALID
     assert b"ldg == ldx" in lib.dl_last_error()
-    # (ABI 10) the three-launch workspace: one [64][156] fp32 image per agent, 16-byte aligned,
+    # (ABI 10) the two-launch workspace: one [64][156] fp32 image per agent, 16-byte aligned,
     # disjoint from X and G
     assert lib.dl_mlp_workspace_bytes(256) == 256 * 64 * 156 * 4
     assert lib.dl_mlp_workspace_bytes(0) == 0

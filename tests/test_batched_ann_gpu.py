@@ -306,11 +306,10 @@ def test_mlp_consensus_follows_the_engine_row_order(cuda, layout):
 @pytest.mark.parametrize("n,dims", [(256, (784, 150, 10)), (16, (784, 150, 10)),
                                     (5, (52, 40, 7)), (3, (16, 152, 16)), (24, (100, 60, 10))])
 def test_split_gradients_equal_the_one_launch_kernel(cuda, n, dims, layout):
-    """dl_mlp_grad with a workspace runs three launches (layer 1 on two workgroups per agent, the
-    hidden phases, dW1 over x's column tiles); every split, product and summation order is the
+    """dl_mlp_grad with a workspace runs two launches (everything up to dZ1, then dW1 over x's
+    column tiles on two workgroups per agent); every split, product and summation order is the
     one-launch kernel's, so gradients and losses are bit-identical, and nothing is written past
-    the parameter columns.  n = 256 and 16 use the XCD-paired layer-1 mapping, 5, 3 and 24 the
-    plain one."""
+    the parameter columns."""
     from distributed_learning_amd import engine
     from distributed_learning_amd.networks.batched_ann import BatchedANN
     din, dh, dout = dims

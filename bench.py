@@ -101,6 +101,8 @@ def parse():
     p.add_argument("--c3-layout", default="rows", choices=["rows", "tiled"],
                    help="c3: resident layout of X and G (tiled: the fused gradient kernel "
                         "addresses the round's column tiles; measured equal overall)")
+    p.add_argument("--c3-tile-cols", type=int, default=0,
+                   help="c3 tiled layout: the tile width (0: the planner's widest, 64)")
     p.add_argument("--batch", type=int, default=64, help="c5: images per agent per step")
     p.add_argument("--cudnn-benchmark", action=argparse.BooleanOptionalAction, default=True,
                    help="c5: torch.backends.cudnn.benchmark (MIOpen picks the fastest measured "
@@ -521,7 +523,8 @@ def run_c3(args, dev, rank, world):
     labels = torch.randint(0, ann.dout, (n, B), device=dev, generator=gen, dtype=torch.int32)
     if ann.path == "fused" and args.c3_layout == "tiled":   # X, G column-tiled
         P_pad = P
-        eng = engine.GossipEngine(csr, P, device=dev, X=X0, layout="tiled")
+        eng = engine.GossipEngine(csr, P, device=dev, X=X0, layout="tiled",
+                                  tile_cols=args.c3_tile_cols or None)
     else:
         P_pad = MLPConsensusSGD.padded_params(csr, P, dev)   # zero columns: no ragged tail
         X0 = torch.nn.functional.pad(X0, (0, P_pad - P))
@@ -655,7 +658,7 @@ def run_c3(args, dev, rank, world):
         "config": {"workload": "c3: ANNModel consensus SGD (batched per-agent MFMA gradients + "
                                "fused round + deviation)",
                    "agents": n, "params": P, "params_padded": P_pad, "batch": B, "lr": lr,
-                   "layout": eng.layout, "gradient_path": ann.path, "emit": sgd.emit,
+                   "layout": eng.layout, "tile_cols": eng.T, "gradient_path": ann.path, "emit": sgd.emit,
                    "graph": "random 4-regular",
                    "weights": f"best-constant {wconst:.6f}",
                    "launch": "hipGraph replay per step" if use_graph else "eager",

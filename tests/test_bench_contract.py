@@ -43,6 +43,15 @@ def test_driver_command_line_parses(bench, monkeypatch):
         monkeypatch.setattr("sys.argv", argv)
         p = bench.parse()
         assert p.gpus >= 1 and p.steps >= 1 and p.warmup >= 0
+    # c3's layout knobs (profiles/r14/c3_layout): rows by default, the planner's tile width unless
+    # one is named
+    monkeypatch.setattr("sys.argv", ["bench.py", "--workload", "c3"])
+    p = bench.parse()
+    assert p.c3_layout == "rows" and p.c3_tile_cols == 0 and p.c3_emit == "grad"
+    monkeypatch.setattr("sys.argv", ["bench.py", "--workload", "c3", "--c3-layout", "tiled",
+                                     "--c3-tile-cols", "32"])
+    p = bench.parse()
+    assert p.c3_layout == "tiled" and p.c3_tile_cols == 32
 
 
 def test_halo_probe_failure_carries_child_stderr(bench):

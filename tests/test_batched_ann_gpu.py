@@ -304,7 +304,8 @@ def test_mlp_consensus_follows_the_engine_row_order(cuda, layout):
 
 @pytest.mark.parametrize("layout", ["rows", "tiled"])
 @pytest.mark.parametrize("n,dims", [(256, (784, 150, 10)), (16, (784, 150, 10)),
-                                    (5, (52, 40, 7)), (3, (16, 152, 16)), (24, (100, 60, 10))])
+                                    (5, (52, 40, 7)), (3, (16, 152, 16)), (24, (100, 60, 10)),
+                                    (1, (784, 150, 10)), (7, (416, 96, 16))])
 def test_split_gradients_equal_the_one_launch_kernel(cuda, n, dims, layout):
     """dl_mlp_grad with a workspace runs two launches (everything up to dZ1, then dW1 over x's
     column tiles on two workgroups per agent); every split, product and summation order is the

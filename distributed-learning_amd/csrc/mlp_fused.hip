@@ -829,9 +829,15 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
                     *reinterpret_cast<bf16x4 *>(wpl + 2 * L1P_BYTES + o) = l;
                 }
             };
-            // loads past the last slice re-read it (unconditional issue, see load)
+            // loads past the last slice re-read it (unconditional issue, see load).  The
+            // scheduling barriers keep the first sets' loads in set order: interleaved by the
+            // scheduler, the wait before set 0's LDS store at the loop head was vmcnt(0), which
+            // drained the whole ring every L1_RING slices.
 #pragma unroll
-            for (int j = 0; j < L1_RING; ++j) load(j, j < ns ? j : ns - 1);
+            for (int j = 0; j < L1_RING; ++j) {
+                load(j, j < ns ? j : ns - 1);
+                __builtin_amdgcn_sched_barrier(0);
+            }
             for (int s0 = 0; s0 < ns; s0 += L1_RING) {
 #pragma unroll
                 for (int j = 0; j < L1_RING; ++j) {   // register set j holds slice s0 + j

@@ -586,10 +586,10 @@ def run_c3(args, dev, rank, world):
     gbs = mix_bytes / (mix_ms / 1e3) / 1e9
     if rank != 0:
         return
-    # HBM bytes per launch from the committed PMC passes of this workload (profiles/r13/c3: the
-    # round-6 build; the local-step emission's from r10), and the kernel's rocprofv3 average over
+    # HBM bytes per launch from the committed PMC passes of this workload (profiles/r14/c3: the
+    # final round-6 build; the local-step emission's from r10), and the kernel's rocprofv3 average over
     # the same command's timed graph steps
-    c3_path = (os.path.join(ROOT, "profiles", "r13", "c3", "summary.json") if sgd.emit == "grad"
+    c3_path = (os.path.join(ROOT, "profiles", "r14", "c3", "summary.json") if sgd.emit == "grad"
                else os.path.join(ROOT, "profiles", "r10", "c3_step", "summary.json"))
     if not os.path.exists(c3_path) and sgd.emit == "grad":
         c3_path = os.path.join(ROOT, "profiles", "r10", "c3", "summary.json")

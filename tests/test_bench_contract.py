@@ -29,7 +29,7 @@ def test_c2_headline_kernel_has_committed_traffic(bench):
 
 
 def test_c3_kernels_have_committed_traffic(bench):
-    path = os.path.join(ROOT, "profiles", "r13", "c3", "summary.json")
+    path = os.path.join(ROOT, "profiles", "r14", "c3", "summary.json")
     for k in ("mlp_fused_kernel", "mix_tile_kernel<"):
         traffic, _ = bench.traffic_from_profile(k, path)
         assert traffic is not None and traffic > 0, k
@@ -132,7 +132,7 @@ def test_c4_ba_kernel_has_committed_traffic(bench):
 
 
 @pytest.mark.parametrize("rnd,workload,plan,n,alg", [
-    ("r13", "c3", {"path": 1, "tile_cols": 64}, 256, 12 * 256 * 164608),
+    ("r14", "c3", {"path": 1, "tile_cols": 64}, 256, 12 * 256 * 164608),
     ("r13", "c4", {"path": 1, "tile_cols": 4}, 4096, 12 * 4096 * 2 ** 18),
     ("r12", "c4gather", {"path": 4, "tile_cols": 4, "head": 5, "tail_fmt": 0}, 4096,
      12 * 4096 * 2 ** 18)])

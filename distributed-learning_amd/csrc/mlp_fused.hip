@@ -328,7 +328,13 @@ struct RowSlice4 {
 // split once when the producer waves stage them.  A lane's fragment is 8 consecutive k of one
 // row = one ds_read_b128 per plane; the 16-byte chunk c of row n sits at chunk c ^ ((n >> 2) & 3),
 // so the 16 rows a read spans cover all 64 banks.
-constexpr int L1_RING = 4;                        // layer-1 slices in flight (producer register sets)
+#ifndef DL_L1_RING
+#define DL_L1_RING 3
+#endif
+// layer-1 slices in flight (producer register sets): with the loop-head waits counted, three
+// measured best (c3 3881-3891 steps/s against 3830-3868 for four, 3808-3818 for six; two noisy,
+// profiles/r14/l1ring*)
+constexpr int L1_RING = DL_L1_RING;
 constexpr int L1P_BYTES = 160 * BK * 2;           // 10240 per plane
 __device__ __forceinline__ uint32_t l1_wofs(int n, int k) {   // byte offset in a plane
     return (uint32_t)(n * 64 + ((((k >> 3) ^ (n >> 2)) & 3) << 4) + (k & 7) * 2);

@@ -335,6 +335,9 @@ struct RowSlice4 {
 // measured best (c3 3881-3891 steps/s against 3830-3868 for four, 3808-3818 for six; two noisy,
 // profiles/r14/l1ring*)
 constexpr int L1_RING = DL_L1_RING;
+#ifndef DL_L1_TILING
+#define DL_L1_TILING 1   // layer-1 MFMA waves: 2 M-tiles x 5 N-tiles each (0: 1 x 10)
+#endif
 constexpr int L1P_BYTES = 160 * BK * 2;           // 10240 per plane
 __device__ __forceinline__ uint32_t l1_wofs(int n, int k) {   // byte offset in a plane
     return (uint32_t)(n * 64 + ((((k >> 3) ^ (n >> 2)) & 3) << 4) + (k & 7) * 2);
@@ -854,30 +857,43 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
                 }
             }
         } else {
-            // wave c: M-tile c (rows 16c..16c+15) x all ten 16-column N-tiles
-            f32x4 acc[10], sml[10];
+            // wave c: M-tiles 2 (c & 1), 2 (c & 1) + 1 x N-tiles 5 (c >> 1) .. + 4, so a wave reads
+            // 2 A and 5 B fragments (x 3 planes) a slice instead of 1 and 10: the four MFMA waves'
+            // LDS reads drop from 132 to 84 KB a slice for the same 60 MFMAs each.  Every tile's
+            // products and their order are unchanged.
+            constexpr int MT = DL_L1_TILING ? 2 : 1, NT = 10 / MT;
+            const int m0 = DL_L1_TILING ? 2 * (wave & 1) : wave, n0 = DL_L1_TILING ? NT * (wave >> 1) : 0;
+            f32x4 acc[MT][NT], sml[MT][NT];
 #pragma unroll
-            for (int t = 0; t < 10; ++t) acc[t] = sml[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-            float bv[10];
+            for (int mi = 0; mi < MT; ++mi)
 #pragma unroll
-            for (int t = 0; t < 10; ++t) {
-                const int n = 16 * t + (lane & 15);
+                for (int t = 0; t < NT; ++t) acc[mi][t] = sml[mi][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+            float bv[NT];
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                const int n = 16 * (n0 + t) + (lane & 15);
                 bv[t] = n < dh ? *Xr.at(o_b1 + n) : 0.f;
             }
-            const int m = wave * 16 + (lane & 15), hq = lane >> 4;
+            const int hq = lane >> 4;
             auto compute = [&](const char *img) {
-                const uint32_t oa = l1_wofs(m, 8 * hq);
-                const bf16x8 ah = *reinterpret_cast<const bf16x8 *>(img + oa);
-                const bf16x8 am = *reinterpret_cast<const bf16x8 *>(img + XPL + oa);
-                const bf16x8 al = *reinterpret_cast<const bf16x8 *>(img + 2 * XPL + oa);
+                bf16x8 ah[MT], am[MT], al[MT];
+#pragma unroll
+                for (int mi = 0; mi < MT; ++mi) {
+                    const uint32_t oa = l1_wofs(16 * (m0 + mi) + (lane & 15), 8 * hq);
+                    ah[mi] = *reinterpret_cast<const bf16x8 *>(img + oa);
+                    am[mi] = *reinterpret_cast<const bf16x8 *>(img + XPL + oa);
+                    al[mi] = *reinterpret_cast<const bf16x8 *>(img + 2 * XPL + oa);
+                }
                 const char *wpl = img + 3 * XPL;
 #pragma unroll
-                for (int t = 0; t < 10; ++t) {
-                    const uint32_t ob = l1_wofs(16 * t + (lane & 15), 8 * hq);
+                for (int t = 0; t < NT; ++t) {
+                    const uint32_t ob = l1_wofs(16 * (n0 + t) + (lane & 15), 8 * hq);
                     const bf16x8 bh = *reinterpret_cast<const bf16x8 *>(wpl + ob);
                     const bf16x8 bm = *reinterpret_cast<const bf16x8 *>(wpl + L1P_BYTES + ob);
                     const bf16x8 bl = *reinterpret_cast<const bf16x8 *>(wpl + 2 * L1P_BYTES + ob);
-                    mfma_x6(ah, am, al, bh, bm, bl, acc[t], sml[t]);
+#pragma unroll
+                    for (int mi = 0; mi < MT; ++mi)
+                        mfma_x6(ah[mi], am[mi], al[mi], bh, bm, bl, acc[mi][t], sml[mi][t]);
                 }
             };
             for (int sl = 0; sl < ns; ++sl) {
@@ -886,14 +902,16 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
             }
             compute(img0 + ((ns - 1) & 1) * IMGB);
 #pragma unroll
-            for (int t = 0; t < 10; ++t) {
-                acc[t] += sml[t];
+            for (int mi = 0; mi < MT; ++mi)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int row = wave * 16 + 4 * hq + r, n = 16 * t + (lane & 15);
-                    if (n < dh) H1[row * LDH + n] = act_fwd(0, acc[t][r] + bv[t]);
+                for (int t = 0; t < NT; ++t) {
+                    acc[mi][t] += sml[mi][t];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int row = 16 * (m0 + mi) + 4 * hq + r, n = 16 * (n0 + t) + (lane & 15);
+                        if (n < dh) H1[row * LDH + n] = act_fwd(0, acc[mi][t][r] + bv[t]);
+                    }
                 }
-            }
         }
         load_all_w(w5, mat(Xr, o_w2, dh), dh);   // layer 2's weights
         __syncthreads();   // every consumer is done with the images before H2/H3 are written

@@ -93,3 +93,17 @@ def test_halo_pack_stores_non_temporally(code_objects):
     asm = _disasm(code_objects, r"_ZN2dl12_GLOBAL__N_122step_rows_tiled_kernel\S*liii")
     stores = re.findall(r"(?:global|buffer)_store_dwordx4[^\n]*", asm)
     assert stores and all(re.search(r"\bnt\b", s) for s in stores)
+
+
+def test_mlp_layer1_ring_waits_are_counted(code_objects):
+    """The c3 gradient kernel's layer-1 producer keeps three slices' loads in flight (7 float4
+    loads a slice per producer lane); the waits before a slice's LDS stores must count the two
+    younger sets' loads: vmcnt(20) down to vmcnt(14), at the ring's loop head too.  When the
+    scheduler interleaved the first sets' loads, the loop-head wait became vmcnt(0) and drained
+    the ring every few slices (fixed: c3 +0.5-1 %, profiles/r14/l1order)."""
+    asm = _disasm(code_objects,
+                  r"_ZN2dl12_GLOBAL__N_116mlp_fused_kernelILb0ELb1ELb0ELb0EEEvNS0_7MlpArgsE")
+    waits = [int(x) for x in re.findall(r"s_waitcnt\s+vmcnt\((\d+)\)", asm)]
+    ring = list(range(20, 13, -1))
+    runs = sum(waits[i:i + 7] == ring for i in range(len(waits)))
+    assert runs >= 3, (runs, waits[:60])   # one per register set of the unrolled ring

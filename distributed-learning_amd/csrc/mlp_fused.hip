@@ -965,9 +965,11 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
         w4v[i] = (e < 16 * LDW4 && n < dout && k < dh) ? *Xr.at(o_w4 + n * dh + k) : 0.f;
     }
     const float b4v = (lane & 15) < dout ? *Xr.at(o_b4 + (lane & 15)) : 0.f;
-    int lab[MB / 8];
+    // this lane's two rows of the cross-entropy head (row wave + 8 i, i = 4 pass + lane / 16)
+    int lab2[2];
 #pragma unroll
-    for (int i = 0; i < MB / 8; ++i) lab[i] = p.labels[(int64_t)a * p.s_lab + wave + 8 * i];
+    for (int ps = 0; ps < 2; ++ps)
+        lab2[ps] = p.labels[(int64_t)a * p.s_lab + wave + 8 * (4 * ps + (lane >> 4))];
     forward_hidden_all<L1X6>(mat(Xr, o_b3, 0), dh, H2, H3, stage, 2, w5, [&](int sl) {
         if (sl == NSL - 1) ta.load(mat(Xr, o_w4, dh), dh, dout, 0);   // dZ3's W4^T (dout <= 16)
     });
@@ -996,22 +998,31 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
     }
     __syncthreads();
     // ---- cross-entropy head (torch.nn.CrossEntropyLoss, mean): dZ4 = (softmax - onehot) / 64
+    // Four rows per pass, one per 16-lane group (lane & 15 = the class, dout <= 16): the max and
+    // sum butterflies need 4 exchange steps instead of 6, over 2 passes instead of 8 rows one
+    // at a time.  The same bits: the 64-lane butterfly's first two steps only combined each
+    // value with -inf / +0 from lanes >= dout.  The per-row loss terms go back to lane 0 and are
+    // summed in row order, as before.
     {
+        const int g = lane >> 4, c = lane & 15;
+        float tq[2];
+#pragma unroll
+        for (int ps = 0; ps < 2; ++ps) {
+            const int m = wave + 8 * (4 * ps + g);
+            const float v = c < dout ? Zs[m * LDZ + c] : 0.f;
+            float mx = c < dout ? v : -INFINITY;
+            for (int s = 8; s >= 1; s >>= 1) mx = fmaxf(mx, __shfl_xor(mx, s));
+            const float e = c < dout ? expf(v - mx) : 0.f;
+            float sum = e;
+            for (int s = 8; s >= 1; s >>= 1) sum += __shfl_xor(sum, s);
+            const int label = lab2[ps];
+            const float zl = __shfl(v, 16 * g + label);
+            if (c < dout) Zs[m * LDZ + c] = (e / sum - (c == label ? 1.f : 0.f)) / (float)MB;
+            tq[ps] = (logf(sum) + mx - zl) / (float)MB;
+        }
         float lsum = 0.f;
 #pragma unroll
-        for (int i = 0; i < MB / 8; ++i) {
-            const int m = wave + 8 * i;
-            const float v = lane < dout ? Zs[m * LDZ + lane] : 0.f;
-            float mx = lane < dout ? v : -INFINITY;
-            for (int s = 32; s >= 1; s >>= 1) mx = fmaxf(mx, __shfl_xor(mx, s));
-            const float e = lane < dout ? expf(v - mx) : 0.f;
-            float sum = e;
-            for (int s = 32; s >= 1; s >>= 1) sum += __shfl_xor(sum, s);
-            const int label = lab[i];
-            const float zl = __shfl(v, label);
-            if (lane < dout) Zs[m * LDZ + lane] = (e / sum - (lane == label ? 1.f : 0.f)) / (float)MB;
-            lsum += (logf(sum) + mx - zl) / (float)MB;
-        }
+        for (int i = 0; i < MB / 8; ++i) lsum += __shfl(tq[i / 4], 16 * (i % 4));
         if (lane == 0) lpart[wave] = lsum;
     }
     __syncthreads();

@@ -335,6 +335,9 @@ struct RowSlice4 {
 // measured best (c3 3881-3891 steps/s against 3830-3868 for four, 3808-3818 for six; two noisy,
 // profiles/r14/l1ring*)
 constexpr int L1_RING = DL_L1_RING;
+#ifndef DL_DW_QUAD
+#define DL_DW_QUAD 1   // hidden dW phases: the 25th 32 x 32 tile as four 16 x 16 quadrants
+#endif
 #ifndef DL_L1_TILING
 #define DL_L1_TILING 1   // layer-1 MFMA waves: 2 M-tiles x 5 N-tiles each (0: 1 x 10)
 #endif
@@ -686,7 +689,11 @@ __device__ __forceinline__ void weight_grad_hidden(const float *dZ, const float 
                                                    const M &gW, const M &gb,
                                                    const GOut<STEP> &o) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    for (int t = wave; t < 25; t += 8) {    // one tile at a time (one accumulator)
+    // tiles 0..23 three per wave; the 25th (rows and columns 128..159) as four 16 x 16 quadrants
+    // on waves 4..7 -- one per SIMD -- instead of a fourth whole tile on wave 0, whose SIMD then
+    // ran seven tiles against six (DL_DW_QUAD=0: the whole tile)
+    constexpr int NT = DL_DW_QUAD ? 24 : 25;
+    for (int t = wave; t < NT; t += 8) {    // one tile at a time (one accumulator)
         f32x16 acc, xo;
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[r] = 0.f;
@@ -698,6 +705,22 @@ __device__ __forceinline__ void weight_grad_hidden(const float *dZ, const float 
             acc = mfma32(dZ[b * LDH + ia], Hin[b * LDH + jb], acc);
         }
         store_tile(acc, xo, (t / 5) * 32 + 4 * (lane >> 5), jb, gW, dh, dh, gb, o);
+    }
+    if (DL_DW_QUAD && wave >= 4 && dh > 128) {
+        const int q = wave - 4, i0 = 128 + 16 * (q >> 1), j0 = 128 + 16 * (q & 1);
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < MB / 4; ++ks) {
+            const int b = 4 * ks + (lane >> 4);
+            acc = mfma4(dZ[b * LDH + i0 + (lane & 15)], Hin[b * LDH + j0 + (lane & 15)], acc);
+        }
+        const int j = j0 + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = i0 + 4 * (lane >> 4) + r;
+            if (i < dh && j < dh) o.put(gW.at(i, j), acc[r]);
+            if (i < dh && j == dh) o.put(gb.at(0, i), acc[r]);   // Hin's ones column: the bias
+        }
     }
 }
 

@@ -1111,7 +1111,15 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
         static_assert(3 * AP <= 2 * H_FLOATS * 4, "dZ1^T planes fit the H2/H3 space");
         static_assert(3 * XP <= H_FLOATS * 4, "x chunk planes fit H1");
         char *aplanes = reinterpret_cast<char *>(H2);
-        char *xplanes = reinterpret_cast<char *>(H1);
+        // x chunk planes, double-buffered so a chunk's planes go in while the previous chunk's
+        // tiles run (one barrier a chunk): even chunks in H1, odd ones in the staging area (two
+        // planes) and the H2/H3 space past the dZ1^T planes (the third)
+        static_assert(2 * XP <= STAGE_FLOATS * 4 && 3 * AP + XP <= 2 * H_FLOATS * 4,
+                      "the second x plane buffer fits the staging area and the H2/H3 tail");
+        char *xbuf[2][3] = {{reinterpret_cast<char *>(H1), reinterpret_cast<char *>(H1) + XP,
+                             reinterpret_cast<char *>(H1) + 2 * XP},
+                            {reinterpret_cast<char *>(stage), reinterpret_cast<char *>(stage) + XP,
+                             aplanes + 3 * AP}};
         auto tofs = [](int r, int b) {   // byte offset of (row r, batch b) in a transposed plane
             return (uint32_t)(r * ROWB + ((((b >> 3) ^ (r >> 1)) & 7) << 4) + (b & 7) * 2);
         };
@@ -1161,7 +1169,10 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
         const int nc = (din + CW) / CW;          // through column din (the ones column)
         const PM gw1 = mat(Gr, o_w1, din), gb1 = mat(Gr, o_b1, 0);
         const int r = lane & 31, hh = lane >> 5;
-        auto chunk = [&](int ci, f32x4 (&xv)[4]) {
+        // (the barrier after a chunk's planes also orders the previous chunk's tiles, all waves,
+        // before the planes of the chunk after it overwrite that buffer)
+        auto chunk = [&](int ci, f32x4 (&xv)[4], int odd) {
+            char *const *xp = xbuf[odd];
             if (xt) {
                 // column din is the ones column (db1); din % 4 == 0 puts it at a float4 start
                 const int c = ci * CW + xc;
@@ -1170,7 +1181,15 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
                 for (int i = 0; i < 4; ++i)
                     v[i] = c < din ? xv[i]
                            : c == din ? f32x4{1.f, 0.f, 0.f, 0.f} : f32x4{0.f, 0.f, 0.f, 0.f};
-                split_store(v, xb0, xc, xplanes, XP);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    bf16x4 h, m, l;
+                    split4(f32x4{v[0][j], v[1][j], v[2][j], v[3][j]}, h, m, l);
+                    const uint32_t o = tofs(xc + j, xb0);
+                    *reinterpret_cast<bf16x4 *>(xp[0] + o) = h;
+                    *reinterpret_cast<bf16x4 *>(xp[1] + o) = m;
+                    *reinterpret_cast<bf16x4 *>(xp[2] + o) = l;
+                }
             }
             __syncthreads();
             const int c0 = ci * CW;
@@ -1190,21 +1209,20 @@ __global__ void __launch_bounds__(NTHR) mlp_fused_kernel(MlpArgs p) {
                     const bf16x8 ah = *reinterpret_cast<const bf16x8 *>(aplanes + oa);
                     const bf16x8 am = *reinterpret_cast<const bf16x8 *>(aplanes + AP + oa);
                     const bf16x8 al = *reinterpret_cast<const bf16x8 *>(aplanes + 2 * AP + oa);
-                    const bf16x8 bh = *reinterpret_cast<const bf16x8 *>(xplanes + ob);
-                    const bf16x8 bm = *reinterpret_cast<const bf16x8 *>(xplanes + XP + ob);
-                    const bf16x8 bl = *reinterpret_cast<const bf16x8 *>(xplanes + 2 * XP + ob);
+                    const bf16x8 bh = *reinterpret_cast<const bf16x8 *>(xp[0] + ob);
+                    const bf16x8 bm = *reinterpret_cast<const bf16x8 *>(xp[1] + ob);
+                    const bf16x8 bl = *reinterpret_cast<const bf16x8 *>(xp[2] + ob);
                     mfma32_x6(ah, am, al, bh, bm, bl, big, sml);
                 }
                 big += sml;
                 store_tile(big, xo, 32 * t + 4 * hh, c0 + 32 * nt + r, gw1, dh, din, gb1, go);
             }
-            __syncthreads();
         };
         // chunks in pairs, the second of the last pair run even past nc (no tiles then: ntc <= 0),
         // so the loads and waits are the same straight-line code every pair
         for (int ci = 0; ci < nc; ci += 2) {
-            chunk(ci, xva);
-            chunk(ci + 1, xvb);
+            chunk(ci, xva, 0);
+            chunk(ci + 1, xvb, 1);
         }
     } else {
     // fp32: dW1 by 256-column chunks of x, staged in the H2/H3 space (free now: dZ2 and dZ3

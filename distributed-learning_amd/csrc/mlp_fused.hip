@@ -390,7 +390,9 @@ __device__ __forceinline__ float act_grad(int layer, float h) {
 // wave w owns M-tile (w & 3) and the five N-tiles 5 * (w >> 2) + t.  acc = sum_k A(m,k) B(n,k)
 // with A(m, k) = Alds[m * lda + k] and B(n, k) = Blds[n * LDS1 + k] (staged [n][k] slice) or
 // Blds[k * LDT + n] (staged [k][n] slice).
-template <bool B_KMAJOR>
+// KS k-steps of 4 (BK / 4: a whole slice; dZ3's K = dout <= 16 needs 4: the slice's rows from
+// dout on are zero, exact-zero products, left out)
+template <bool B_KMAJOR, int KS = BK / 4>
 __device__ __forceinline__ void mma_rows64(f32x4 (&acc)[5], const float *A, int lda,
                                            const float *Bs) {
     // a whole BK slice, software-pipelined: the fragments of k-step s + 1 are read while the
@@ -412,8 +414,8 @@ __device__ __forceinline__ void mma_rows64(f32x4 (&acc)[5], const float *A, int 
     };
     read(0, 0);
 #pragma unroll
-    for (int s = 0; s < BK / 4; ++s) {
-        if (s + 1 < BK / 4) read(s + 1, (s + 1) & 1);
+    for (int s = 0; s < KS; ++s) {
+        if (s + 1 < KS) read(s + 1, (s + 1) & 1);
 #pragma unroll
         for (int t = 0; t < 5; ++t) acc[t] = mfma4(a[s & 1], b[s & 1][t], acc[t]);
     }
@@ -668,7 +670,7 @@ __device__ __forceinline__ void backward_dz_one(int dh, const float *dZ, int ldz
     zero(acc);
     A.store(stage);
     __syncthreads();
-    mma_rows64<true>(acc, dZ, ldz, stage);
+    mma_rows64<true, 4>(acc, dZ, ldz, stage);   // K = dout <= 16
     __syncthreads();
     next();
     epi_rows64(acc, [&](int m, int n, float v) {

@@ -80,12 +80,33 @@ __device__ __forceinline__ f32x4 mfma_bf(const bf16x8 &a, const bf16x8 &b, f32x4
 }
 
 // split two floats into their (h, m, l) bf16 pairs (v_cvt_pk_bf16_f32, round to nearest even)
+#ifndef DL_SPLIT_PK
+#define DL_SPLIT_PK 1
+#endif
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+#if DL_SPLIT_PK
+// both lanes of a pair at once: one packed conversion per plane, the bf16 pair widened back to
+// fp32 by two bit operations, the remainders by one packed subtraction (exact: x - bf16(x) is
+// representable), 9 VALU instructions per pair instead of 17 element-wise ones
+__device__ __forceinline__ f32x2 widen2(bf16x2 v) {
+    const uint32_t u = __builtin_bit_cast(uint32_t, v);
+    return f32x2{__builtin_bit_cast(float, u << 16), __builtin_bit_cast(float, u & 0xffff0000u)};
+}
+__device__ __forceinline__ void split2(float x0, float x1, bf16x2 &h, bf16x2 &m, bf16x2 &l) {
+    const f32x2 x = {x0, x1};
+    h = __builtin_convertvector(x, bf16x2);
+    const f32x2 r = x - widen2(h);
+    m = __builtin_convertvector(r, bf16x2);
+    l = __builtin_convertvector(r - widen2(m), bf16x2);
+}
+#else
 __device__ __forceinline__ void split2(float x0, float x1, bf16x2 &h, bf16x2 &m, bf16x2 &l) {
     h = bf16x2{(__bf16)x0, (__bf16)x1};
     const float r0 = x0 - (float)h[0], r1 = x1 - (float)h[1];
     m = bf16x2{(__bf16)r0, (__bf16)r1};
     l = bf16x2{(__bf16)(r0 - (float)m[0]), (__bf16)(r1 - (float)m[1])};
 }
+#endif
 
 __device__ __forceinline__ void split4(const f32x4 &x, bf16x4 &h, bf16x4 &m, bf16x4 &l) {
     bf16x2 h0, m0, l0, h1, m1, l1;

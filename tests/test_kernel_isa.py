@@ -107,3 +107,15 @@ def test_mlp_layer1_ring_waits_are_counted(code_objects):
     ring = list(range(20, 13, -1))
     runs = sum(waits[i:i + 7] == ring for i in range(len(waits)))
     assert runs >= 3, (runs, waits[:60])   # one per register set of the unrolled ring
+
+
+def test_mlp_bf16_split_is_packed(code_objects):
+    """The exact three-way bf16 split of the c3 gradient kernel converts pairs: one
+    v_cvt_pk_bf16_f32 per plane and pair, the remainders by v_pk_add_f32.  Element-wise, the same
+    kernel had 1722 conversions and 62 packed adds; packed, 738 and 408 (c3 +1.1 %, bit-identical,
+    profiles/r14/splitpk).  A regression to per-element conversions shows as the count jumping."""
+    asm = _disasm(code_objects,
+                  r"_ZN2dl12_GLOBAL__N_116mlp_fused_kernelILb0ELb1ELb0ELb0EEEvNS0_7MlpArgsE")
+    cvt = len(re.findall(r"v_cvt_pk_bf16_f32", asm))
+    pk_add = len(re.findall(r"v_pk_add_f32", asm))
+    assert 0 < cvt <= 1000 and pk_add >= 300, (cvt, pk_add)
